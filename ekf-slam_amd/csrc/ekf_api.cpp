@@ -1,0 +1,687 @@
+// Host runtime behind include/ekf.h: device memory, the handle's HIP stream, message staging and
+// the launch sequence for the reference's two callbacks (nuslam/src/slam.cpp:180-316, :318-530).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "ekf.h"
+#include "ekf_device.hpp"
+#include "ekf_launch.hpp"
+#include "geom.hpp"
+
+using namespace ekfslam;
+
+namespace {
+
+constexpr int kRing = 16;  // pinned staging slots (host may run this many uploads ahead)
+
+struct Marker {
+  int id;
+  double zr, zb;
+};
+
+struct ProfEvents {
+  std::vector<hipEvent_t> start, stop;
+};
+
+}  // namespace
+
+struct ekf_ctx {
+  ekf_config cfg{};
+  int n = 0, ld = 0, ldk = 0, F = 0;
+  size_t w = 8;
+  hipStream_t stream = nullptr;
+  void* sig[2] = {nullptr, nullptr};
+  double* x[2] = {nullptr, nullptr};
+  void* kcat = nullptr;
+  void* mcat = nullptr;
+  FilterCtl* ctl = nullptr;
+  MsgDesc* ddesc = nullptr;
+  size_t sig_stride = 0, x_stride = 0, km_stride = 0;
+  size_t desc_cap = 0;  // descriptors per upload
+  // host mirror
+  std::vector<Pose2> odom;
+  std::vector<int> parity;
+  std::vector<char> pending;
+  // staging ring
+  MsgDesc* pinned = nullptr;
+  int ring_next = 0;
+  hipEvent_t ring_ev[kRing] = {};
+  bool ring_used[kRing] = {};
+  // scratch
+  std::vector<std::vector<Marker>> msgs;
+  // profiling
+  bool prof = false;
+  ProfEvents pe[3];
+  std::vector<hipEvent_t> pool;
+  long long prof_launches[3] = {0, 0, 0};
+  double prof_ms[3] = {0, 0, 0};
+};
+
+#define HIPCHK(expr)                       \
+  do {                                     \
+    if ((expr) != hipSuccess) return EKF_E_HIP; \
+  } while (0)
+
+namespace {
+
+template <typename T>
+PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
+  PassArgs<T> a{};
+  a.sig[0] = static_cast<T*>(h->sig[0]);
+  a.sig[1] = static_cast<T*>(h->sig[1]);
+  a.sig_stride = h->sig_stride;
+  a.x[0] = h->x[0];
+  a.x[1] = h->x[1];
+  a.x_stride = h->x_stride;
+  a.kcat = static_cast<T*>(h->kcat);
+  a.mcat = static_cast<T*>(h->mcat);
+  a.km_stride = h->km_stride;
+  a.ldk = h->ldk;
+  a.ctl = h->ctl;
+  a.desc = desc;
+  a.n = h->n;
+  a.ld = h->ld;
+  a.N = h->cfg.n_landmarks;
+  a.f0 = f0;
+  a.q = h->cfg.q_noise;
+  a.r = h->cfg.r_noise;
+  a.gate = h->cfg.mah_gate;
+  return a;
+}
+
+hipEvent_t pool_get(ekf_ctx* h) {
+  if (!h->pool.empty()) {
+    hipEvent_t e = h->pool.back();
+    h->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Launch `fn` bracketed by events when profiling (kind 0 = Σ pass, 1 = gain, 2 = association).
+template <typename Fn>
+int timed(ekf_ctx* h, int kind, Fn fn) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (h->prof) {
+    a = pool_get(h);
+    b = pool_get(h);
+    if (a) hipEventRecord(a, h->stream);
+  }
+  const hipError_t e = fn();
+  if (h->prof && a && b) {
+    hipEventRecord(b, h->stream);
+    h->pe[kind].start.push_back(a);
+    h->pe[kind].stop.push_back(b);
+  }
+  return e == hipSuccess ? EKF_OK : EKF_E_HIP;
+}
+
+// Reserve `count` descriptors in the next pinned staging slot.
+MsgDesc* stage(ekf_ctx* h, int* slot) {
+  const int s = h->ring_next;
+  h->ring_next = (h->ring_next + 1) % kRing;
+  if (h->ring_used[s]) hipEventSynchronize(h->ring_ev[s]);
+  *slot = s;
+  return h->pinned + static_cast<size_t>(s) * h->desc_cap;
+}
+
+int upload(ekf_ctx* h, int slot, size_t count) {
+  const MsgDesc* src = h->pinned + static_cast<size_t>(slot) * h->desc_cap;
+  HIPCHK(hipMemcpyAsync(h->ddesc, src, count * sizeof(MsgDesc), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipEventRecord(h->ring_ev[slot], h->stream));
+  h->ring_used[slot] = true;
+  return EKF_OK;
+}
+
+void fill_desc(MsgDesc* d, int m, int flags, int parity, const Pose2& odom) {
+  std::memset(d, 0, sizeof(MsgDesc));
+  d->m = m;
+  d->flags = flags;
+  d->parity = parity;
+  d->odom[0] = odom.theta;
+  d->odom[1] = odom.x;
+  d->odom[2] = odom.y;
+}
+
+// slam.cpp:208-210 (host, glibc, as the reference)
+inline void measure(double rx, double ry, double* zr, double* zb) {
+  *zr = std::sqrt(std::pow(rx, 2) + std::pow(ry, 2));
+  *zb = std::atan2(ry, rx);
+}
+
+template <typename T>
+int launch_pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw) {
+  const PassArgs<T> a = args<T>(h, dptr, f0);
+  int rc = timed(h, 1, [&] { return launch_gain<T>(a, nf, h->stream); });
+  if (rc) return rc;
+  return timed(h, 0, [&] { return launch_sigma_pass<T>(a, nf, kw, h->stream); });
+}
+
+int pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw) {
+  return h->cfg.dtype == EKF_F32 ? launch_pair<float>(h, dptr, f0, nf, kw)
+                                 : launch_pair<double>(h, dptr, f0, nf, kw);
+}
+
+int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
+  if (h->cfg.dtype == EKF_F32) {
+    const PassArgs<float> a = args<float>(h, dptr, f0);
+    return timed(h, 2, [&] { return launch_assoc<float>(a, nf, h->stream); });
+  }
+  const PassArgs<double> a = args<double>(h, dptr, f0);
+  return timed(h, 2, [&] { return launch_assoc<double>(a, nf, h->stream); });
+}
+
+// Known association, one message per filter in [f0, f0+nf): msgs[k] holds filter f0+k's markers.
+// Predict + chunks of ≤ kMaxChunk corrections + posterior (slam.cpp:180-316).
+int run_known(ekf_ctx* h, int f0, int nf, bool predict) {
+  int chunks = 1;
+  for (int k = 0; k < nf; ++k)
+    chunks = std::max(chunks, static_cast<int>((h->msgs[k].size() + kMaxChunk - 1) / kMaxChunk));
+  for (int c0 = 0; c0 < chunks;) {
+    const int cn = std::min(chunks - c0, static_cast<int>(h->desc_cap / nf));
+    int slot;
+    MsgDesc* st = stage(h, &slot);
+    std::vector<int> kws(cn, 4);
+    for (int c = 0; c < cn; ++c) {
+      const int chunk = c0 + c;
+      for (int k = 0; k < nf; ++k) {
+        const int f = f0 + k;
+        const auto& mk = h->msgs[k];
+        const int nk = static_cast<int>((mk.size() + kMaxChunk - 1) / kMaxChunk);
+        const int nchunks = std::max(nk, 1);
+        MsgDesc* d = st + static_cast<size_t>(c) * nf + k;
+        if (chunk >= nchunks) {
+          std::memset(d, 0, sizeof(MsgDesc));
+          continue;
+        }
+        const int b = chunk * kMaxChunk;
+        const int m = std::min(kMaxChunk, static_cast<int>(mk.size()) - b);
+        int flags = kActive;
+        if (chunk == 0 && (predict || h->pending[f])) flags |= kFirst;
+        if (chunk == nchunks - 1 && predict) flags |= kLast;
+        fill_desc(d, std::max(m, 0), flags, h->parity[f], h->odom[f]);
+        for (int i = 0; i < m; ++i) {
+          d->ids[i] = mk[b + i].id;
+          d->z[i][0] = mk[b + i].zr;
+          d->z[i][1] = mk[b + i].zb;
+        }
+        h->parity[f] ^= 1;
+        kws[c] = std::max(kws[c], ((2 + 2 * std::max(m, 0) + 3) / 4) * 4);
+        if (chunk == 0) h->pending[f] = 0;
+      }
+    }
+    int rc = upload(h, slot, static_cast<size_t>(cn) * nf);
+    if (rc) return rc;
+    for (int c = 0; c < cn; ++c) {
+      rc = pair(h, h->ddesc + static_cast<size_t>(c) * nf, f0, nf, kws[c]);
+      if (rc) return rc;
+    }
+    c0 += cn;
+  }
+  return EKF_OK;
+}
+
+// Unknown association (slam.cpp:318-530): markers one at a time, each = association kernel +
+// single-marker launch pair. Decisions land in FilterCtl::assoc_j/new; read back when requested.
+int run_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int m_max, int* j_out,
+              int* new_out) {
+  int mm = 0;
+  for (int k = 0; k < nf; ++k) mm = std::max(mm, static_cast<int>(h->msgs[k].size()));
+  const int steps = std::max(mm, 1);
+  const int per_upload = std::max(1, std::min(kMaxAssoc, static_cast<int>(h->desc_cap / nf)));
+  for (int i0 = 0; i0 < steps; i0 += per_upload) {
+    const int cn = std::min(per_upload, steps - i0);
+    int slot;
+    MsgDesc* st = stage(h, &slot);
+    for (int c = 0; c < cn; ++c) {
+      const int i = i0 + c;
+      for (int k = 0; k < nf; ++k) {
+        const int f = f0 + k;
+        const auto& mk = h->msgs[k];
+        const int mf = static_cast<int>(mk.size());
+        MsgDesc* d = st + static_cast<size_t>(c) * nf + k;
+        const bool active = i < std::max(mf, 1);
+        if (!active) {
+          std::memset(d, 0, sizeof(MsgDesc));
+          continue;
+        }
+        int flags = kActive | kNoInit;
+        if (i == 0 && (predict || h->pending[f])) flags |= kFirst;
+        if (i == std::max(mf, 1) - 1 && posterior) flags |= kLast;
+        const int m = mf > 0 ? 1 : 0;
+        fill_desc(d, m, flags, h->parity[f], h->odom[f]);
+        d->assoc_slot = c;
+        if (m) {
+          d->ids[0] = -1;
+          d->z[0][0] = mk[i].zr;
+          d->z[0][1] = mk[i].zb;
+        }
+        h->parity[f] ^= 1;
+        if (i == 0) h->pending[f] = 0;
+      }
+    }
+    int rc = upload(h, slot, static_cast<size_t>(cn) * nf);
+    if (rc) return rc;
+    for (int c = 0; c < cn; ++c) {
+      const MsgDesc* dp = h->ddesc + static_cast<size_t>(c) * nf;
+      rc = assoc(h, dp, f0, nf);
+      if (rc) return rc;
+      rc = pair(h, dp, f0, nf, 4);
+      if (rc) return rc;
+    }
+    if (j_out || new_out) {
+      HIPCHK(hipStreamSynchronize(h->stream));
+      for (int k = 0; k < nf; ++k) {
+        FilterCtl c;
+        HIPCHK(hipMemcpy(&c, h->ctl + f0 + k, sizeof(FilterCtl), hipMemcpyDeviceToHost));
+        const int mf = static_cast<int>(h->msgs[k].size());
+        for (int c2 = 0; c2 < cn; ++c2) {
+          const int i = i0 + c2;
+          if (i >= mf) continue;
+          if (j_out) j_out[static_cast<size_t>(k) * m_max + i] = c.assoc_j[c2];
+          if (new_out) new_out[static_cast<size_t>(k) * m_max + i] = c.assoc_new[c2];
+        }
+      }
+    }
+  }
+  return EKF_OK;
+}
+
+bool valid(ekf_ctx* h, int f) { return h && f >= 0 && f < h->F; }
+
+}  // namespace
+
+extern "C" {
+
+void ekf_config_default(ekf_config* c) {
+  if (!c) return;
+  c->n_landmarks = 50;
+  c->n_filters = 1;
+  c->dtype = EKF_F64;
+  c->q_noise = 1.0e-2;
+  c->r_noise = 1.0e-2;
+  c->init_var = 10e6;
+  c->mah_gate = 2.0;
+  c->device = 0;
+}
+
+const char* ekf_strerror(int s) {
+  switch (s) {
+    case EKF_OK: return "ok";
+    case EKF_E_ARG: return "invalid argument";
+    case EKF_E_RANGE: return "landmark index out of range / landmark capacity exhausted";
+    case EKF_E_EMPTY: return "empty marker array";
+    case EKF_E_NUMERIC: return "singular or non-finite innovation covariance";
+    case EKF_E_HIP: return "HIP runtime error";
+    case EKF_E_NOMEM: return "out of memory";
+    default: return "unknown status";
+  }
+}
+
+int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
+  if (!out) return EKF_E_ARG;
+  *out = nullptr;
+  ekf_config cfg;
+  ekf_config_default(&cfg);
+  if (cfg_in) cfg = *cfg_in;
+  if (cfg.n_landmarks < 1 || cfg.n_filters < 1 || (cfg.dtype != EKF_F64 && cfg.dtype != EKF_F32))
+    return EKF_E_ARG;
+  ekf_ctx* h = new (std::nothrow) ekf_ctx;
+  if (!h) return EKF_E_NOMEM;
+  h->cfg = cfg;
+  h->F = cfg.n_filters;
+  h->n = 3 + 2 * cfg.n_landmarks;
+  h->w = cfg.dtype == EKF_F32 ? 4 : 8;
+  const int per_line = static_cast<int>(128 / h->w);
+  h->ld = (h->n + per_line - 1) / per_line * per_line;
+  h->ldk = (h->n + 63) / 64 * 64;
+  h->sig_stride = static_cast<size_t>(h->n) * h->ld;
+  h->x_stride = static_cast<size_t>((h->n + 15) / 16 * 16);
+  h->km_stride = static_cast<size_t>(kMaxKW) * h->ldk;
+  h->desc_cap = static_cast<size_t>(h->F) * kMaxAssoc;
+  h->odom.assign(h->F, Pose2{});
+  h->parity.assign(h->F, 0);
+  h->pending.assign(h->F, 0);
+  h->msgs.resize(h->F);
+  auto fail = [&](int rc) {
+    ekf_destroy(h);
+    return rc;
+  };
+  if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(EKF_E_HIP);
+  const size_t sig_bytes = h->sig_stride * h->F * h->w;
+  for (int p = 0; p < 2; ++p) {
+    if (hipMalloc(&h->sig[p], sig_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
+    if (hipMalloc(&h->x[p], h->x_stride * h->F * sizeof(double)) != hipSuccess)
+      return fail(EKF_E_NOMEM);
+  }
+  const size_t km_bytes = h->km_stride * h->F * h->w;
+  if (hipMalloc(&h->kcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
+  if (hipMalloc(&h->mcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
+  if (hipMalloc(&h->ctl, sizeof(FilterCtl) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
+  if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->desc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->pinned), sizeof(MsgDesc) * h->desc_cap * kRing,
+                    hipHostMallocDefault) != hipSuccess)
+    return fail(EKF_E_NOMEM);
+  for (int i = 0; i < kRing; ++i)
+    if (hipEventCreateWithFlags(&h->ring_ev[i], hipEventDisableTiming) != hipSuccess)
+      return fail(EKF_E_HIP);
+  // Σ₀ = diag(0,0,0, init_var·I_2N), state = 0 (slam.cpp:127-132, :674)
+  for (int p = 0; p < 2; ++p) {
+    if (hipMemsetAsync(h->sig[p], 0, sig_bytes, h->stream) != hipSuccess) return fail(EKF_E_HIP);
+    if (hipMemsetAsync(h->x[p], 0, h->x_stride * h->F * sizeof(double), h->stream) != hipSuccess)
+      return fail(EKF_E_HIP);
+  }
+  if (hipMemsetAsync(h->kcat, 0, km_bytes, h->stream) != hipSuccess ||
+      hipMemsetAsync(h->mcat, 0, km_bytes, h->stream) != hipSuccess ||
+      hipMemsetAsync(h->ctl, 0, sizeof(FilterCtl) * h->F, h->stream) != hipSuccess)
+    return fail(EKF_E_HIP);
+  hipError_t e = cfg.dtype == EKF_F32
+                     ? launch_init_diag<float>(static_cast<float*>(h->sig[0]), h->sig_stride, h->n,
+                                               h->ld, cfg.init_var, h->F, h->stream)
+                     : launch_init_diag<double>(static_cast<double*>(h->sig[0]), h->sig_stride,
+                                                h->n, h->ld, cfg.init_var, h->F, h->stream);
+  if (e != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess) return fail(EKF_E_HIP);
+  *out = h;
+  return EKF_OK;
+}
+
+int ekf_destroy(ekf_t h) {
+  if (!h) return EKF_E_ARG;
+  hipSetDevice(h->cfg.device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (int p = 0; p < 2; ++p) {
+    if (h->sig[p]) hipFree(h->sig[p]);
+    if (h->x[p]) hipFree(h->x[p]);
+  }
+  if (h->kcat) hipFree(h->kcat);
+  if (h->mcat) hipFree(h->mcat);
+  if (h->ctl) hipFree(h->ctl);
+  if (h->ddesc) hipFree(h->ddesc);
+  if (h->pinned) hipHostFree(h->pinned);
+  for (int i = 0; i < kRing; ++i)
+    if (h->ring_ev[i]) hipEventDestroy(h->ring_ev[i]);
+  for (auto& pe : h->pe) {
+    for (auto e : pe.start) hipEventDestroy(e);
+    for (auto e : pe.stop) hipEventDestroy(e);
+  }
+  for (auto e : h->pool) hipEventDestroy(e);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return EKF_OK;
+}
+
+int ekf_dims(ekf_t h, int* n, int* ld, int* nf) {
+  if (!h) return EKF_E_ARG;
+  if (n) *n = h->n;
+  if (ld) *ld = h->ld;
+  if (nf) *nf = h->F;
+  return EKF_OK;
+}
+
+int ekf_set_odom(ekf_t h, int f, double theta, double x, double y) {
+  if (!valid(h, f)) return EKF_E_ARG;
+  h->odom[f] = Pose2{theta, x, y};
+  return EKF_OK;
+}
+
+int ekf_fake_sensor(ekf_t h, int f, int m, const int* ids, const int* actions,
+                    const double* rel_xy) {
+  if (!valid(h, f) || m < 0 || (m > 0 && (!ids || !rel_xy))) return EKF_E_ARG;
+  if (m == 0) return EKF_E_EMPTY;
+  auto& mk = h->msgs[0];
+  mk.clear();
+  for (int i = 0; i < m; ++i) {
+    if (actions && actions[i] == EKF_MARKER_DELETE) continue;
+    if (ids[i] < 0 || ids[i] >= h->cfg.n_landmarks) return EKF_E_RANGE;
+    Marker k;
+    k.id = ids[i];
+    measure(rel_xy[2 * i], rel_xy[2 * i + 1], &k.zr, &k.zb);
+    mk.push_back(k);
+  }
+  hipSetDevice(h->cfg.device);
+  return run_known(h, f, 1, true);
+}
+
+int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int* is_new_out) {
+  if (!valid(h, f) || m < 0 || (m > 0 && !rel_xy)) return EKF_E_ARG;
+  if (m == 0) return EKF_E_EMPTY;
+  auto& mk = h->msgs[0];
+  mk.clear();
+  for (int i = 0; i < m; ++i) {
+    Marker k;
+    k.id = -1;
+    measure(rel_xy[2 * i], rel_xy[2 * i + 1], &k.zr, &k.zb);
+    mk.push_back(k);
+  }
+  hipSetDevice(h->cfg.device);
+  const int rc = run_assoc(h, f, 1, true, true, m, assoc_out, is_new_out);
+  if (rc) return rc;
+  if (assoc_out || is_new_out) {
+    unsigned fl = 0;
+    HIPCHK(hipMemcpy(&fl, &h->ctl[f].status, sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (fl & EKF_FLAG_RANGE) return EKF_E_RANGE;
+  }
+  return EKF_OK;
+}
+
+int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, const int* ids,
+                     const int* actions, const double* rel_xy, const double* odom) {
+  if (!h || m_max < 0 || !counts || (m_max > 0 && !rel_xy) || (!assoc_mode && m_max > 0 && !ids))
+    return EKF_E_ARG;
+  for (int f = 0; f < h->F; ++f) {
+    if (odom) h->odom[f] = Pose2{odom[3 * f], odom[3 * f + 1], odom[3 * f + 2]};
+    auto& mk = h->msgs[f];
+    mk.clear();
+    const int c = counts[f];
+    if (c < 0 || c > m_max) return EKF_E_ARG;
+    for (int i = 0; i < c; ++i) {
+      const size_t e = static_cast<size_t>(f) * m_max + i;
+      if (!assoc_mode) {
+        if (actions && actions[e] == EKF_MARKER_DELETE) continue;
+        if (ids[e] < 0 || ids[e] >= h->cfg.n_landmarks) return EKF_E_RANGE;
+      }
+      Marker k;
+      k.id = assoc_mode ? -1 : ids[e];
+      measure(rel_xy[2 * e], rel_xy[2 * e + 1], &k.zr, &k.zb);
+      mk.push_back(k);
+    }
+  }
+  hipSetDevice(h->cfg.device);
+  return assoc_mode ? run_assoc(h, 0, h->F, true, true, m_max, nullptr, nullptr)
+                    : run_known(h, 0, h->F, true);
+}
+
+int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, const int* ids,
+               const int* actions, const double* rel_xy, const double* odom, double* out_pose) {
+  if (!h || T < 0 || !counts || !odom) return EKF_E_ARG;
+  const size_t F = static_cast<size_t>(h->F);
+  for (int t = 0; t < T; ++t) {
+    const size_t o = static_cast<size_t>(t) * F * m_max;
+    const int rc = ekf_batch_sensor(h, assoc_mode, m_max, counts + t * F, ids ? ids + o : nullptr,
+                                    actions ? actions + o : nullptr, rel_xy + 2 * o,
+                                    odom + 3 * F * t);
+    if (rc) return rc;
+    if (out_pose) {
+      HIPCHK(hipStreamSynchronize(h->stream));
+      for (size_t f = 0; f < F; ++f)
+        HIPCHK(hipMemcpy(out_pose + 3 * (F * t + f), h->x[h->parity[f]] + f * h->x_stride,
+                         3 * sizeof(double), hipMemcpyDeviceToHost));
+    }
+  }
+  return EKF_OK;
+}
+
+int ekf_predict(ekf_t h, int f) {
+  if (!valid(h, f)) return EKF_E_ARG;
+  h->pending[f] = 1;
+  return EKF_OK;
+}
+
+int ekf_correct(ekf_t h, int f, int id, double rx, double ry) {
+  if (!valid(h, f)) return EKF_E_ARG;
+  if (id < 0 || id >= h->cfg.n_landmarks) return EKF_E_RANGE;
+  auto& mk = h->msgs[0];
+  mk.clear();
+  Marker k;
+  k.id = id;
+  measure(rx, ry, &k.zr, &k.zb);
+  mk.push_back(k);
+  hipSetDevice(h->cfg.device);
+  return run_known(h, f, 1, false);
+}
+
+int ekf_associate_correct(ekf_t h, int f, double rx, double ry, int* j, int* is_new) {
+  if (!valid(h, f)) return EKF_E_ARG;
+  auto& mk = h->msgs[0];
+  mk.clear();
+  Marker k;
+  k.id = -1;
+  measure(rx, ry, &k.zr, &k.zb);
+  mk.push_back(k);
+  hipSetDevice(h->cfg.device);
+  const int rc = run_assoc(h, f, 1, false, false, 1, j, is_new);
+  if (rc) return rc;
+  if (j && *j < 0) return EKF_E_RANGE;
+  return EKF_OK;
+}
+
+int ekf_posterior(ekf_t h, int f) {
+  if (!valid(h, f)) return EKF_E_ARG;
+  hipSetDevice(h->cfg.device);
+  if (h->pending[f]) {  // fold the pending predict into a zero-marker pass, then the posterior
+    h->msgs[0].clear();
+    return run_known(h, f, 1, true);
+  }
+  int slot;
+  MsgDesc* d = stage(h, &slot);
+  fill_desc(d, 0, kActive, h->parity[f], h->odom[f]);
+  int rc = upload(h, slot, 1);
+  if (rc) return rc;
+  hipError_t e = h->cfg.dtype == EKF_F32
+                     ? launch_posterior<float>(args<float>(h, h->ddesc, f), 1, h->stream)
+                     : launch_posterior<double>(args<double>(h, h->ddesc, f), 1, h->stream);
+  return e == hipSuccess ? EKF_OK : EKF_E_HIP;
+}
+
+int ekf_sync(ekf_t h) {
+  if (!h) return EKF_E_ARG;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return EKF_OK;
+}
+
+int ekf_get_pose(ekf_t h, int f, double* p) {
+  if (!valid(h, f) || !p) return EKF_E_ARG;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(p, h->x[h->parity[f]] + f * h->x_stride, 3 * sizeof(double),
+                   hipMemcpyDeviceToHost));
+  return EKF_OK;
+}
+
+int ekf_get_map_odom(ekf_t h, int f, double* p) {
+  if (!valid(h, f) || !p) return EKF_E_ARG;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(p, h->ctl[f].tmo, 3 * sizeof(double), hipMemcpyDeviceToHost));
+  return EKF_OK;
+}
+
+int ekf_get_state(ekf_t h, int f, double* state, double* sigma, unsigned* counter) {
+  if (!valid(h, f)) return EKF_E_ARG;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const int p = h->parity[f];
+  if (state)
+    HIPCHK(hipMemcpy(state, h->x[p] + f * h->x_stride, h->n * sizeof(double),
+                     hipMemcpyDeviceToHost));
+  if (sigma) {
+    std::vector<char> buf(h->sig_stride * h->w);
+    const char* src = static_cast<const char*>(h->sig[p]) + f * h->sig_stride * h->w;
+    HIPCHK(hipMemcpy(buf.data(), src, buf.size(), hipMemcpyDeviceToHost));
+    for (int i = 0; i < h->n; ++i)
+      for (int j = 0; j < h->n; ++j) {
+        const size_t e = static_cast<size_t>(i) * h->ld + j;
+        sigma[static_cast<size_t>(i) * h->n + j] =
+            h->w == 4 ? reinterpret_cast<const float*>(buf.data())[e]
+                      : reinterpret_cast<const double*>(buf.data())[e];
+      }
+  }
+  if (counter) HIPCHK(hipMemcpy(counter, &h->ctl[f].counter, sizeof(unsigned), hipMemcpyDeviceToHost));
+  return EKF_OK;
+}
+
+int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, const double* tmo,
+                  unsigned counter) {
+  if (!valid(h, f)) return EKF_E_ARG;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  const int p = h->parity[f];
+  if (state)
+    HIPCHK(hipMemcpy(h->x[p] + f * h->x_stride, state, h->n * sizeof(double),
+                     hipMemcpyHostToDevice));
+  if (sigma) {
+    std::vector<char> buf(h->sig_stride * h->w, 0);
+    for (int i = 0; i < h->n; ++i)
+      for (int j = 0; j < h->n; ++j) {
+        const size_t e = static_cast<size_t>(i) * h->ld + j;
+        const double v = sigma[static_cast<size_t>(i) * h->n + j];
+        if (h->w == 4)
+          reinterpret_cast<float*>(buf.data())[e] = static_cast<float>(v);
+        else
+          reinterpret_cast<double*>(buf.data())[e] = v;
+      }
+    char* dst = static_cast<char*>(h->sig[p]) + f * h->sig_stride * h->w;
+    HIPCHK(hipMemcpy(dst, buf.data(), buf.size(), hipMemcpyHostToDevice));
+  }
+  if (tmo) HIPCHK(hipMemcpy(h->ctl[f].tmo, tmo, 3 * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(&h->ctl[f].counter, &counter, sizeof(unsigned), hipMemcpyHostToDevice));
+  h->pending[f] = 0;
+  return EKF_OK;
+}
+
+int ekf_get_status(ekf_t h, int f, unsigned* flags) {
+  if (!valid(h, f) || !flags) return EKF_E_ARG;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(flags, &h->ctl[f].status, sizeof(unsigned), hipMemcpyDeviceToHost));
+  const unsigned z = 0;
+  HIPCHK(hipMemcpy(&h->ctl[f].status, &z, sizeof(unsigned), hipMemcpyHostToDevice));
+  return EKF_OK;
+}
+
+int ekf_profile_enable(ekf_t h, int enable) {
+  if (!h) return EKF_E_ARG;
+  h->prof = enable != 0;
+  return EKF_OK;
+}
+
+int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
+  if (!h || kind < 0 || kind > 2) return EKF_E_ARG;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  auto& pe = h->pe[kind];
+  for (size_t i = 0; i < pe.start.size(); ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, pe.start[i], pe.stop[i]) == hipSuccess) h->prof_ms[kind] += ms;
+    h->prof_launches[kind] += 1;
+    h->pool.push_back(pe.start[i]);
+    h->pool.push_back(pe.stop[i]);
+  }
+  pe.start.clear();
+  pe.stop.clear();
+  if (launches) *launches = h->prof_launches[kind];
+  if (total_ms) *total_ms = h->prof_ms[kind];
+  h->prof_launches[kind] = 0;
+  h->prof_ms[kind] = 0.0;
+  return EKF_OK;
+}
+
+double ekf_sigma_pass_bytes(ekf_t h, int nf) {
+  if (!h) return 0.0;
+  return 2.0 * static_cast<double>(h->n) * h->n * static_cast<double>(h->w) * nf;
+}
+
+}  // extern "C"

@@ -1,0 +1,46 @@
+// Device-side data layout shared by the kernels (ekf_kernels.hip) and the host runtime (ekf_api.cpp).
+//
+// HBM layout per filter f (row-major, fp64 or fp32 per ekf_config.dtype):
+//   Σ[2]      : two n × ld ping-pong copies (ld = n rounded up to 128 bytes). One launch pair reads
+//               Σ_in and writes Σ_out, so no workgroup ever reads a row another one is rewriting.
+//   x[2]      : state, n doubles each (state math is always fp64).
+//   Kcat,Mcat : KW × ldk low-rank factors of one chunk: Σ_out = Σ_in + Q − Kcatᵀ·Mcat.
+//   FilterCtl : t_map_odom, counter_obstacles, status, association results.
+#pragma once
+#include <cstdint>
+
+namespace ekfslam {
+
+constexpr int kMaxChunk = 16;                    // markers folded into one Σ pass (EKF_MAX_CHUNK)
+constexpr int kMaxU = 3 + 2 * kMaxChunk;         // touched rows/cols of one chunk: pose + 2 per marker
+constexpr int kMaxKW = ((2 + 2 * kMaxChunk + 3) / 4) * 4;  // rank of the fused update, padded to 4
+constexpr int kMaxAssoc = 64;                    // association slots per filter per upload
+
+// MsgDesc.flags
+constexpr int kFirst = 1;    // chunk carries the predict (slam.cpp:184-198) for this message
+constexpr int kLast = 2;     // chunk ends the message: posterior t_map_odom (slam.cpp:273-291)
+constexpr int kNoInit = 4;   // association path: no first-sighting init in the correction
+constexpr int kActive = 8;   // filter takes part in this launch
+
+// One chunk of one message for one filter (uploaded by the host, read by every kernel of the pair).
+struct alignas(16) MsgDesc {
+  int m;             // markers in this chunk (≤ kMaxChunk)
+  int flags;
+  int parity;        // which Σ / x copy is "in"
+  int assoc_slot;    // association: index into FilterCtl::assoc_j for ids[c] < 0
+  double odom[3];    // t_odom_robot (θ, x, y) at this message
+  double pad0;
+  int ids[kMaxChunk];        // landmark ids; < 0 ⇒ taken from FilterCtl::assoc_j[assoc_slot + c]
+  double z[kMaxChunk][2];    // measured (range, bearing), computed on the host like slam.cpp:208-210
+};
+
+struct alignas(16) FilterCtl {
+  double tmo[3];       // t_map_odom (θ, x, y), slam.cpp:659
+  double tmo_next[3];  // posterior written by the gain kernel, committed by the Σ pass
+  unsigned counter;    // counter_obstacles, slam.cpp:670
+  unsigned status;     // EKF_FLAG_* bits
+  int assoc_j[kMaxAssoc];
+  int assoc_new[kMaxAssoc];
+};
+
+}  // namespace ekfslam

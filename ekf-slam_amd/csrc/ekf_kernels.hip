@@ -1,0 +1,691 @@
+// HIP kernels (gfx950 / CDNA4) for the EKF-SLAM predict → correct* → posterior path of
+// maxipalay/ekf-slam nuslam/src/slam.cpp.
+//
+// One message (up to kMaxChunk markers) is one launch pair:
+//
+//   k_gain        The m corrections of a message only couple through the rows/columns the message
+//                 touches, U = {θ, x, y} ∪ {jx, jy per marker} (|U| ≤ 3+2m). Every workgroup first
+//                 replays the m corrections on the |U|×|U| block in LDS (predict folded in), which
+//                 gives each step's H, S⁻¹, ν and K[U], M[:,U]. Then every thread owns one row
+//                 (or one column) of Σ, gathers its |U| entries and runs the same m steps on them,
+//                 emitting K_c[i] (rows) / M_c[:,c] (columns) and the new state x[i].
+//   k_sigma_pass  Σ_out = Σ_in + Q̄ − Σ_k Kcat[k]ᵀ ⊗ Mcat[k], a rank-(2+2m) update of the dense
+//                 covariance: the predict's two rank-1 terms (A Σ Aᵀ, slam.cpp:198) and one rank-2
+//                 term per correction ((I − KH)Σ, slam.cpp:264-265). It streams Σ once per message
+//                 through MFMA (v_mfma_f64_16x16x4f64 / v_mfma_f32_16x16x4f32), so the HBM cost of
+//                 a correction is 2·n²·w / m instead of the 2·n²·w of a per-correction update.
+//
+// Equal to the reference's sequential dense algebra in exact arithmetic; the summation order
+// differs (tolerances in tests/). Unknown association adds k_assoc before each single-marker pair.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+#include <cstdint>
+
+#include "ekf_device.hpp"
+#include "ekf_launch.hpp"
+#include "geom.hpp"
+
+namespace ekfslam {
+
+#define EKF_FLAG_RANGE_D 1u
+#define EKF_FLAG_NUMERIC_D 2u
+
+__device__ __forceinline__ double alpha_of(int idx, double a1, double a2) {
+  return idx == 1 ? a1 : (idx == 2 ? a2 : 0.0);
+}
+
+// Predicted pose and the two nonzeros of At (slam.cpp:184-196). xin = posterior of the last
+// message = filter_previous_configuration (slam.cpp:291).
+__device__ __forceinline__ void predicted_pose(const FilterCtl* ctl, const MsgDesc& d,
+                                               const double* xin, double* pose, double* a1,
+                                               double* a2) {
+  if (d.flags & kFirst) {
+    const Pose2 cur = compose(Pose2{ctl->tmo[0], ctl->tmo[1], ctl->tmo[2]},
+                              Pose2{d.odom[0], d.odom[1], d.odom[2]});
+    *a1 = -(cur.y - xin[2]);
+    *a2 = cur.x - xin[1];
+    pose[0] = normalize_angle(cur.theta);
+    pose[1] = cur.x;
+    pose[2] = cur.y;
+  } else {
+    *a1 = 0.0;
+    *a2 = 0.0;
+    pose[0] = xin[0];
+    pose[1] = xin[1];
+    pose[2] = xin[2];
+  }
+}
+
+// Range-bearing model for landmark at (lx, ly) seen from pose: ẑ and the 2×5 H over
+// {θ, x, y, jx, jy} (slam.cpp:219-249).
+__device__ __forceinline__ void range_bearing(const double* pose, double lx, double ly,
+                                              double* zhat, double* H0, double* H1) {
+  const double ex = lx - pose[1], ey = ly - pose[2];
+  zhat[0] = sqrt(ex * ex + ey * ey);
+  zhat[1] = normalize_angle(atan2(ey, ex) - pose[0]);
+  const double d = ex * ex + ey * ey;
+  const double sd = sqrt(d);
+  H0[0] = 0.0;
+  H0[1] = -ex / sd;
+  H0[2] = -ey / sd;
+  H0[3] = ex / sd;
+  H0[4] = ey / sd;
+  H1[0] = -1.0;
+  H1[1] = ey / d;
+  H1[2] = -ex / d;
+  H1[3] = -ey / d;
+  H1[4] = ex / d;
+}
+
+// arma::inv on a 2×2 (closed form). false if singular / non-finite.
+__device__ __forceinline__ bool inv2(const double* A, double* o) {
+  const double det = A[0] * A[3] - A[1] * A[2];
+  if (!(fabs(det) > 0.0)) return false;
+  o[0] = A[3] / det;
+  o[1] = -A[1] / det;
+  o[2] = -A[2] / det;
+  o[3] = A[0] / det;
+  return isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
+}
+
+struct GainShared {
+  int u[kMaxU];
+  int skip[kMaxChunk];
+  double alphaU[kMaxU];
+  double row0raw[kMaxU];  // Σ_in[0][u_b]
+  double col0raw[kMaxU];  // Σ_in[u_a][0]
+  double xU[kMaxU];
+  double P[kMaxU][kMaxU + 1];
+  double KU[kMaxChunk][kMaxU][2];
+  double MU[kMaxChunk][kMaxU][2];
+  double H[kMaxChunk][10];
+  double Si[kMaxChunk][4];
+  double nu[kMaxChunk][2];
+  double pose[3];
+  double a1, a2, s00;
+  int nu_cnt;
+  unsigned status;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
+  __shared__ GainShared sh;
+  const MsgDesc& d = A.desc[blockIdx.y];
+  if (!(d.flags & kActive)) return;
+  const int f = A.f0 + blockIdx.y;
+  const int tid = threadIdx.x;
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const T* S = A.sig[d.parity] + f * A.sig_stride;
+  const double* xin = A.x[d.parity] + f * A.x_stride;
+  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
+  T* kc = A.kcat + f * A.km_stride;
+  T* mc = A.mcat + f * A.km_stride;
+  FilterCtl* ctl = A.ctl + f;
+  const int m = d.m;
+  const bool first = (d.flags & kFirst) != 0;
+  const int kw = ((2 + 2 * m + 3) / 4) * 4;
+
+  // ---- phase A0: predict pose, index set U --------------------------------------------------
+  if (tid == 0) {
+    double a1, a2;
+    predicted_pose(ctl, d, xin, sh.pose, &a1, &a2);
+    sh.a1 = a1;
+    sh.a2 = a2;
+    sh.u[0] = 0;
+    sh.u[1] = 1;
+    sh.u[2] = 2;
+    unsigned st = 0;
+    for (int c = 0; c < m; ++c) {
+      const int id = d.ids[c] >= 0 ? d.ids[c] : ctl->assoc_j[d.assoc_slot + c];
+      const bool bad = id < 0 || id >= A.N;
+      sh.skip[c] = bad ? 1 : 0;
+      if (bad && d.ids[c] >= 0) st |= EKF_FLAG_RANGE_D;  // association skips were flagged already
+      const int j = bad ? 3 : 3 + 2 * id;
+      sh.u[3 + 2 * c] = j;
+      sh.u[4 + 2 * c] = j + 1;
+    }
+    sh.nu_cnt = 3 + 2 * m;
+    sh.status = st;
+  }
+  __syncthreads();
+  const int nu = sh.nu_cnt;
+
+  // ---- phase A1: gather the |U|×|U| block and x[U] --------------------------------------------
+  for (int e = tid; e < nu * nu; e += blockDim.x) {
+    const int a = e / nu, b = e - a * nu;
+    sh.P[a][b] = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]]);
+  }
+  if (tid < nu) {
+    sh.xU[tid] = tid < 3 ? sh.pose[tid] : xin[sh.u[tid]];
+    sh.alphaU[tid] = first ? alpha_of(sh.u[tid], sh.a1, sh.a2) : 0.0;
+  }
+  __syncthreads();
+  if (tid < nu) {
+    sh.row0raw[tid] = sh.P[0][tid];
+    sh.col0raw[tid] = sh.P[tid][0];
+  }
+  if (tid == 0) sh.s00 = sh.P[0][0];
+  __syncthreads();
+  // predict folded in: P ← A P Aᵀ + Q̄ on the block (slam.cpp:198)
+  if (first) {
+    for (int e = tid; e < nu * nu; e += blockDim.x) {
+      const int a = e / nu, b = e - a * nu;
+      double v = sh.P[a][b] + sh.alphaU[a] * sh.row0raw[b];
+      v = v + (sh.col0raw[a] + sh.alphaU[a] * sh.s00) * sh.alphaU[b];
+      if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
+      sh.P[a][b] = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase A2: the m corrections on the block ---------------------------------------------
+  for (int c = 0; c < m; ++c) {
+    const int pj = 3 + 2 * c;
+    if (tid == 0) {
+      double H0[5] = {0, 0, 0, 0, 0}, H1[5] = {0, 0, 0, 0, 0}, Si[4] = {0, 0, 0, 0}, nv[2] = {0, 0};
+      int sk = sh.skip[c];
+      if (!sk) {
+        // first sighting (slam.cpp:213-216); all copies of a repeated landmark are kept equal
+        if (!(d.flags & kNoInit) && sh.xU[pj] == 0.0 && sh.xU[pj + 1] == 0.0) {
+          const double ix = sh.xU[1] + d.z[c][0] * cos(d.z[c][1] + sh.xU[0]);
+          const double iy = sh.xU[2] + d.z[c][0] * sin(d.z[c][1] + sh.xU[0]);
+          const int jx = sh.u[pj];
+          for (int b = 3; b < nu; ++b) {
+            if (sh.u[b] == jx) sh.xU[b] = ix;
+            else if (sh.u[b] == jx + 1) sh.xU[b] = iy;
+          }
+        }
+        double zhat[2];
+        range_bearing(sh.xU, sh.xU[pj], sh.xU[pj + 1], zhat, H0, H1);
+        const int pA[5] = {0, 1, 2, pj, pj + 1};
+        double HP0[5], HP1[5];
+        for (int bb = 0; bb < 5; ++bb) {
+          double s0 = 0.0, s1 = 0.0;
+          for (int a = 0; a < 5; ++a) {
+            const double v = sh.P[pA[a]][pA[bb]];
+            s0 += H0[a] * v;
+            s1 += H1[a] * v;
+          }
+          HP0[bb] = s0;
+          HP1[bb] = s1;
+        }
+        double Sm[4] = {0, 0, 0, 0};
+        for (int a = 0; a < 5; ++a) {
+          Sm[0] += HP0[a] * H0[a];
+          Sm[1] += HP0[a] * H1[a];
+          Sm[2] += HP1[a] * H0[a];
+          Sm[3] += HP1[a] * H1[a];
+        }
+        Sm[0] += A.r;
+        Sm[3] += A.r;
+        if (inv2(Sm, Si)) {
+          nv[0] = d.z[c][0] - zhat[0];
+          nv[1] = normalize_angle(d.z[c][1] - zhat[1]);
+        } else {
+          sk = 1;
+          sh.status |= EKF_FLAG_NUMERIC_D;
+        }
+      }
+      if (sk) {
+        for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
+        Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
+        nv[0] = nv[1] = 0.0;
+      }
+      sh.skip[c] = sk;
+      for (int a = 0; a < 5; ++a) {
+        sh.H[c][a] = H0[a];
+        sh.H[c][5 + a] = H1[a];
+      }
+      for (int a = 0; a < 4; ++a) sh.Si[c][a] = Si[a];
+      sh.nu[c][0] = nv[0];
+      sh.nu[c][1] = nv[1];
+    }
+    __syncthreads();
+    if (tid < nu) {
+      const int pA[5] = {0, 1, 2, pj, pj + 1};
+      const double* H = sh.H[c];
+      const double* Si = sh.Si[c];
+      double kt0 = 0.0, kt1 = 0.0, mm0 = 0.0, mm1 = 0.0;
+      for (int a = 0; a < 5; ++a) {
+        const double v = sh.P[tid][pA[a]];
+        kt0 += v * H[a];
+        kt1 += v * H[5 + a];
+      }
+      for (int a = 0; a < 5; ++a) {
+        const double v = sh.P[pA[a]][tid];
+        mm0 += H[a] * v;
+        mm1 += H[5 + a] * v;
+      }
+      const double K0 = kt0 * Si[0] + kt1 * Si[2];
+      const double K1 = kt0 * Si[1] + kt1 * Si[3];
+      sh.KU[c][tid][0] = K0;
+      sh.KU[c][tid][1] = K1;
+      sh.MU[c][tid][0] = mm0;
+      sh.MU[c][tid][1] = mm1;
+      sh.xU[tid] = sh.xU[tid] + (K0 * sh.nu[c][0] + K1 * sh.nu[c][1]);
+    }
+    __syncthreads();
+    for (int e = tid; e < nu * nu; e += blockDim.x) {
+      const int a = e / nu, b = e - a * nu;
+      sh.P[a][b] -= sh.KU[c][a][0] * sh.MU[c][b][0] + sh.KU[c][a][1] * sh.MU[c][b][1];
+    }
+    if (tid == 0) sh.xU[0] = normalize_angle(sh.xU[0]);  // slam.cpp:267
+    __syncthreads();
+  }
+
+  if (blockIdx.x == 0 && tid == 0) {
+    if (sh.status) atomicOr(&ctl->status, sh.status);
+    if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
+      const Pose2 tmo = compose(Pose2{sh.xU[0], sh.xU[1], sh.xU[2]},
+                                inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
+      ctl->tmo_next[0] = tmo.theta;
+      ctl->tmo_next[1] = tmo.x;
+      ctl->tmo_next[2] = tmo.y;
+    }
+  }
+
+  // ---- phase B: one row or one column of Σ per thread ----------------------------------------
+  const int gi = blockIdx.x * blockDim.x + tid;
+  const double s00 = sh.s00;
+  if (gi < n) {
+    const int i = gi;
+    const T* rowp = S + static_cast<size_t>(i) * ld;
+    double r[kMaxU];
+#pragma unroll
+    for (int b = 0; b < kMaxU; ++b) r[b] = b < nu ? static_cast<double>(rowp[sh.u[b]]) : 0.0;
+    const double ai = first ? alpha_of(i, sh.a1, sh.a2) : 0.0;
+    const double r0raw = r[0];
+    if (first) {
+#pragma unroll
+      for (int b = 0; b < kMaxU; ++b) {
+        if (b < nu) {
+          double v = r[b] + ai * sh.row0raw[b];
+          v = v + (r0raw + ai * s00) * sh.alphaU[b];
+          if (i == sh.u[b] && i < 3) v += A.q;
+          r[b] = v;
+        }
+      }
+    }
+    kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
+    kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
+    double xi = xin[i];
+#pragma unroll
+    for (int c = 0; c < kMaxChunk; ++c) {
+      if (c < m) {
+        const double* H = sh.H[c];
+        const double* Si = sh.Si[c];
+        const double v[5] = {r[0], r[1], r[2], r[3 + 2 * c], r[4 + 2 * c]};
+        double kt0 = 0.0, kt1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          kt0 += v[a] * H[a];
+          kt1 += v[a] * H[5 + a];
+        }
+        const double K0 = kt0 * Si[0] + kt1 * Si[2];
+        const double K1 = kt0 * Si[1] + kt1 * Si[3];
+        kc[(2 + 2 * c) * ldk + i] = static_cast<T>(K0);
+        kc[(3 + 2 * c) * ldk + i] = static_cast<T>(K1);
+        xi = xi + (K0 * sh.nu[c][0] + K1 * sh.nu[c][1]);
+#pragma unroll
+        for (int b = 0; b < kMaxU; ++b)
+          if (b < nu) r[b] -= K0 * sh.MU[c][b][0] + K1 * sh.MU[c][b][1];
+      }
+    }
+    for (int k = 2 + 2 * m; k < kw; ++k) kc[k * ldk + i] = static_cast<T>(0);
+    int pos = -1;
+    for (int b = nu - 1; b >= 0; --b)
+      if (sh.u[b] == i) pos = b;
+    xout[i] = pos >= 0 ? sh.xU[pos] : xi;
+  } else if (gi < 2 * n) {
+    const int col = gi - n;
+    double cl[kMaxU];
+#pragma unroll
+    for (int a = 0; a < kMaxU; ++a)
+      cl[a] = a < nu ? static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + col]) : 0.0;
+    const double ac = first ? alpha_of(col, sh.a1, sh.a2) : 0.0;
+    const double c0raw = cl[0];
+    if (first) {
+#pragma unroll
+      for (int a = 0; a < kMaxU; ++a) {
+        if (a < nu) {
+          double v = cl[a] + sh.alphaU[a] * c0raw;
+          v = v + (sh.col0raw[a] + sh.alphaU[a] * s00) * ac;
+          if (sh.u[a] == col && col < 3) v += A.q;
+          cl[a] = v;
+        }
+      }
+    }
+    mc[0 * ldk + col] = static_cast<T>(first ? c0raw : 0.0);
+    mc[1 * ldk + col] = static_cast<T>(first ? ac : 0.0);
+#pragma unroll
+    for (int c = 0; c < kMaxChunk; ++c) {
+      if (c < m) {
+        const double* H = sh.H[c];
+        const double v[5] = {cl[0], cl[1], cl[2], cl[3 + 2 * c], cl[4 + 2 * c]};
+        double mm0 = 0.0, mm1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          mm0 += H[a] * v[a];
+          mm1 += H[5 + a] * v[a];
+        }
+        mc[(2 + 2 * c) * ldk + col] = static_cast<T>(mm0);
+        mc[(3 + 2 * c) * ldk + col] = static_cast<T>(mm1);
+#pragma unroll
+        for (int a = 0; a < kMaxU; ++a)
+          if (a < nu) cl[a] -= sh.KU[c][a][0] * mm0 + sh.KU[c][a][1] * mm1;
+      }
+    }
+    for (int k = 2 + 2 * m; k < kw; ++k) mc[k * ldk + col] = static_cast<T>(0);
+  }
+}
+
+// ---- Σ pass on MFMA -------------------------------------------------------------------------
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Mfma;
+template <> struct Mfma<double> {
+  using acc_t = d4;
+  // v_mfma_f64_16x16x4_f64: D[row = (lane>>4) + 4r][col = lane&15]
+  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+  static __device__ __forceinline__ acc_t op(double a, double b, acc_t c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<float> {
+  using acc_t = f4;
+  // v_mfma_f32_16x16x4_f32: D[row = 4(lane>>4) + r][col = lane&15]
+  static __device__ __forceinline__ int row(int lane, int r) { return 4 * (lane >> 4) + r; }
+  static __device__ __forceinline__ acc_t op(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+};
+
+// Block tile 64×64, four waves of 32×32 (2×2 MFMA tiles of 16×16). A operand lane map for both
+// shapes: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15].
+template <typename T>
+__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles) {
+  using M = Mfma<T>;
+  using acc_t = typename M::acc_t;
+  const MsgDesc& d = A.desc[blockIdx.y];
+  if (!(d.flags & kActive)) return;
+  const int f = A.f0 + blockIdx.y;
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const T* Sin = A.sig[d.parity] + f * A.sig_stride;
+  T* Sout = A.sig[d.parity ^ 1] + f * A.sig_stride;
+  const T* kc = A.kcat + f * A.km_stride;
+  const T* mc = A.mcat + f * A.km_stride;
+  const bool first = (d.flags & kFirst) != 0;
+  const T q = static_cast<T>(A.q);
+  const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
+
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (d.flags & kLast)) {
+    FilterCtl* ctl = A.ctl + f;
+    ctl->tmo[0] = ctl->tmo_next[0];
+    ctl->tmo[1] = ctl->tmo_next[1];
+    ctl->tmo[2] = ctl->tmo_next[2];
+  }
+
+  const int tr = blockIdx.x / tiles, tc = blockIdx.x - tr * tiles;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int R0 = tr * 64 + (w >> 1) * 32, C0 = tc * 64 + (w & 1) * 32;
+  if (R0 >= n || C0 >= n) return;
+
+  acc_t acc[2][2];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = R0 + 16 * ti + M::row(lane, r);
+        const int col = C0 + 16 * tj + (lane & 15);
+        T v = (row < n && col < n) ? Sin[static_cast<size_t>(row) * ld + col] : static_cast<T>(0);
+        if (first && row == col && row < 3) v += q;
+        acc[ti][tj][r] = v;
+      }
+
+  const int kr = lane >> 4, kcol = lane & 15;
+  for (int s = 0; s < kw; s += 4) {
+    const T* krow = kc + static_cast<size_t>(s + kr) * ldk;
+    const T* mrow = mc + static_cast<size_t>(s + kr) * ldk;
+    T a0 = -krow[R0 + kcol], a1 = -krow[R0 + 16 + kcol];
+    T b0 = mrow[C0 + kcol], b1 = mrow[C0 + 16 + kcol];
+    acc[0][0] = M::op(a0, b0, acc[0][0]);
+    acc[0][1] = M::op(a0, b1, acc[0][1]);
+    acc[1][0] = M::op(a1, b0, acc[1][0]);
+    acc[1][1] = M::op(a1, b1, acc[1][1]);
+  }
+
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = R0 + 16 * ti + M::row(lane, r);
+        const int col = C0 + 16 * tj + (lane & 15);
+        if (row < n && col < n) Sout[static_cast<size_t>(row) * ld + col] = acc[ti][tj][r];
+      }
+}
+
+// ---- association ------------------------------------------------------------------------------
+// slam.cpp:344-440 for the marker in desc.z[0]: d_k = νᵀψ_k⁻¹ν over the known landmarks k < counter
+// (predict folded in when pending), the new slot's d forced to the gate (:406-408), first-index
+// argmin (arma::index_min), then commit (new landmark written into x_in, counter++) or roll back.
+template <typename T>
+__global__ __launch_bounds__(256) void k_assoc(PassArgs<T> A) {
+  __shared__ double s_pose[3], s_a[2], s_P33[3][3];
+  __shared__ double s_bd[4];
+  __shared__ int s_bk[4];
+  __shared__ int s_abort;
+  const MsgDesc& d = A.desc[blockIdx.y];
+  if (!(d.flags & kActive) || d.m == 0) return;
+  const int f = A.f0 + blockIdx.y;
+  const int tid = threadIdx.x;
+  const int ld = A.ld;
+  const T* S = A.sig[d.parity] + f * A.sig_stride;
+  double* x = A.x[d.parity] + f * A.x_stride;
+  FilterCtl* ctl = A.ctl + f;
+  const unsigned s = ctl->counter;
+  const int slot = d.assoc_slot;
+  if (tid == 0) {
+    double a1, a2;
+    predicted_pose(ctl, d, x, s_pose, &a1, &a2);
+    s_a[0] = a1;
+    s_a[1] = a2;
+    double raw[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) raw[a][b] = static_cast<double>(S[a * ld + b]);
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        const double aa = (d.flags & kFirst) ? alpha_of(a, a1, a2) : 0.0;
+        const double ab = (d.flags & kFirst) ? alpha_of(b, a1, a2) : 0.0;
+        double v = raw[a][b] + aa * raw[0][b];
+        v = v + (raw[a][0] + aa * raw[0][0]) * ab;
+        if ((d.flags & kFirst) && a == b) v += A.q;
+        s_P33[a][b] = v;
+      }
+    s_abort = 0;
+    if (s >= static_cast<unsigned>(A.N)) {  // the reference indexes state(3+2·counter) out of range
+      s_abort = 1;
+      atomicOr(&ctl->status, EKF_FLAG_RANGE_D);
+      ctl->assoc_j[slot] = -1;
+      ctl->assoc_new[slot] = 0;
+    }
+  }
+  __syncthreads();
+  if (s_abort) return;
+  const double z0 = d.z[0][0], z1 = d.z[0][1];
+  const double a1 = s_a[0], a2 = s_a[1];
+  const bool first = (d.flags & kFirst) != 0;
+  double bestd = INFINITY;
+  int bestk = INT_MAX;
+  for (unsigned k = tid; k < s; k += blockDim.x) {
+    const int j = 3 + 2 * static_cast<int>(k);
+    double P[5][5];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) P[a][b] = s_P33[a][b];
+    const double r0j0 = static_cast<double>(S[j]), r0j1 = static_cast<double>(S[j + 1]);
+    for (int a = 0; a < 3; ++a) {
+      const double aa = first ? alpha_of(a, a1, a2) : 0.0;
+      P[a][3] = static_cast<double>(S[a * ld + j]) + aa * r0j0;
+      P[a][4] = static_cast<double>(S[a * ld + j + 1]) + aa * r0j1;
+    }
+    for (int e = 0; e < 2; ++e) {
+      const T* row = S + static_cast<size_t>(j + e) * ld;
+      const double rj0 = static_cast<double>(row[0]);
+      for (int b = 0; b < 3; ++b) {
+        const double ab = first ? alpha_of(b, a1, a2) : 0.0;
+        P[3 + e][b] = static_cast<double>(row[b]) + rj0 * ab;
+      }
+      P[3 + e][3] = static_cast<double>(row[j]);
+      P[3 + e][4] = static_cast<double>(row[j + 1]);
+    }
+    double zhat[2], H0[5], H1[5];
+    range_bearing(s_pose, x[j], x[j + 1], zhat, H0, H1);
+    double HP0[5], HP1[5];
+    for (int bb = 0; bb < 5; ++bb) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int a = 0; a < 5; ++a) {
+        s0 += H0[a] * P[a][bb];
+        s1 += H1[a] * P[a][bb];
+      }
+      HP0[bb] = s0;
+      HP1[bb] = s1;
+    }
+    double psi[4] = {0, 0, 0, 0};
+    for (int b = 0; b < 5; ++b) {
+      psi[0] += HP0[b] * H0[b];
+      psi[1] += HP0[b] * H1[b];
+      psi[2] += HP1[b] * H0[b];
+      psi[3] += HP1[b] * H1[b];
+    }
+    psi[0] += A.r;
+    psi[3] += A.r;
+    const double nu0 = z0 - zhat[0];
+    const double nu1 = normalize_angle(z1 - zhat[1]);
+    double pi[4];
+    double dist = NAN;
+    const double det = psi[0] * psi[3] - psi[1] * psi[2];
+    if (fabs(det) > 0.0) {
+      pi[0] = psi[3] / det;
+      pi[1] = -psi[1] / det;
+      pi[2] = -psi[2] / det;
+      pi[3] = psi[0] / det;
+      const double t0 = nu0 * pi[0] + nu1 * pi[2];
+      const double t1 = nu0 * pi[1] + nu1 * pi[3];
+      dist = t0 * nu0 + t1 * nu1;
+    }
+    if (dist < bestd) {  // strict: first index kept, NaN never selected
+      bestd = dist;
+      bestk = static_cast<int>(k);
+    }
+  }
+  // wave argmin (64 lanes), ties → lower index
+  for (int off = 32; off > 0; off >>= 1) {
+    const double od = __shfl_xor(bestd, off, 64);
+    const int ok = __shfl_xor(bestk, off, 64);
+    if (od < bestd || (od == bestd && ok < bestk)) {
+      bestd = od;
+      bestk = ok;
+    }
+  }
+  const int wv = tid >> 6;
+  if ((tid & 63) == 0) {
+    s_bd[wv] = bestd;
+    s_bk[wv] = bestk;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < static_cast<int>(blockDim.x >> 6); ++w)
+      if (s_bd[w] < bestd || (s_bd[w] == bestd && s_bk[w] < bestk)) {
+        bestd = s_bd[w];
+        bestk = s_bk[w];
+      }
+    // the new slot (index s, d = gate) wins only over a strictly larger existing minimum
+    if (!(bestd <= A.gate)) {
+      const int js = 3 + 2 * static_cast<int>(s);
+      x[js] = s_pose[1] + z0 * cos(z1 + s_pose[0]);      // slam.cpp:351-354
+      x[js + 1] = s_pose[2] + z0 * sin(z1 + s_pose[0]);
+      ctl->counter = s + 1;
+      ctl->assoc_j[slot] = static_cast<int>(s);
+      ctl->assoc_new[slot] = 1;
+    } else {
+      ctl->assoc_j[slot] = bestk;
+      ctl->assoc_new[slot] = 0;
+    }
+  }
+}
+
+template <typename T>
+__global__ void k_posterior(PassArgs<T> A, int nf) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nf) return;
+  const MsgDesc& d = A.desc[k];
+  if (!(d.flags & kActive)) return;
+  const int f = A.f0 + k;
+  const double* x = A.x[d.parity] + f * A.x_stride;
+  FilterCtl* ctl = A.ctl + f;
+  const Pose2 tmo = compose(Pose2{x[0], x[1], x[2]}, inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
+  ctl->tmo[0] = tmo.theta;
+  ctl->tmo[1] = tmo.x;
+  ctl->tmo[2] = tmo.y;
+}
+
+template <typename T>
+__global__ void k_init_diag(T* sig, size_t stride, int n, int ld, double v, int nf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x + 3;
+  if (i >= n) return;
+  for (int f = blockIdx.y; f < nf; f += gridDim.y)
+    sig[f * stride + static_cast<size_t>(i) * ld + i] = static_cast<T>(v);
+}
+
+// ---- launchers ------------------------------------------------------------------------------
+template <typename T>
+hipError_t launch_gain(const PassArgs<T>& a, int nf, hipStream_t s) {
+  const dim3 grid((2 * a.n + 255) / 256, nf);
+  hipLaunchKernelGGL(k_gain<T>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s) {
+  const int tiles = (a.n + 63) / 64;
+  const dim3 grid(tiles * tiles, nf);
+  (void)kw;
+  hipLaunchKernelGGL(k_sigma_pass<T>, grid, dim3(256), 0, s, a, tiles);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_assoc(const PassArgs<T>& a, int nf, hipStream_t s) {
+  hipLaunchKernelGGL(k_assoc<T>, dim3(1, nf), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_posterior(const PassArgs<T>& a, int nf, hipStream_t s) {
+  hipLaunchKernelGGL(k_posterior<T>, dim3((nf + 63) / 64), dim3(64), 0, s, a, nf);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int nf, hipStream_t s) {
+  hipLaunchKernelGGL(k_init_diag<T>, dim3((n + 255) / 256, nf < 65535 ? nf : 65535), dim3(256), 0,
+                     s, sig, stride, n, ld, v, nf);
+  return hipGetLastError();
+}
+
+#define EKF_INSTANTIATE(T)                                                              \
+  template hipError_t launch_gain<T>(const PassArgs<T>&, int, hipStream_t);             \
+  template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, int, hipStream_t);  \
+  template hipError_t launch_assoc<T>(const PassArgs<T>&, int, hipStream_t);            \
+  template hipError_t launch_posterior<T>(const PassArgs<T>&, int, hipStream_t);              \
+  template hipError_t launch_init_diag<T>(T*, size_t, int, int, double, int, hipStream_t);
+EKF_INSTANTIATE(double)
+EKF_INSTANTIATE(float)
+
+}  // namespace ekfslam

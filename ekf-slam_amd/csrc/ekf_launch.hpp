@@ -1,0 +1,50 @@
+// Kernel launchers (defined in ekf_kernels.hip, called by the host runtime in ekf_api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "ekf_device.hpp"
+
+namespace ekfslam {
+
+// Everything a launch needs to find filter f's buffers. Filters [f0, f0 + grid.y) take part;
+// desc[k] describes filter f0 + k.
+template <typename T>
+struct PassArgs {
+  T* sig[2];            // Σ ping-pong copies, filter 0
+  size_t sig_stride;    // elements between filters
+  double* x[2];         // state ping-pong copies, filter 0
+  size_t x_stride;
+  T* kcat;              // [KW][ldk] per filter (row k = one rank-1 factor over rows i)
+  T* mcat;              // [KW][ldk] per filter (row k = one rank-1 factor over cols c)
+  size_t km_stride;
+  int ldk;
+  FilterCtl* ctl;
+  const MsgDesc* desc;
+  int n, ld, N, f0;
+  double q, r, gate;
+};
+
+// Fused gain kernel: small-block sequential corrections + per-row/per-column recursions that emit
+// Kcat/Mcat and the new state. Grid (ceil(2n/256), filters).
+template <typename T>
+hipError_t launch_gain(const PassArgs<T>& a, int n_filters, hipStream_t s);
+
+// Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, 64×64 tiles. kw = padded rank for this launch.
+template <typename T>
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, int kw, hipStream_t s);
+
+// Mahalanobis nearest-neighbour association for one marker per filter (one workgroup each).
+template <typename T>
+hipError_t launch_assoc(const PassArgs<T>& a, int n_filters, hipStream_t s);
+
+// Posterior t_map_odom for filters with no pending Σ pass.
+template <typename T>
+hipError_t launch_posterior(const PassArgs<T>& a, int n_filters, hipStream_t s);
+
+// Σ₀ diagonal: Σ[i][i] = v for i ≥ 3 (the rest is zero-filled by the caller).
+template <typename T>
+hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int nf, hipStream_t s);
+
+}  // namespace ekfslam

@@ -1,0 +1,96 @@
+// SE(2) geometry and differential-drive odometry, host + device.
+//
+// Same semantics as the reference's turtlelib (maxipalay/ekf-slam), written fresh for use on both
+// sides of the HIP boundary:
+//   normalize_angle   turtlelib/src/geometry2d.cpp:5-14   (fmod based, maps into (-π, π], -π → π)
+//   Pose2 compose     turtlelib/src/se2d.cpp:66-75        (Transform2D::operator*=; θ not wrapped)
+//   Pose2 inverse     turtlelib/src/se2d.cpp:57-63        (Transform2D::inv)
+//   integrate_twist   turtlelib/src/se2d.cpp:127-138
+//   DiffDrive::fkin   turtlelib/src/diff_drive.cpp:10-28
+//   DiffDrive::ikin   turtlelib/src/diff_drive.cpp:30-38  (host only; throws on lateral twist)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+namespace ekfslam {
+
+constexpr double kPi = 3.14159265358979323846;
+
+__host__ __device__ inline double normalize_angle(double rad) {
+  const double d = fmod(rad + kPi, 2.0 * kPi);
+  return d <= 0.0 ? d + kPi : d - kPi;
+}
+
+// A planar rigid transform {θ, x, y} (turtlelib Transform2D).
+struct Pose2 {
+  double theta = 0.0, x = 0.0, y = 0.0;
+};
+
+struct Twist2 {
+  double omega = 0.0, vx = 0.0, vy = 0.0;
+};
+
+__host__ __device__ inline Pose2 compose(const Pose2& a, const Pose2& b) {
+  const double c = cos(a.theta), s = sin(a.theta);
+  Pose2 r;
+  r.theta = a.theta + b.theta;
+  r.x = c * b.x - s * b.y + a.x;
+  r.y = s * b.x + c * b.y + a.y;
+  return r;
+}
+
+__host__ __device__ inline Pose2 inverse(const Pose2& t) {
+  const double c = cos(t.theta), s = sin(t.theta);
+  Pose2 r;
+  r.theta = -t.theta;
+  r.x = -t.x * c - t.y * s;
+  r.y = -t.y * c + t.x * s;
+  return r;
+}
+
+// Exact integration of a body twist over unit time.
+__host__ __device__ inline Pose2 integrate_twist(const Twist2& tw) {
+  if (tw.omega == 0.0) return Pose2{0.0, tw.vx, tw.vy};
+  const Pose2 tsb{0.0, tw.vy / tw.omega, -tw.vx / tw.omega};
+  return compose(compose(inverse(tsb), Pose2{tw.omega, 0.0, 0.0}), tsb);
+}
+
+struct WheelSpeeds {
+  double left = 0.0, right = 0.0;
+};
+
+class DiffDrive {
+ public:
+  __host__ __device__ DiffDrive(double track = 0.160, double radius = 0.033)
+      : track_(track), radius_(radius) {}
+
+  // Wheel angles → body twist → exact arc → config ← config · Δ.
+  __host__ __device__ Pose2 fkin(double rad_left, double rad_right) {
+    const double dl = rad_left - phi_l_, dr = rad_right - phi_r_;
+    const Twist2 tw{radius_ / track_ * (-dl + dr), radius_ / 2.0 * (dl + dr), 0.0};
+    config_ = compose(config_, integrate_twist(tw));
+    phi_l_ = rad_left;
+    phi_r_ = rad_right;
+    return config_;
+  }
+
+  // Body twist → wheel velocities. Returns false on a twist with lateral velocity (the reference
+  // throws std::logic_error there, diff_drive.cpp:31-33).
+  __host__ bool ikin(const Twist2& tw, WheelSpeeds* out) const {
+    if (std::fabs(tw.vy) > 1e-12) return false;
+    out->left = -track_ / 2.0 / radius_ * tw.omega + 1.0 / radius_ * tw.vx;
+    out->right = track_ / 2.0 / radius_ * tw.omega + 1.0 / radius_ * tw.vx;
+    return true;
+  }
+
+  __host__ __device__ Pose2 config() const { return config_; }
+  __host__ __device__ void set_config(const Pose2& p) { config_ = p; }
+
+ private:
+  double track_, radius_;
+  double phi_l_ = 0.0, phi_r_ = 0.0;
+  Pose2 config_{};
+};
+
+}  // namespace ekfslam

@@ -1,0 +1,320 @@
+"""ctypes binding of libekfslam.so (include/ekf.h, include/slam_core.h).
+
+The binding is plumbing for tests and bench.py; the product is the C-ABI library. Loading fails
+loudly when the HIP library has not been built — there is no CPU fallback anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libekfslam.so")
+
+EKF_OK, EKF_E_ARG, EKF_E_RANGE, EKF_E_EMPTY, EKF_E_NUMERIC, EKF_E_HIP, EKF_E_NOMEM = \
+    0, -1, -2, -3, -4, -5, -6
+EKF_FLAG_RANGE, EKF_FLAG_NUMERIC = 1, 2
+EKF_F64, EKF_F32 = 0, 1
+ADD, DELETE = 0, 2
+SOURCE_SIM, SOURCE_ASSOC = 0, 1
+
+# every symbol include/ekf.h and include/slam_core.h declare
+EXPORTS = [
+    "ekf_config_default", "ekf_strerror", "ekf_create", "ekf_destroy", "ekf_dims", "ekf_set_odom",
+    "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_predict",
+    "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_get_pose",
+    "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status",
+    "ekf_profile_enable", "ekf_profile_read", "ekf_sigma_pass_bytes",
+    "slam_create", "slam_destroy", "slam_joint_states", "slam_markers", "slam_initial_pose",
+    "slam_odom", "slam_map_odom", "slam_filter", "slam_replay", "slam_integrate_odometry",
+]
+
+
+class EkfError(RuntimeError):
+    def __init__(self, rc: int, what: str = ""):
+        self.rc = rc
+        super().__init__(f"{what}: {lib().ekf_strerror(rc).decode()} ({rc})")
+
+
+class Config(C.Structure):
+    _fields_ = [("n_landmarks", C.c_int), ("n_filters", C.c_int), ("dtype", C.c_int),
+                ("q_noise", C.c_double), ("r_noise", C.c_double), ("init_var", C.c_double),
+                ("mah_gate", C.c_double), ("device", C.c_int)]
+
+
+_lib = None
+_vp, _ip, _dp, _i, _d = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_int, C.c_double
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` "
+                               "(or __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        sig = {
+            "ekf_config_default": (None, [C.POINTER(Config)]),
+            "ekf_strerror": (C.c_char_p, [_i]),
+            "ekf_create": (_i, [C.POINTER(_vp), C.POINTER(Config)]),
+            "ekf_destroy": (_i, [_vp]),
+            "ekf_dims": (_i, [_vp, _ip, _ip, _ip]),
+            "ekf_set_odom": (_i, [_vp, _i, _d, _d, _d]),
+            "ekf_fake_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+            "ekf_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+            "ekf_batch_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+            "ekf_replay": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+            "ekf_predict": (_i, [_vp, _i]),
+            "ekf_correct": (_i, [_vp, _i, _i, _d, _d]),
+            "ekf_associate_correct": (_i, [_vp, _i, _d, _d, _ip, _ip]),
+            "ekf_posterior": (_i, [_vp, _i]),
+            "ekf_sync": (_i, [_vp]),
+            "ekf_get_pose": (_i, [_vp, _i, _vp]),
+            "ekf_get_map_odom": (_i, [_vp, _i, _vp]),
+            "ekf_get_state": (_i, [_vp, _i, _vp, _vp, _vp]),
+            "ekf_set_state": (_i, [_vp, _i, _vp, _vp, _vp, C.c_uint]),
+            "ekf_get_status": (_i, [_vp, _i, C.POINTER(C.c_uint)]),
+            "ekf_profile_enable": (_i, [_vp, _i]),
+            "ekf_profile_read": (_i, [_vp, _i, C.POINTER(C.c_longlong), _dp]),
+            "ekf_sigma_pass_bytes": (C.c_double, [_vp, _i]),
+            "slam_create": (_i, [C.POINTER(_vp), C.POINTER(Config), _d, _d, _i]),
+            "slam_destroy": (_i, [_vp]),
+            "slam_joint_states": (_i, [_vp, _d, _d]),
+            "slam_markers": (_i, [_vp, _i, _vp, _vp, _vp]),
+            "slam_initial_pose": (_i, [_vp, _d, _d, _d]),
+            "slam_odom": (_i, [_vp, _vp]),
+            "slam_map_odom": (_i, [_vp, _vp]),
+            "slam_filter": (_vp, [_vp]),
+            "slam_replay": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+            "slam_integrate_odometry": (_i, [_d, _d, _i, _i, _vp, _vp]),
+        }
+        for name, (res, argt) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = argt
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def make_config(n_landmarks=50, n_filters=1, dtype=EKF_F64, q_noise=1e-2, r_noise=1e-2,
+                init_var=10e6, mah_gate=2.0, device=0) -> Config:
+    c = Config()
+    lib().ekf_config_default(C.byref(c))
+    c.n_landmarks, c.n_filters, c.dtype = n_landmarks, n_filters, dtype
+    c.q_noise, c.r_noise, c.init_var, c.mah_gate, c.device = (q_noise, r_noise, init_var,
+                                                             mah_gate, device)
+    return c
+
+
+def _check(rc, what):
+    if rc != EKF_OK:
+        raise EkfError(rc, what)
+    return rc
+
+
+class EKF:
+    """A handle of F independent filters (F = 1: one slam node's filter)."""
+
+    def __init__(self, n_landmarks=50, n_filters=1, dtype=EKF_F64, **kw):
+        self.cfg = make_config(n_landmarks, n_filters, dtype, **kw)
+        h = C.c_void_p()
+        _check(lib().ekf_create(C.byref(h), C.byref(self.cfg)), "ekf_create")
+        self.h = h
+        n, ld, nf = C.c_int(), C.c_int(), C.c_int()
+        lib().ekf_dims(self.h, C.byref(n), C.byref(ld), C.byref(nf))
+        self.n, self.ld, self.F = n.value, ld.value, nf.value
+        self.N = n_landmarks
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ekf_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    # callbacks
+    def set_odom(self, pose, f=0):
+        return lib().ekf_set_odom(self.h, f, float(pose[0]), float(pose[1]), float(pose[2]))
+
+    def fake_sensor(self, ids, actions, rel_xy, f=0) -> int:
+        ids, act, rel = _i32(ids), _i32(actions), _f64(rel_xy)
+        return lib().ekf_fake_sensor(self.h, f, len(ids), _ptr(ids), _ptr(act), _ptr(rel))
+
+    def sensor(self, rel_xy, f=0, decisions=True):
+        rel = _f64(rel_xy)
+        m = rel.size // 2
+        j = np.zeros(max(m, 1), np.int32)
+        nw = np.zeros(max(m, 1), np.int32)
+        rc = lib().ekf_sensor(self.h, f, m, _ptr(rel), _ptr(j) if decisions else None,
+                              _ptr(nw) if decisions else None)
+        return rc, j[:m], nw[:m]
+
+    def batch_sensor(self, counts, rel_xy, odom=None, ids=None, actions=None, assoc=False):
+        counts, rel = _i32(counts), _f64(rel_xy)
+        m_max = rel.shape[1]
+        ids = None if ids is None else _i32(ids)
+        actions = None if actions is None else _i32(actions)
+        odom = None if odom is None else _f64(odom)
+        return lib().ekf_batch_sensor(self.h, int(assoc), m_max, _ptr(counts), _ptr(ids),
+                                      _ptr(actions), _ptr(rel), _ptr(odom))
+
+    def replay(self, counts, rel_xy, odom, ids=None, actions=None, assoc=False, poses=False):
+        """counts[T][F], rel_xy[T][F][M][2], odom[T][F][3]."""
+        counts, rel, odom = _i32(counts), _f64(rel_xy), _f64(odom)
+        T, M = rel.shape[0], rel.shape[2]
+        ids = None if ids is None else _i32(ids)
+        actions = None if actions is None else _i32(actions)
+        out = np.zeros((T, self.F, 3)) if poses else None
+        rc = lib().ekf_replay(self.h, int(assoc), T, M, _ptr(counts), _ptr(ids), _ptr(actions),
+                              _ptr(rel), _ptr(odom), _ptr(out))
+        _check(rc, "ekf_replay")
+        return out
+
+    # fine-grained
+    def predict(self, f=0):
+        return lib().ekf_predict(self.h, f)
+
+    def correct(self, mid, rx, ry, f=0):
+        return lib().ekf_correct(self.h, f, int(mid), float(rx), float(ry))
+
+    def associate_correct(self, rx, ry, f=0):
+        j, nw = C.c_int(-1), C.c_int(0)
+        rc = lib().ekf_associate_correct(self.h, f, float(rx), float(ry), C.byref(j), C.byref(nw))
+        return rc, j.value, nw.value
+
+    def posterior(self, f=0):
+        return lib().ekf_posterior(self.h, f)
+
+    # state
+    def sync(self):
+        _check(lib().ekf_sync(self.h), "ekf_sync")
+
+    def pose(self, f=0):
+        p = np.zeros(3)
+        _check(lib().ekf_get_pose(self.h, f, _ptr(p)), "ekf_get_pose")
+        return p
+
+    def map_odom(self, f=0):
+        p = np.zeros(3)
+        _check(lib().ekf_get_map_odom(self.h, f, _ptr(p)), "ekf_get_map_odom")
+        return p
+
+    def state(self, f=0, sigma=True):
+        x = np.zeros(self.n)
+        S = np.zeros((self.n, self.n)) if sigma else None
+        cnt = C.c_uint(0)
+        _check(lib().ekf_get_state(self.h, f, _ptr(x), _ptr(S), C.byref(cnt)), "ekf_get_state")
+        return x, S, cnt.value
+
+    def set_state(self, state, sigma=None, tmo=None, counter=0, f=0):
+        state = _f64(state)
+        sigma = None if sigma is None else _f64(sigma)
+        tmo = None if tmo is None else _f64(tmo)
+        _check(lib().ekf_set_state(self.h, f, _ptr(state), _ptr(sigma), _ptr(tmo), counter),
+               "ekf_set_state")
+
+    def status(self, f=0) -> int:
+        fl = C.c_uint(0)
+        _check(lib().ekf_get_status(self.h, f, C.byref(fl)), "ekf_get_status")
+        return fl.value
+
+    def profile(self, enable=True):
+        lib().ekf_profile_enable(self.h, int(enable))
+
+    def profile_read(self, kernel):
+        n, ms = C.c_longlong(0), C.c_double(0)
+        _check(lib().ekf_profile_read(self.h, kernel, C.byref(n), C.byref(ms)), "profile_read")
+        return n.value, ms.value
+
+    def sigma_pass_bytes(self, filters=None):
+        return lib().ekf_sigma_pass_bytes(self.h, self.F if filters is None else filters)
+
+
+class Slam:
+    """slam_core: the reference node's callbacks (include/slam_core.h)."""
+
+    def __init__(self, n_landmarks=50, source=SOURCE_SIM, dtype=EKF_F64, track=0.160,
+                 radius=0.033, **kw):
+        self.cfg = make_config(n_landmarks, 1, dtype, **kw)
+        h = C.c_void_p()
+        _check(lib().slam_create(C.byref(h), C.byref(self.cfg), track, radius, source),
+               "slam_create")
+        self.h = h
+        self.n = 3 + 2 * n_landmarks
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().slam_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def joint_states(self, left, right):
+        return lib().slam_joint_states(self.h, float(left), float(right))
+
+    def markers(self, ids, actions, rel_xy):
+        rel = _f64(rel_xy)
+        ids = None if ids is None else _i32(ids)
+        actions = None if actions is None else _i32(actions)
+        return lib().slam_markers(self.h, rel.size // 2, _ptr(ids), _ptr(actions), _ptr(rel))
+
+    def initial_pose(self, x, y, theta):
+        return lib().slam_initial_pose(self.h, x, y, theta)
+
+    def odom(self):
+        p = np.zeros(3)
+        lib().slam_odom(self.h, _ptr(p))
+        return p
+
+    def map_odom(self):
+        p = np.zeros(3)
+        _check(lib().slam_map_odom(self.h, _ptr(p)), "slam_map_odom")
+        return p
+
+    def filter_state(self, sigma=True):
+        ekf = lib().slam_filter(self.h)
+        n = self.n
+        x = np.zeros(n)
+        S = np.zeros((n, n)) if sigma else None
+        cnt = C.c_uint(0)
+        _check(lib().ekf_get_state(ekf, 0, _ptr(x), _ptr(S), C.byref(cnt)), "ekf_get_state")
+        return x, S, cnt.value
+
+    def replay(self, sc, poses=True):
+        """Drive a synth.Scenario (wheel ticks + marker arrays) natively through the node mirror."""
+        T, ticks = sc.wheel.shape[0], sc.wheel.shape[1]
+        M = sc.ids.shape[1]
+        wheel, counts = _f64(sc.wheel), _i32(sc.count)
+        ids, act, rel = _i32(sc.ids), _i32(sc.actions), _f64(sc.rel)
+        out_p = np.zeros((T, 3)) if poses else None
+        out_t = np.zeros((T, 3)) if poses else None
+        rc = lib().slam_replay(self.h, T, ticks, _ptr(wheel), M, _ptr(counts), _ptr(ids),
+                               _ptr(act), _ptr(rel), _ptr(out_p), _ptr(out_t))
+        return rc, out_p, out_t
+
+
+def odometry(sc, track=None, radius=None):
+    """t_odom_robot at each sensor message of a scenario, integrated natively by the product's
+    DiffDrive::fkin (slam_integrate_odometry) — input preparation for ekf_replay."""
+    track = sc.track if track is None else track
+    radius = sc.radius if radius is None else radius
+    wheel = _f64(sc.wheel)
+    T, ticks = wheel.shape[0], wheel.shape[1]
+    out = np.zeros((T, 3))
+    _check(lib().slam_integrate_odometry(track, radius, T, ticks, _ptr(wheel), _ptr(out)),
+           "slam_integrate_odometry")
+    return out

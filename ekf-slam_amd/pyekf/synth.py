@@ -1,0 +1,169 @@
+"""Synthetic EKF-SLAM inputs (the stand-in for nusim's simulator and fake sensor).
+
+This is input generation, not filter math: it plays the role of ``nusim``
+(nusim/src/nusim.cpp:211-289 wheel integration with slip, :310-349 fake landmark sensor) so the
+same odometry + marker streams can be fed to the HIP path, the CPU oracle and the benchmark.
+
+* Robot drives a circle (nuturtle_control/src/circle.cpp:85-86: v = ω·r) sampled at ``tick_hz``
+  joint-state ticks; the sensor fires every ``ticks_per_msg`` ticks (5 Hz at 200 Hz ticks,
+  nusim.cpp:72,89).
+* True wheel angles carry multiplicative slip noise U(-slip, slip) (nusim.cpp:224-227); the encoders
+  report the commanded angles, so odometry drifts from the truth and the EKF has work to do.
+* Each message carries landmark positions in the true body frame plus N(0, σ²) noise on x and y
+  (nusim.cpp:317-346). ``basic_world`` reports every landmark with DELETE beyond ``max_range``
+  (nusim.cpp:332-336); the large synthetic maps report the ``m`` nearest landmarks.
+
+Seeds are explicit; every array is deterministic for a given argument set.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+ADD, DELETE = 0, 2  # visualization_msgs Marker actions
+
+# basic_world.yaml:5-10 and diff_params.yaml:3-4 of the reference
+BASIC_WORLD_LANDMARKS = np.array([[-0.5, -0.7], [0.8, -0.8], [0.4, 0.8], [-0.6, 0.65]])
+BASIC_WORLD_THETA0 = 1.28
+WHEEL_RADIUS = 0.033
+TRACK_WIDTH = 0.160
+
+
+@dataclass
+class Scenario:
+    n_landmarks: int          # filter slots N (state dim 3 + 2N)
+    landmarks: np.ndarray     # [L, 2] true landmark positions, L <= N
+    wheel: np.ndarray         # [T, ticks, 2] encoder wheel angles (left, right), cumulative rad
+    ids: np.ndarray           # [T, M] int32 landmark ids (-1 = padding)
+    actions: np.ndarray       # [T, M] int32 ADD / DELETE
+    rel: np.ndarray           # [T, M, 2] body-frame marker positions (noisy)
+    count: np.ndarray         # [T] markers per message
+    truth: np.ndarray         # [T, 3] true (θ, x, y) at each sensor message
+    track: float = TRACK_WIDTH
+    radius: float = WHEEL_RADIUS
+
+    @property
+    def n_messages(self) -> int:
+        return int(self.ids.shape[0])
+
+    def corrections(self, start: int = 0, stop: int | None = None) -> int:
+        """Number of non-DELETE markers (= EKF correction steps) in messages [start, stop)."""
+        stop = self.n_messages if stop is None else stop
+        c = 0
+        for t in range(start, stop):
+            k = int(self.count[t])
+            c += int(np.count_nonzero(self.actions[t, :k] == ADD))
+        return c
+
+
+def _se2_step(pose, omega, vx):
+    """Exact arc integration of a body twist (same kinematics as turtlelib integrate_twist)."""
+    th, x, y = pose
+    if omega == 0.0:
+        dx, dy = vx, 0.0
+    else:
+        dx = vx / omega * math.sin(omega)
+        dy = vx / omega * (1.0 - math.cos(omega))
+    c, s = math.cos(th), math.sin(th)
+    return (th + omega, x + c * dx - s * dy, y + s * dx + c * dy)
+
+
+def make_scenario(n_landmarks: int, landmarks: np.ndarray, n_messages: int, *,
+                  max_markers: int = 16, nearest: bool = True, start_pose=(0.0, 0.0, -1.0),
+                  circle_radius: float = 1.0, omega: float = 0.5, tick_hz: float = 200.0,
+                  ticks_per_msg: int = 40, sensor_sigma: float = 1e-3, slip: float = 0.02,
+                  max_range: float = 5.0, seed: int = 20240317, shuffle: bool = False,
+                  n_delete: int = 0) -> Scenario:
+    """Generate a drive + sensing sequence. ``start_pose`` is (θ, x, y)."""
+    rng = np.random.default_rng(seed)
+    L = landmarks.shape[0]
+    assert L <= n_landmarks
+    v = omega * circle_radius
+    wr = (v + omega * TRACK_WIDTH / 2.0) / WHEEL_RADIUS
+    wl = (v - omega * TRACK_WIDTH / 2.0) / WHEEL_RADIUS
+    dt = 1.0 / tick_hz
+    m = L if not nearest else min(max_markers, L)
+    M = m + n_delete
+    wheel = np.zeros((n_messages, ticks_per_msg, 2))
+    ids = np.full((n_messages, M), -1, dtype=np.int32)
+    actions = np.zeros((n_messages, M), dtype=np.int32)
+    rel = np.zeros((n_messages, M, 2))
+    count = np.zeros(n_messages, dtype=np.int32)
+    truth = np.zeros((n_messages, 3))
+    enc = np.zeros(2)
+    true_w = np.zeros(2)
+    pose = tuple(float(p) for p in start_pose)
+    for t in range(n_messages):
+        for k in range(ticks_per_msg):
+            cmd = np.array([wl, wr]) * dt
+            enc = enc + cmd
+            slipped = cmd * (1.0 + rng.uniform(-slip, slip, size=2))
+            true_w = true_w + slipped
+            om = WHEEL_RADIUS / TRACK_WIDTH * (-slipped[0] + slipped[1])
+            vx = WHEEL_RADIUS / 2.0 * (slipped[0] + slipped[1])
+            pose = _se2_step(pose, om, vx)
+            wheel[t, k] = enc
+        truth[t] = pose
+        th, x, y = pose
+        c, s = math.cos(th), math.sin(th)
+        d = landmarks - np.array([x, y])
+        # body frame: R(θ)ᵀ (p − x)
+        bx = c * d[:, 0] + s * d[:, 1]
+        by = -s * d[:, 0] + c * d[:, 1]
+        dist = np.hypot(bx, by)
+        if nearest:
+            sel = np.argsort(dist, kind="stable")[:m]
+            sel = sel[dist[sel] <= max_range]
+        else:
+            sel = np.arange(L)
+        if shuffle:
+            sel = rng.permutation(sel)
+        k = len(sel)
+        noise = rng.normal(0.0, sensor_sigma, size=(k, 2))
+        ids[t, :k] = sel
+        rel[t, :k, 0] = bx[sel] + noise[:, 0]
+        rel[t, :k, 1] = by[sel] + noise[:, 1]
+        actions[t, :k] = np.where(dist[sel] <= max_range, ADD, DELETE)
+        if n_delete:
+            far = rng.integers(0, n_landmarks, size=n_delete)
+            ids[t, k:k + n_delete] = far
+            rel[t, k:k + n_delete] = 100.0
+            actions[t, k:k + n_delete] = DELETE
+            k += n_delete
+        count[t] = k
+    return Scenario(n_landmarks, landmarks, wheel, ids, actions, rel, count, truth)
+
+
+def basic_world(n_messages: int = 100, seed: int = 20240317, **kw) -> Scenario:
+    """nusim basic_world (4 landmarks, θ0 = 1.28) in a 50-slot filter (slam.cpp:665)."""
+    kw.setdefault("circle_radius", 0.3)
+    kw.setdefault("nearest", False)
+    return make_scenario(50, BASIC_WORLD_LANDMARKS, n_messages, seed=seed,
+                         start_pose=(BASIC_WORLD_THETA0, 0.0, 0.0), **kw)
+
+
+def random_landmarks(n: int, seed: int = 20240317, circle_radius: float = 1.0,
+                     clearance: float = 0.3) -> np.ndarray:
+    """N landmarks uniform in [-L, L]², L = 0.5·sqrt(N), kept `clearance` m off the circle path."""
+    rng = np.random.default_rng(seed + 7919)
+    half = 0.5 * math.sqrt(n)
+    half = max(half, circle_radius + 2 * clearance + 0.5)
+    out = np.zeros((n, 2))
+    k = 0
+    while k < n:
+        p = rng.uniform(-half, half, size=(2 * n, 2))
+        r = np.hypot(p[:, 0], p[:, 1])
+        p = p[np.abs(r - circle_radius) >= clearance]
+        take = min(n - k, len(p))
+        out[k:k + take] = p[:take]
+        k += take
+    return out
+
+
+def synthetic(n_landmarks: int, n_messages: int, seed: int = 20240317, max_markers: int = 16,
+              **kw) -> Scenario:
+    """SURVEY.md §8d synthetic map: N landmarks, unit circle at ω = 0.5, m nearest markers."""
+    lm = random_landmarks(n_landmarks, seed)
+    return make_scenario(n_landmarks, lm, n_messages, seed=seed, max_markers=max_markers, **kw)

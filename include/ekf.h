@@ -1,0 +1,128 @@
+/*
+ * ekf.h — C-ABI of the MI355X-native EKF-SLAM update path (libekfslam.so).
+ *
+ * Drop-in boundary for the EKF inside maxipalay/ekf-slam's `slam` node (nuslam/src/slam.cpp).
+ * The reference has no predict()/update()/associate() functions: the filter is inline code inside
+ * two ROS 2 subscription callbacks. Each entry point below names the reference lines it replaces.
+ * Plain C types only (no HIP / torch types); every call returns a status code and never throws.
+ *
+ * Threading: one handle is not thread-safe (the reference runs every callback on one executor
+ * thread, slam.cpp:683); distinct handles are independent. The handle owns its device memory and a
+ * private HIP stream; host arrays are caller-owned and copied in. Calls are asynchronous on the
+ * handle's stream unless stated otherwise; ekf_get_* and ekf_sync synchronise.
+ */
+#ifndef EKFSLAM_EKF_H
+#define EKFSLAM_EKF_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define EKF_OK 0
+#define EKF_E_ARG (-1)     /* bad argument / handle */
+#define EKF_E_RANGE (-2)   /* landmark id >= N, or counter_obstacles overflow: the reference's
+                              Armadillo bounds check throws (slam.cpp:213, :351) */
+#define EKF_E_EMPTY (-3)   /* empty MarkerArray: the reference throws at msg.markers.at(0)
+                              (slam.cpp:281, :498) */
+#define EKF_E_NUMERIC (-4) /* singular or non-finite innovation covariance S (slam.cpp:252) */
+#define EKF_E_HIP (-5)     /* HIP runtime error */
+#define EKF_E_NOMEM (-6)
+
+/* status flag bits (ekf_get_status), accumulated on the device */
+#define EKF_FLAG_RANGE 1u
+#define EKF_FLAG_NUMERIC 2u
+
+#define EKF_F64 0
+#define EKF_F32 1 /* Σ stored and contracted in fp32; state and all O(n) math stay fp64 */
+
+#define EKF_MARKER_ADD 0
+#define EKF_MARKER_DELETE 2 /* visualization_msgs::msg::Marker::DELETE (skipped, slam.cpp:205) */
+
+#define EKF_MAX_CHUNK 16 /* markers folded into one Σ pass; longer messages are split */
+
+typedef struct ekf_ctx* ekf_t;
+
+/* Filter parameters. Defaults = the reference's hard-coded members (slam.cpp:665-671, :130). */
+typedef struct {
+  int n_landmarks; /* N, state dim n = 3 + 2N (slam.cpp:665: 50)                 */
+  int n_filters;   /* independent filters in one handle (Monte-Carlo swarm); 1 = one slam node */
+  int dtype;       /* EKF_F64 | EKF_F32                                              */
+  double q_noise;  /* Q̄ = q·I₃ on the pose block (slam.cpp:135-136, :666: 1e-2)     */
+  double r_noise;  /* R = r·I₂ (slam.cpp:139, :667: 1e-2)                          */
+  double init_var; /* landmark prior variance (slam.cpp:130: 10e6 = 1e7)           */
+  double mah_gate; /* Mahalanobis gate on the squared distance (slam.cpp:671: 2.0)  */
+  int device;      /* HIP device ordinal                                            */
+} ekf_config;
+
+void ekf_config_default(ekf_config* cfg);
+const char* ekf_strerror(int status);
+
+/* Filter construction: Σ₀ = diag(0,0,0, init_var·I_2N), state = 0, Q̄, R (slam.cpp:127-139, :674). */
+int ekf_create(ekf_t* out, const ekf_config* cfg);
+int ekf_destroy(ekf_t h);
+/* n = 3+2N, ld = Σ row stride in elements, n_filters */
+int ekf_dims(ekf_t h, int* n, int* ld, int* n_filters);
+
+/* ---- the callbacks (fast path) ---- */
+
+/* t_odom_robot ← DiffDrive::FKin output (slam.cpp:633, jointStateCallback :599-634). */
+int ekf_set_odom(ekf_t h, int filter, double theta, double x, double y);
+
+/* Slam::fake_sensor_cb (slam.cpp:180-316) minus ROS publishing: predict with the current
+ * t_odom_robot, one correction per non-DELETE marker (ids known), posterior t_map_odom.
+ * ids are validated before anything changes (EKF_E_RANGE). rel_xy = body-frame (x, y) pairs. */
+int ekf_fake_sensor(ekf_t h, int filter, int m, const int* ids, const int* actions,
+                    const double* rel_xy);
+
+/* Slam::sensor_cb (slam.cpp:318-530) minus ROS publishing: predict, then per marker the
+ * Mahalanobis nearest-neighbour association (:344-440) and the correction (:443-488).
+ * If assoc_out/is_new_out are non-NULL the call synchronises and returns the decisions. */
+int ekf_sensor(ekf_t h, int filter, int m, const double* rel_xy, int* assoc_out,
+               int* is_new_out);
+
+/* All filters of the handle at once, one message per filter (the swarm / replay path).
+ * counts[F], ids/actions[F][m_max], rel_xy[F][m_max][2], odom[F][3] (t_odom_robot per filter,
+ * NULL = keep). ids may be NULL with assoc=1 (unknown association). Asynchronous. */
+int ekf_batch_sensor(ekf_t h, int assoc, int m_max, const int* counts, const int* ids,
+                     const int* actions, const double* rel_xy, const double* odom);
+
+/* Replay T messages through ekf_batch_sensor (arrays as there, with a leading [T] axis):
+ * counts[T][F], ids/actions[T][F][m_max], rel_xy[T][F][m_max][2], odom[T][F][3].
+ * out_pose[T][F][3] (nullable) receives each posterior pose and makes every message synchronous. */
+int ekf_replay(ekf_t h, int assoc, int T, int m_max, const int* counts, const int* ids,
+               const int* actions, const double* rel_xy, const double* odom, double* out_pose);
+
+/* ---- the finer-grained surface (north_star: predict()/update()/associate()) ---- */
+
+/* Predict (slam.cpp:184-198): deferred and folded into the next Σ pass. */
+int ekf_predict(ekf_t h, int filter);
+/* One known-association correction (slam.cpp:207-268), predict folded in if pending. */
+int ekf_correct(ekf_t h, int filter, int landmark_id, double rel_x, double rel_y);
+/* One association + correction (slam.cpp:345-488). Synchronous when j/is_new non-NULL. */
+int ekf_associate_correct(ekf_t h, int filter, double rel_x, double rel_y, int* j, int* is_new);
+/* Posterior (slam.cpp:273-291): t_map_odom = T(x, y, θ)·t_odom_robot⁻¹. */
+int ekf_posterior(ekf_t h, int filter);
+
+/* ---- state access (synchronising) ---- */
+int ekf_sync(ekf_t h);
+int ekf_get_pose(ekf_t h, int filter, double* theta_x_y);
+int ekf_get_map_odom(ekf_t h, int filter, double* theta_x_y); /* t_map_odom */
+/* state[n] (fp64), sigma[n*n] row-major fp64 (nullable), counter (nullable) */
+int ekf_get_state(ekf_t h, int filter, double* state, double* sigma, unsigned* counter);
+/* overwrite a filter (fixtures / resync after an association flip); t_map_odom nullable */
+int ekf_set_state(ekf_t h, int filter, const double* state, const double* sigma,
+                  const double* t_map_odom, unsigned counter);
+int ekf_get_status(ekf_t h, int filter, unsigned* flags); /* and clears them */
+
+/* ---- measurement ---- */
+/* Per-kernel device time with HIP events on the handle's stream (0 = Σ pass, 1 = gain,
+ * 2 = association). Adds two event records per timed launch; off by default. */
+int ekf_profile_enable(ekf_t h, int enable);
+int ekf_profile_read(ekf_t h, int kernel, long long* launches, double* total_ms);
+/* Bytes the Σ pass must move per launch for the current handle (2·n²·w·F). */
+double ekf_sigma_pass_bytes(ekf_t h, int filters_in_launch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

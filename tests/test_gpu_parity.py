@@ -1,0 +1,225 @@
+"""HIP path (through the C-ABI) against the golden fixtures and the C oracle.
+
+Tolerances (fp64): posterior poses / state 1e-8, Σ 1e-8 absolute (1e-15 of the reference's 1e7
+prior variance, slam.cpp:130), association decisions exact. The HIP path folds a message's
+corrections into one rank-(2+2m) Σ pass, so its summation order differs from the reference's
+sequential dense algebra; the results agree to rounding.
+"""
+import numpy as np
+import pytest
+
+import orc
+import pyekf
+from conftest import GOLDEN_CASES, load_golden
+from pyekf import synth
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-8
+SIGMA_TOL = 1e-8
+
+
+def _replay_node(sc, assoc, dtype=pyekf.EKF_F64):
+    s = pyekf.Slam(n_landmarks=sc.n_landmarks,
+                   source=pyekf.SOURCE_ASSOC if assoc else pyekf.SOURCE_SIM, dtype=dtype,
+                   track=sc.track, radius=sc.radius)
+    rc, poses, tmo = s.replay(sc)
+    x, S, cnt = s.filter_state()
+    return rc, poses, tmo, x, S, cnt, s
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+def test_node_replay_matches_golden(name):
+    sc, g = load_golden(name)
+    rc, poses, tmo, x, S, cnt, _ = _replay_node(sc, bool(g["assoc"]))
+    assert rc == pyekf.EKF_OK
+    assert np.abs(poses - g["poses"]).max() < POSE_TOL
+    assert np.abs(tmo - g["tmo"]).max() < POSE_TOL
+    assert np.abs(x - g["state"]).max() < POSE_TOL
+    assert np.abs(S - g["sigma"]).max() < SIGMA_TOL
+    assert cnt == int(g["counter"])
+
+
+@pytest.mark.parametrize("name", [c for c in GOLDEN_CASES if "assoc" in c])
+def test_association_decisions_match_golden(name):
+    sc, g = load_golden(name)
+    ekf = pyekf.EKF(n_landmarks=sc.n_landmarks)
+    odom = pyekf.odometry(sc)
+    for t in range(sc.n_messages):
+        ekf.set_odom(odom[t])
+        c = int(sc.count[t])
+        rc, j, nw = ekf.sensor(sc.rel[t, :c])
+        assert rc == 0
+        assert np.array_equal(j, g["assoc_j"][t, :c]), t
+        assert np.array_equal(nw, g["assoc_new"][t, :c]), t
+    assert np.abs(ekf.pose() - g["poses"][-1]).max() < POSE_TOL
+
+
+def test_fine_grained_surface_equals_callback():
+    """predict()/correct()/posterior() one marker at a time == fake_sensor_cb (slam.cpp:180-316)."""
+    sc, g = load_golden("basic_world_known")
+    ekf = pyekf.EKF(n_landmarks=sc.n_landmarks)
+    odom = pyekf.odometry(sc)
+    for t in range(sc.n_messages):
+        ekf.set_odom(odom[t])
+        assert ekf.predict() == 0
+        for i in range(int(sc.count[t])):
+            if sc.actions[t, i] == pyekf.DELETE:
+                continue
+            assert ekf.correct(sc.ids[t, i], *sc.rel[t, i]) == 0
+        assert ekf.posterior() == 0
+        assert np.abs(ekf.pose() - g["poses"][t]).max() < POSE_TOL
+        assert np.abs(ekf.map_odom() - g["tmo"][t]).max() < POSE_TOL
+    x, S, _ = ekf.state()
+    assert np.abs(S - g["sigma"]).max() < SIGMA_TOL
+
+
+def test_fine_grained_associate_equals_callback():
+    sc, g = load_golden("synth16_assoc")
+    ekf = pyekf.EKF(n_landmarks=sc.n_landmarks)
+    odom = pyekf.odometry(sc)
+    for t in range(sc.n_messages):
+        ekf.set_odom(odom[t])
+        ekf.predict()
+        for i in range(int(sc.count[t])):
+            rc, j, nw = ekf.associate_correct(*sc.rel[t, i])
+            assert rc == 0 and j == g["assoc_j"][t, i] and nw == g["assoc_new"][t, i]
+        ekf.posterior()
+    assert np.abs(ekf.pose() - g["poses"][-1]).max() < POSE_TOL
+
+
+@pytest.mark.parametrize("assoc", [False, True], ids=["known", "assoc"])
+def test_batched_filters_match_oracle(assoc):
+    """8 independent filters in one handle (the swarm layout), each vs its own oracle run."""
+    F, T, N = 8, 30, 20
+    scs = [synth.make_scenario(N, synth.random_landmarks(12, seed=100 + f), T, max_markers=6,
+                               seed=200 + f, shuffle=assoc) for f in range(F)]
+    M = max(s.ids.shape[1] for s in scs)
+    counts = np.zeros((T, F), np.int32)
+    ids = np.full((T, F, M), -1, np.int32)
+    act = np.zeros((T, F, M), np.int32)
+    rel = np.zeros((T, F, M, 2))
+    odom = np.zeros((T, F, 3))
+    for f, s in enumerate(scs):
+        m = s.ids.shape[1]
+        counts[:, f] = s.count
+        ids[:, f, :m] = s.ids
+        act[:, f, :m] = s.actions
+        rel[:, f, :m] = s.rel
+        odom[:, f] = pyekf.odometry(s)
+    ekf = pyekf.EKF(n_landmarks=N, n_filters=F)
+    poses = ekf.replay(counts, rel, odom, ids=None if assoc else ids, actions=act, assoc=assoc,
+                       poses=True)
+    for f, s in enumerate(scs):
+        o = orc.run_scenario(s, assoc)
+        assert np.abs(poses[:, f] - o["poses"]).max() < POSE_TOL, f
+        x, S, cnt = ekf.state(f)
+        assert np.abs(S - o["sigma"]).max() < SIGMA_TOL, f
+        assert cnt == o["counter"]
+
+
+def test_long_message_is_chunked():
+    """40 markers in one message → three Σ passes (EKF_MAX_CHUNK = 16), same result."""
+    lm = synth.random_landmarks(40, seed=3)
+    sc = synth.make_scenario(50, lm, 12, max_markers=40, seed=4)
+    assert sc.count.max() > 16
+    rc, poses, tmo, x, S, cnt, _ = _replay_node(sc, False)
+    o = orc.run_scenario(sc, False)
+    assert rc == 0
+    assert np.abs(poses - o["poses"]).max() < POSE_TOL
+    assert np.abs(S - o["sigma"]).max() < SIGMA_TOL
+
+
+def test_repeated_landmark_in_one_message():
+    """The same id twice in one message (two copies of its rows in the touched-index set)."""
+    ekf = pyekf.EKF(n_landmarks=6)
+    ref = orc.OracleEKF(n_landmarks=6)
+    rng = np.random.default_rng(0)
+    for t in range(10):
+        od = (0.05 * t, 0.1 * t, 0.02 * t)
+        ekf.set_odom(od)
+        ref.set_odom(od)
+        ids = np.array([1, 3, 1, 1, 4], np.int32)
+        rel = np.array([[1.0, 0.2], [0.5, -1.0], [1.0, 0.2], [1.0, 0.21], [-0.7, 0.4]])
+        rel = rel + rng.normal(0, 1e-3, rel.shape)
+        assert ekf.fake_sensor(ids, np.zeros(5, np.int32), rel) == 0
+        assert ref.fake_sensor_cb(ids, np.zeros(5, np.int32), rel) == 0
+    x, S, _ = ekf.state()
+    xr, Sr, _, _ = ref.get()
+    assert np.abs(x - xr).max() < POSE_TOL
+    assert np.abs(S - Sr).max() < SIGMA_TOL
+
+
+def test_error_paths():
+    ekf = pyekf.EKF(n_landmarks=3)
+    x0, S0, _ = ekf.state()
+    assert ekf.fake_sensor(np.array([3]), np.array([0]), np.array([[1.0, 0.5]])) == \
+        pyekf.EKF_E_RANGE
+    assert ekf.fake_sensor(np.zeros(0), np.zeros(0), np.zeros((0, 2))) == pyekf.EKF_E_EMPTY
+    x1, S1, _ = ekf.state()
+    assert np.array_equal(x0, x1) and np.array_equal(S0, S1)  # rejected atomically
+    # DELETE-only message: predict only
+    ekf.set_odom((0.1, 0.2, 0.0))
+    assert ekf.fake_sensor(np.array([0, 1]), np.array([2, 2]), np.ones((2, 2))) == 0
+    x, S, _ = ekf.state()
+    assert np.allclose(x[:3], [0.1, 0.2, 0.0]) and np.all(x[3:] == 0)
+    # capacity overflow on the association path (the reference indexes past the state)
+    pts = np.array([[1.0, 0.0], [0.0, 3.0], [-4.0, 0.0], [0.0, -5.0]])
+    rc, j, nw = ekf.sensor(pts)
+    assert rc == pyekf.EKF_E_RANGE and list(nw[:3]) == [1, 1, 1] and j[3] == -1
+    assert ekf.status() & pyekf.EKF_FLAG_RANGE
+
+
+def test_set_get_state_roundtrip():
+    sc, g = load_golden("synth16_known")
+    ekf = pyekf.EKF(n_landmarks=sc.n_landmarks)
+    ekf.set_state(g["state"], g["sigma"], tmo=g["tmo"][-1], counter=7)
+    x, S, cnt = ekf.state()
+    assert np.array_equal(x, g["state"]) and np.array_equal(S, g["sigma"]) and cnt == 7
+    assert np.array_equal(ekf.map_odom(), g["tmo"][-1])
+
+
+def test_n256_fp64_against_oracle():
+    """BASELINE config 2 size (N=256, fp64) over 25 messages × 16 markers, vs the C oracle."""
+    sc = synth.synthetic(256, 25)
+    rc, poses, tmo, x, S, cnt, _ = _replay_node(sc, False)
+    o = orc.run_scenario(sc, False)
+    assert rc == 0
+    assert np.abs(poses - o["poses"]).max() < 1e-7
+    assert np.abs(S - o["sigma"]).max() < 1e-7
+
+
+def test_n1024_fp32_warm_state_against_oracle():
+    """BASELINE config 3 (N=1024, fp32 Σ): warm state from an fp64 pass, then fp32 vs fp64 oracle.
+
+    fp32 cannot take a first sighting against the 1e7 prior (1e7 − (1e7 − 1e-2) in fp32 is
+    noise), so the fp32 filter starts from the state of an fp64 lap. Tolerance:
+    posterior positions within 2e-4 m and headings within 2e-4 rad of the fp64 oracle after 40
+    messages (640 corrections)."""
+    N, warm, T = 1024, 63, 40
+    sc = synth.synthetic(N, warm + T)
+    odom = pyekf.odometry(sc)
+    M = sc.ids.shape[1]
+    ekf64 = pyekf.EKF(n_landmarks=N)
+    ekf64.replay(sc.count[:warm, None], sc.rel[:warm, None], odom[:warm, None],
+                 ids=sc.ids[:warm, None], actions=sc.actions[:warm, None])
+    x, S, cnt = ekf64.state()
+    tmo = ekf64.map_odom()
+    ekf64.close()
+    ekf32 = pyekf.EKF(n_landmarks=N, dtype=pyekf.EKF_F32)
+    ekf32.set_state(x, S, tmo=tmo, counter=cnt)
+    ref = orc.OracleEKF(n_landmarks=N)
+    ref.set(x, S, tmo, x[:3], cnt)
+    poses = ekf32.replay(sc.count[warm:, None], sc.rel[warm:, None], odom[warm:, None],
+                         ids=sc.ids[warm:, None], actions=sc.actions[warm:, None], poses=True)
+    for t in range(T):
+        ref.set_odom(odom[warm + t])
+        c = int(sc.count[warm + t])
+        ref.fake_sensor_cb(sc.ids[warm + t, :c], sc.actions[warm + t, :c], sc.rel[warm + t, :c])
+        xr, _, _, _ = ref.get(sigma=False)
+        d = np.abs(poses[t, 0] - xr[:3])
+        assert d.max() < 2e-4, (t, d)
+    x32, S32, _ = ekf32.state()
+    seen = np.abs(np.diag(S32)) < 1e6
+    assert np.all(np.diag(S32)[seen][3:] > 0)
+    assert np.all(np.isfinite(S32))
