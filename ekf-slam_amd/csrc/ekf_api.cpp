@@ -24,6 +24,19 @@ struct Marker {
   double zr, zb;
 };
 
+struct Launch {
+  int kind;    // 0 = gain + Σ pass, 1 = association + gain + Σ pass, 2 = posterior only
+  size_t off;  // first descriptor
+  int f0, nf, kw;
+};
+
+struct StageSlot {
+  MsgDesc* p = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool used = false;
+};
+
 struct ProfEvents {
   std::vector<hipEvent_t> start, stop;
 };
@@ -42,16 +55,17 @@ struct ekf_ctx {
   FilterCtl* ctl = nullptr;
   MsgDesc* ddesc = nullptr;
   size_t sig_stride = 0, x_stride = 0, km_stride = 0;
-  size_t desc_cap = 0;  // descriptors per upload
   // host mirror
   std::vector<Pose2> odom;
   std::vector<int> parity;
   std::vector<char> pending;
-  // staging ring
-  MsgDesc* pinned = nullptr;
+  // launch plan: descriptors for a whole call (or a whole replay) uploaded with ONE copy
+  std::vector<MsgDesc> plan_d;
+  std::vector<Launch> plan_l;
+  size_t ddesc_cap = 0;
+  // pinned staging ring (the host may run kRing uploads ahead of the device)
+  StageSlot ring[kRing];
   int ring_next = 0;
-  hipEvent_t ring_ev[kRing] = {};
-  bool ring_used[kRing] = {};
   // scratch
   std::vector<std::vector<Marker>> msgs;
   // profiling
@@ -123,23 +137,6 @@ int timed(ekf_ctx* h, int kind, Fn fn) {
   return e == hipSuccess ? EKF_OK : EKF_E_HIP;
 }
 
-// Reserve `count` descriptors in the next pinned staging slot.
-MsgDesc* stage(ekf_ctx* h, int* slot) {
-  const int s = h->ring_next;
-  h->ring_next = (h->ring_next + 1) % kRing;
-  if (h->ring_used[s]) hipEventSynchronize(h->ring_ev[s]);
-  *slot = s;
-  return h->pinned + static_cast<size_t>(s) * h->desc_cap;
-}
-
-int upload(ekf_ctx* h, int slot, size_t count) {
-  const MsgDesc* src = h->pinned + static_cast<size_t>(slot) * h->desc_cap;
-  HIPCHK(hipMemcpyAsync(h->ddesc, src, count * sizeof(MsgDesc), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipEventRecord(h->ring_ev[slot], h->stream));
-  h->ring_used[slot] = true;
-  return EKF_OK;
-}
-
 void fill_desc(MsgDesc* d, int m, int flags, int parity, const Pose2& odom) {
   std::memset(d, 0, sizeof(MsgDesc));
   d->m = m;
@@ -179,116 +176,181 @@ int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
 }
 
 // Known association, one message per filter in [f0, f0+nf): msgs[k] holds filter f0+k's markers.
-// Predict + chunks of ≤ kMaxChunk corrections + posterior (slam.cpp:180-316).
-int run_known(ekf_ctx* h, int f0, int nf, bool predict) {
+// Predict + chunks of ≤ kMaxChunk corrections + posterior (slam.cpp:180-316), appended to the plan.
+void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
   int chunks = 1;
   for (int k = 0; k < nf; ++k)
     chunks = std::max(chunks, static_cast<int>((h->msgs[k].size() + kMaxChunk - 1) / kMaxChunk));
-  for (int c0 = 0; c0 < chunks;) {
-    const int cn = std::min(chunks - c0, static_cast<int>(h->desc_cap / nf));
-    int slot;
-    MsgDesc* st = stage(h, &slot);
-    std::vector<int> kws(cn, 4);
-    for (int c = 0; c < cn; ++c) {
-      const int chunk = c0 + c;
-      for (int k = 0; k < nf; ++k) {
-        const int f = f0 + k;
-        const auto& mk = h->msgs[k];
-        const int nk = static_cast<int>((mk.size() + kMaxChunk - 1) / kMaxChunk);
-        const int nchunks = std::max(nk, 1);
-        MsgDesc* d = st + static_cast<size_t>(c) * nf + k;
-        if (chunk >= nchunks) {
-          std::memset(d, 0, sizeof(MsgDesc));
-          continue;
-        }
-        const int b = chunk * kMaxChunk;
-        const int m = std::min(kMaxChunk, static_cast<int>(mk.size()) - b);
-        int flags = kActive;
-        if (chunk == 0 && (predict || h->pending[f])) flags |= kFirst;
-        if (chunk == nchunks - 1 && predict) flags |= kLast;
-        fill_desc(d, std::max(m, 0), flags, h->parity[f], h->odom[f]);
-        for (int i = 0; i < m; ++i) {
-          d->ids[i] = mk[b + i].id;
-          d->z[i][0] = mk[b + i].zr;
-          d->z[i][1] = mk[b + i].zb;
-        }
-        h->parity[f] ^= 1;
-        kws[c] = std::max(kws[c], ((2 + 2 * std::max(m, 0) + 3) / 4) * 4);
-        if (chunk == 0) h->pending[f] = 0;
+  for (int chunk = 0; chunk < chunks; ++chunk) {
+    const size_t off = h->plan_d.size();
+    h->plan_d.resize(off + nf);
+    int kw = 4;
+    for (int k = 0; k < nf; ++k) {
+      const int f = f0 + k;
+      const auto& mk = h->msgs[k];
+      const int nchunks = std::max(1, static_cast<int>((mk.size() + kMaxChunk - 1) / kMaxChunk));
+      MsgDesc* d = &h->plan_d[off + k];
+      if (chunk >= nchunks) {
+        std::memset(d, 0, sizeof(MsgDesc));
+        continue;
+      }
+      const int b = chunk * kMaxChunk;
+      const int m = std::max(0, std::min(kMaxChunk, static_cast<int>(mk.size()) - b));
+      int flags = kActive;
+      if (chunk == 0 && (predict || h->pending[f])) flags |= kFirst;
+      if (chunk == nchunks - 1 && predict) flags |= kLast;
+      fill_desc(d, m, flags, h->parity[f], h->odom[f]);
+      for (int i = 0; i < m; ++i) {
+        d->ids[i] = mk[b + i].id;
+        d->z[i][0] = mk[b + i].zr;
+        d->z[i][1] = mk[b + i].zb;
+      }
+      h->parity[f] ^= 1;
+      kw = std::max(kw, ((2 + 2 * m + 3) / 4) * 4);
+      if (chunk == 0) h->pending[f] = 0;
+    }
+    h->plan_l.push_back(Launch{0, off, f0, nf, kw});
+  }
+}
+
+// Unknown association (slam.cpp:318-530), markers [i0, i1) of each filter's message: per marker the
+// association kernel + a single-marker launch pair. Decisions land in FilterCtl::assoc_j/new at
+// slot i % kMaxAssoc.
+void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0, int i1) {
+  for (int i = i0; i < i1; ++i) {
+    const size_t off = h->plan_d.size();
+    h->plan_d.resize(off + nf);
+    for (int k = 0; k < nf; ++k) {
+      const int f = f0 + k;
+      const auto& mk = h->msgs[k];
+      const int mf = static_cast<int>(mk.size());
+      MsgDesc* d = &h->plan_d[off + k];
+      if (i >= std::max(mf, 1)) {
+        std::memset(d, 0, sizeof(MsgDesc));
+        continue;
+      }
+      int flags = kActive | kNoInit;
+      if (i == 0 && (predict || h->pending[f])) flags |= kFirst;
+      if (i == std::max(mf, 1) - 1 && posterior) flags |= kLast;
+      const int m = mf > 0 ? 1 : 0;
+      fill_desc(d, m, flags, h->parity[f], h->odom[f]);
+      d->assoc_slot = i % kMaxAssoc;
+      if (m) {
+        d->ids[0] = -1;
+        d->z[0][0] = mk[i].zr;
+        d->z[0][1] = mk[i].zb;
+      }
+      h->parity[f] ^= 1;
+      if (i == 0) h->pending[f] = 0;
+    }
+    h->plan_l.push_back(Launch{1, off, f0, nf, 4});
+  }
+}
+
+void plan_posterior(ekf_ctx* h, int f) {
+  const size_t off = h->plan_d.size();
+  h->plan_d.resize(off + 1);
+  fill_desc(&h->plan_d[off], 0, kActive, h->parity[f], h->odom[f]);
+  h->plan_l.push_back(Launch{2, off, f, 1, 4});
+}
+
+int posterior_launch(ekf_ctx* h, const MsgDesc* dp, int f0, int nf) {
+  const hipError_t e =
+      h->cfg.dtype == EKF_F32
+          ? launch_posterior<float>(args<float>(h, dp, f0), nf, h->stream)
+          : launch_posterior<double>(args<double>(h, dp, f0), nf, h->stream);
+  return e == hipSuccess ? EKF_OK : EKF_E_HIP;
+}
+
+// Upload the whole plan with one copy, then enqueue its launches in order.
+int flush(ekf_ctx* h) {
+  const size_t nd = h->plan_d.size();
+  if (nd == 0) return EKF_OK;
+  if (nd > h->ddesc_cap) {  // grow the device descriptor buffer (kernels may still read the old one)
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (h->ddesc) HIPCHK(hipFree(h->ddesc));
+    h->ddesc = nullptr;
+    const size_t cap = std::max(nd, 2 * h->ddesc_cap);
+    if (hipMalloc(&h->ddesc, cap * sizeof(MsgDesc)) != hipSuccess) return EKF_E_NOMEM;
+    h->ddesc_cap = cap;
+  }
+  StageSlot& sl = h->ring[h->ring_next];
+  h->ring_next = (h->ring_next + 1) % kRing;
+  if (sl.used) HIPCHK(hipEventSynchronize(sl.ev));
+  if (nd > sl.cap) {
+    if (sl.p) HIPCHK(hipHostFree(sl.p));
+    sl.p = nullptr;
+    const size_t cap = std::max<size_t>(nd, 64);
+    if (hipHostMalloc(reinterpret_cast<void**>(&sl.p), cap * sizeof(MsgDesc),
+                      hipHostMallocDefault) != hipSuccess)
+      return EKF_E_NOMEM;
+    sl.cap = cap;
+  }
+  std::memcpy(sl.p, h->plan_d.data(), nd * sizeof(MsgDesc));
+  HIPCHK(hipMemcpyAsync(h->ddesc, sl.p, nd * sizeof(MsgDesc), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipEventRecord(sl.ev, h->stream));
+  sl.used = true;
+  int rc = EKF_OK;
+  for (const Launch& L : h->plan_l) {
+    const MsgDesc* dp = h->ddesc + L.off;
+    if (L.kind == 1) rc = assoc(h, dp, L.f0, L.nf);
+    if (!rc && L.kind <= 1) rc = pair(h, dp, L.f0, L.nf, L.kw);
+    if (!rc && L.kind == 2) rc = posterior_launch(h, dp, L.f0, L.nf);
+    if (rc) break;
+  }
+  h->plan_d.clear();
+  h->plan_l.clear();
+  return rc;
+}
+
+// Association with the decisions read back (synchronous), kMaxAssoc markers per upload.
+int assoc_sync(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int m_max, int* j_out,
+               int* new_out) {
+  int mm = 1;
+  for (int k = 0; k < nf; ++k) mm = std::max(mm, static_cast<int>(h->msgs[k].size()));
+  for (int i0 = 0; i0 < mm; i0 += kMaxAssoc) {
+    const int i1 = std::min(mm, i0 + kMaxAssoc);
+    plan_assoc(h, f0, nf, predict, posterior && i1 == mm, i0, i1);
+    int rc = flush(h);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    for (int k = 0; k < nf; ++k) {
+      FilterCtl c;
+      HIPCHK(hipMemcpy(&c, h->ctl + f0 + k, sizeof(FilterCtl), hipMemcpyDeviceToHost));
+      const int mf = static_cast<int>(h->msgs[k].size());
+      for (int i = i0; i < std::min(i1, mf); ++i) {
+        if (j_out) j_out[static_cast<size_t>(k) * m_max + i] = c.assoc_j[i % kMaxAssoc];
+        if (new_out) new_out[static_cast<size_t>(k) * m_max + i] = c.assoc_new[i % kMaxAssoc];
       }
     }
-    int rc = upload(h, slot, static_cast<size_t>(cn) * nf);
-    if (rc) return rc;
-    for (int c = 0; c < cn; ++c) {
-      rc = pair(h, h->ddesc + static_cast<size_t>(c) * nf, f0, nf, kws[c]);
-      if (rc) return rc;
-    }
-    c0 += cn;
   }
   return EKF_OK;
 }
 
-// Unknown association (slam.cpp:318-530): markers one at a time, each = association kernel +
-// single-marker launch pair. Decisions land in FilterCtl::assoc_j/new; read back when requested.
-int run_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int m_max, int* j_out,
-              int* new_out) {
-  int mm = 0;
-  for (int k = 0; k < nf; ++k) mm = std::max(mm, static_cast<int>(h->msgs[k].size()));
-  const int steps = std::max(mm, 1);
-  const int per_upload = std::max(1, std::min(kMaxAssoc, static_cast<int>(h->desc_cap / nf)));
-  for (int i0 = 0; i0 < steps; i0 += per_upload) {
-    const int cn = std::min(per_upload, steps - i0);
-    int slot;
-    MsgDesc* st = stage(h, &slot);
-    for (int c = 0; c < cn; ++c) {
-      const int i = i0 + c;
-      for (int k = 0; k < nf; ++k) {
-        const int f = f0 + k;
-        const auto& mk = h->msgs[k];
-        const int mf = static_cast<int>(mk.size());
-        MsgDesc* d = st + static_cast<size_t>(c) * nf + k;
-        const bool active = i < std::max(mf, 1);
-        if (!active) {
-          std::memset(d, 0, sizeof(MsgDesc));
-          continue;
-        }
-        int flags = kActive | kNoInit;
-        if (i == 0 && (predict || h->pending[f])) flags |= kFirst;
-        if (i == std::max(mf, 1) - 1 && posterior) flags |= kLast;
-        const int m = mf > 0 ? 1 : 0;
-        fill_desc(d, m, flags, h->parity[f], h->odom[f]);
-        d->assoc_slot = c;
-        if (m) {
-          d->ids[0] = -1;
-          d->z[0][0] = mk[i].zr;
-          d->z[0][1] = mk[i].zb;
-        }
-        h->parity[f] ^= 1;
-        if (i == 0) h->pending[f] = 0;
+// Parse one message per filter (ekf_batch_sensor layout) into h->msgs.
+int load_batch(ekf_ctx* h, int assoc_mode, int m_max, const int* counts, const int* ids,
+               const int* actions, const double* rel_xy, const double* odom) {
+  for (int f = 0; f < h->F; ++f) {
+    const int c = counts[f];
+    if (c < 0 || c > m_max) return EKF_E_ARG;
+    if (!assoc_mode)
+      for (int i = 0; i < c; ++i) {
+        const size_t e = static_cast<size_t>(f) * m_max + i;
+        if (actions && actions[e] == EKF_MARKER_DELETE) continue;
+        if (ids[e] < 0 || ids[e] >= h->cfg.n_landmarks) return EKF_E_RANGE;
       }
-    }
-    int rc = upload(h, slot, static_cast<size_t>(cn) * nf);
-    if (rc) return rc;
-    for (int c = 0; c < cn; ++c) {
-      const MsgDesc* dp = h->ddesc + static_cast<size_t>(c) * nf;
-      rc = assoc(h, dp, f0, nf);
-      if (rc) return rc;
-      rc = pair(h, dp, f0, nf, 4);
-      if (rc) return rc;
-    }
-    if (j_out || new_out) {
-      HIPCHK(hipStreamSynchronize(h->stream));
-      for (int k = 0; k < nf; ++k) {
-        FilterCtl c;
-        HIPCHK(hipMemcpy(&c, h->ctl + f0 + k, sizeof(FilterCtl), hipMemcpyDeviceToHost));
-        const int mf = static_cast<int>(h->msgs[k].size());
-        for (int c2 = 0; c2 < cn; ++c2) {
-          const int i = i0 + c2;
-          if (i >= mf) continue;
-          if (j_out) j_out[static_cast<size_t>(k) * m_max + i] = c.assoc_j[c2];
-          if (new_out) new_out[static_cast<size_t>(k) * m_max + i] = c.assoc_new[c2];
-        }
-      }
+  }
+  for (int f = 0; f < h->F; ++f) {
+    if (odom) h->odom[f] = Pose2{odom[3 * f], odom[3 * f + 1], odom[3 * f + 2]};
+    auto& mk = h->msgs[f];
+    mk.clear();
+    for (int i = 0; i < counts[f]; ++i) {
+      const size_t e = static_cast<size_t>(f) * m_max + i;
+      if (!assoc_mode && actions && actions[e] == EKF_MARKER_DELETE) continue;
+      Marker k;
+      k.id = assoc_mode ? -1 : ids[e];
+      measure(rel_xy[2 * e], rel_xy[2 * e + 1], &k.zr, &k.zb);
+      mk.push_back(k);
     }
   }
   return EKF_OK;
@@ -345,7 +407,6 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   h->sig_stride = static_cast<size_t>(h->n) * h->ld;
   h->x_stride = static_cast<size_t>((h->n + 15) / 16 * 16);
   h->km_stride = static_cast<size_t>(kMaxKW) * h->ldk;
-  h->desc_cap = static_cast<size_t>(h->F) * kMaxAssoc;
   h->odom.assign(h->F, Pose2{});
   h->parity.assign(h->F, 0);
   h->pending.assign(h->F, 0);
@@ -367,12 +428,10 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipMalloc(&h->kcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->mcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->ctl, sizeof(FilterCtl) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
-  if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->desc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
-  if (hipHostMalloc(reinterpret_cast<void**>(&h->pinned), sizeof(MsgDesc) * h->desc_cap * kRing,
-                    hipHostMallocDefault) != hipSuccess)
-    return fail(EKF_E_NOMEM);
+  h->ddesc_cap = static_cast<size_t>(h->F) * 4;
+  if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->ddesc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
   for (int i = 0; i < kRing; ++i)
-    if (hipEventCreateWithFlags(&h->ring_ev[i], hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&h->ring[i].ev, hipEventDisableTiming) != hipSuccess)
       return fail(EKF_E_HIP);
   // Σ₀ = diag(0,0,0, init_var·I_2N), state = 0 (slam.cpp:127-132, :674)
   for (int p = 0; p < 2; ++p) {
@@ -406,9 +465,10 @@ int ekf_destroy(ekf_t h) {
   if (h->mcat) hipFree(h->mcat);
   if (h->ctl) hipFree(h->ctl);
   if (h->ddesc) hipFree(h->ddesc);
-  if (h->pinned) hipHostFree(h->pinned);
-  for (int i = 0; i < kRing; ++i)
-    if (h->ring_ev[i]) hipEventDestroy(h->ring_ev[i]);
+  for (int i = 0; i < kRing; ++i) {
+    if (h->ring[i].p) hipHostFree(h->ring[i].p);
+    if (h->ring[i].ev) hipEventDestroy(h->ring[i].ev);
+  }
   for (auto& pe : h->pe) {
     for (auto e : pe.start) hipEventDestroy(e);
     for (auto e : pe.stop) hipEventDestroy(e);
@@ -448,7 +508,8 @@ int ekf_fake_sensor(ekf_t h, int f, int m, const int* ids, const int* actions,
     mk.push_back(k);
   }
   hipSetDevice(h->cfg.device);
-  return run_known(h, f, 1, true);
+  plan_known(h, f, 1, true);
+  return flush(h);
 }
 
 int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int* is_new_out) {
@@ -463,9 +524,13 @@ int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int*
     mk.push_back(k);
   }
   hipSetDevice(h->cfg.device);
-  const int rc = run_assoc(h, f, 1, true, true, m, assoc_out, is_new_out);
+  if (!assoc_out && !is_new_out) {
+    plan_assoc(h, f, 1, true, true, 0, m);
+    return flush(h);
+  }
+  const int rc = assoc_sync(h, f, 1, true, true, m, assoc_out, is_new_out);
   if (rc) return rc;
-  if (assoc_out || is_new_out) {
+  {
     unsigned fl = 0;
     HIPCHK(hipMemcpy(&fl, &h->ctl[f].status, sizeof(unsigned), hipMemcpyDeviceToHost));
     if (fl & EKF_FLAG_RANGE) return EKF_E_RANGE;
@@ -477,47 +542,51 @@ int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, cons
                      const int* actions, const double* rel_xy, const double* odom) {
   if (!h || m_max < 0 || !counts || (m_max > 0 && !rel_xy) || (!assoc_mode && m_max > 0 && !ids))
     return EKF_E_ARG;
-  for (int f = 0; f < h->F; ++f) {
-    if (odom) h->odom[f] = Pose2{odom[3 * f], odom[3 * f + 1], odom[3 * f + 2]};
-    auto& mk = h->msgs[f];
-    mk.clear();
-    const int c = counts[f];
-    if (c < 0 || c > m_max) return EKF_E_ARG;
-    for (int i = 0; i < c; ++i) {
-      const size_t e = static_cast<size_t>(f) * m_max + i;
-      if (!assoc_mode) {
-        if (actions && actions[e] == EKF_MARKER_DELETE) continue;
-        if (ids[e] < 0 || ids[e] >= h->cfg.n_landmarks) return EKF_E_RANGE;
-      }
-      Marker k;
-      k.id = assoc_mode ? -1 : ids[e];
-      measure(rel_xy[2 * e], rel_xy[2 * e + 1], &k.zr, &k.zb);
-      mk.push_back(k);
-    }
-  }
+  const int rc = load_batch(h, assoc_mode, m_max, counts, ids, actions, rel_xy, odom);
+  if (rc) return rc;
   hipSetDevice(h->cfg.device);
-  return assoc_mode ? run_assoc(h, 0, h->F, true, true, m_max, nullptr, nullptr)
-                    : run_known(h, 0, h->F, true);
+  if (assoc_mode) {
+    int mm = 1;
+    for (int f = 0; f < h->F; ++f) mm = std::max(mm, static_cast<int>(h->msgs[f].size()));
+    plan_assoc(h, 0, h->F, true, true, 0, mm);
+  } else {
+    plan_known(h, 0, h->F, true);
+  }
+  return flush(h);
 }
 
 int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, const int* ids,
                const int* actions, const double* rel_xy, const double* odom, double* out_pose) {
-  if (!h || T < 0 || !counts || !odom) return EKF_E_ARG;
+  if (!h || T < 0 || !counts || !odom || m_max < 0 || (m_max > 0 && !rel_xy) ||
+      (!assoc_mode && m_max > 0 && !ids))
+    return EKF_E_ARG;
   const size_t F = static_cast<size_t>(h->F);
+  hipSetDevice(h->cfg.device);
   for (int t = 0; t < T; ++t) {
     const size_t o = static_cast<size_t>(t) * F * m_max;
-    const int rc = ekf_batch_sensor(h, assoc_mode, m_max, counts + t * F, ids ? ids + o : nullptr,
-                                    actions ? actions + o : nullptr, rel_xy + 2 * o,
-                                    odom + 3 * F * t);
-    if (rc) return rc;
+    int rc = load_batch(h, assoc_mode, m_max, counts + t * F, ids ? ids + o : nullptr,
+                        actions ? actions + o : nullptr, rel_xy + 2 * o, odom + 3 * F * t);
+    if (rc) {
+      flush(h);
+      return rc;
+    }
+    if (assoc_mode) {
+      int mm = 1;
+      for (size_t f = 0; f < F; ++f) mm = std::max(mm, static_cast<int>(h->msgs[f].size()));
+      plan_assoc(h, 0, h->F, true, true, 0, mm);
+    } else {
+      plan_known(h, 0, h->F, true);
+    }
     if (out_pose) {
+      rc = flush(h);
+      if (rc) return rc;
       HIPCHK(hipStreamSynchronize(h->stream));
       for (size_t f = 0; f < F; ++f)
         HIPCHK(hipMemcpy(out_pose + 3 * (F * t + f), h->x[h->parity[f]] + f * h->x_stride,
                          3 * sizeof(double), hipMemcpyDeviceToHost));
     }
   }
-  return EKF_OK;
+  return flush(h);
 }
 
 int ekf_predict(ekf_t h, int f) {
@@ -536,7 +605,8 @@ int ekf_correct(ekf_t h, int f, int id, double rx, double ry) {
   measure(rx, ry, &k.zr, &k.zb);
   mk.push_back(k);
   hipSetDevice(h->cfg.device);
-  return run_known(h, f, 1, false);
+  plan_known(h, f, 1, false);
+  return flush(h);
 }
 
 int ekf_associate_correct(ekf_t h, int f, double rx, double ry, int* j, int* is_new) {
@@ -548,9 +618,12 @@ int ekf_associate_correct(ekf_t h, int f, double rx, double ry, int* j, int* is_
   measure(rx, ry, &k.zr, &k.zb);
   mk.push_back(k);
   hipSetDevice(h->cfg.device);
-  const int rc = run_assoc(h, f, 1, false, false, 1, j, is_new);
+  int jj = -1, nn = 0;
+  const int rc = assoc_sync(h, f, 1, false, false, 1, &jj, &nn);
   if (rc) return rc;
-  if (j && *j < 0) return EKF_E_RANGE;
+  if (j) *j = jj;
+  if (is_new) *is_new = nn;
+  if (jj < 0) return EKF_E_RANGE;
   return EKF_OK;
 }
 
@@ -559,17 +632,11 @@ int ekf_posterior(ekf_t h, int f) {
   hipSetDevice(h->cfg.device);
   if (h->pending[f]) {  // fold the pending predict into a zero-marker pass, then the posterior
     h->msgs[0].clear();
-    return run_known(h, f, 1, true);
+    plan_known(h, f, 1, true);
+  } else {
+    plan_posterior(h, f);
   }
-  int slot;
-  MsgDesc* d = stage(h, &slot);
-  fill_desc(d, 0, kActive, h->parity[f], h->odom[f]);
-  int rc = upload(h, slot, 1);
-  if (rc) return rc;
-  hipError_t e = h->cfg.dtype == EKF_F32
-                     ? launch_posterior<float>(args<float>(h, h->ddesc, f), 1, h->stream)
-                     : launch_posterior<double>(args<double>(h, h->ddesc, f), 1, h->stream);
-  return e == hipSuccess ? EKF_OK : EKF_E_HIP;
+  return flush(h);
 }
 
 int ekf_sync(ekf_t h) {
@@ -678,6 +745,8 @@ int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
   h->prof_ms[kind] = 0.0;
   return EKF_OK;
 }
+
+double ekf_normalize_angle(double rad) { return normalize_angle(rad); }
 
 double ekf_sigma_pass_bytes(ekf_t h, int nf) {
   if (!h) return 0.0;

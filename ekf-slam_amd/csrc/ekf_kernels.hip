@@ -29,6 +29,20 @@
 
 namespace ekfslam {
 
+// Diagnostic build only (tools/gain_bench.hip): s_memtime stamps of block (0,0), thread 0.
+#ifdef EKF_DIAG_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define EKF_STAMP(i)                                                              \
+  do {                                                                            \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                   \
+      g_stamps[i] = __builtin_amdgcn_s_memtime();                                 \
+  } while (0)
+#else
+#define EKF_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 #define EKF_FLAG_RANGE_D 1u
 #define EKF_FLAG_NUMERIC_D 2u
 
@@ -66,27 +80,28 @@ __device__ __forceinline__ void range_bearing(const double* pose, double lx, dou
   zhat[0] = sqrt(ex * ex + ey * ey);
   zhat[1] = normalize_angle(atan2(ey, ex) - pose[0]);
   const double d = ex * ex + ey * ey;
-  const double sd = sqrt(d);
+  const double isd = 1.0 / sqrt(d), id = 1.0 / d;  // one division each instead of four
   H0[0] = 0.0;
-  H0[1] = -ex / sd;
-  H0[2] = -ey / sd;
-  H0[3] = ex / sd;
-  H0[4] = ey / sd;
+  H0[1] = -ex * isd;
+  H0[2] = -ey * isd;
+  H0[3] = ex * isd;
+  H0[4] = ey * isd;
   H1[0] = -1.0;
-  H1[1] = ey / d;
-  H1[2] = -ex / d;
-  H1[3] = -ey / d;
-  H1[4] = ex / d;
+  H1[1] = ey * id;
+  H1[2] = -ex * id;
+  H1[3] = -ey * id;
+  H1[4] = ex * id;
 }
 
-// arma::inv on a 2×2 (closed form). false if singular / non-finite.
+// arma::inv on a 2×2 (closed form: adjugate / det, one reciprocal). false if singular / non-finite.
 __device__ __forceinline__ bool inv2(const double* A, double* o) {
   const double det = A[0] * A[3] - A[1] * A[2];
   if (!(fabs(det) > 0.0)) return false;
-  o[0] = A[3] / det;
-  o[1] = -A[1] / det;
-  o[2] = -A[2] / det;
-  o[3] = A[0] / det;
+  const double idet = 1.0 / det;
+  o[0] = A[3] * idet;
+  o[1] = -A[1] * idet;
+  o[2] = -A[2] * idet;
+  o[3] = A[0] * idet;
   return isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
 }
 
@@ -96,7 +111,7 @@ struct GainShared {
   double alphaU[kMaxU];
   double row0raw[kMaxU];  // Σ_in[0][u_b]
   double col0raw[kMaxU];  // Σ_in[u_a][0]
-  double xU[kMaxU];
+  double xU[2][kMaxU];  // ping-pong across steps (read in S1 while S2 writes)
   double P[kMaxU][kMaxU + 1];
   double KU[kMaxChunk][kMaxU][2];
   double MU[kMaxChunk][kMaxU][2];
@@ -112,8 +127,15 @@ struct GainShared {
 template <typename T>
 __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   __shared__ GainShared sh;
-  const MsgDesc& d = A.desc[blockIdx.y];
-  if (!(d.flags & kActive)) return;
+  __shared__ MsgDesc sdesc;  // the descriptor is read every step: keep it in LDS, not global
+  static_assert(sizeof(MsgDesc) % 16 == 0, "MsgDesc copied as uint4");
+  const MsgDesc& gd = A.desc[blockIdx.y];
+  if (!(gd.flags & kActive)) return;
+  if (threadIdx.x < sizeof(MsgDesc) / 16)
+    reinterpret_cast<uint4*>(&sdesc)[threadIdx.x] =
+        reinterpret_cast<const uint4*>(&gd)[threadIdx.x];
+  __syncthreads();
+  const MsgDesc& d = sdesc;
   const int f = A.f0 + blockIdx.y;
   const int tid = threadIdx.x;
   const int n = A.n, ld = A.ld, ldk = A.ldk;
@@ -126,6 +148,7 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   const int m = d.m;
   const bool first = (d.flags & kFirst) != 0;
   const int kw = ((2 + 2 * m + 3) / 4) * 4;
+  EKF_STAMP(0);
 
   // ---- phase A0: predict pose, index set U --------------------------------------------------
   if (tid == 0) {
@@ -146,10 +169,12 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       sh.u[3 + 2 * c] = j;
       sh.u[4 + 2 * c] = j + 1;
     }
+    for (int b = 3 + 2 * m; b < kMaxU; ++b) sh.u[b] = 0;  // padding: loads stay in bounds
     sh.nu_cnt = 3 + 2 * m;
     sh.status = st;
   }
   __syncthreads();
+  EKF_STAMP(1);
   const int nu = sh.nu_cnt;
 
   // ---- phase A1: gather the |U|×|U| block and x[U] --------------------------------------------
@@ -158,7 +183,7 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
     sh.P[a][b] = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]]);
   }
   if (tid < nu) {
-    sh.xU[tid] = tid < 3 ? sh.pose[tid] : xin[sh.u[tid]];
+    sh.xU[0][tid] = tid < 3 ? sh.pose[tid] : xin[sh.u[tid]];
     sh.alphaU[tid] = first ? alpha_of(sh.u[tid], sh.a1, sh.a2) : 0.0;
   }
   __syncthreads();
@@ -180,105 +205,140 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   }
   __syncthreads();
 
+  EKF_STAMP(2);
   // ---- phase A2: the m corrections on the block ---------------------------------------------
+  // Per step every thread recomputes ẑ, H, S⁻¹, ν redundantly (no serial section, no barrier);
+  // threads 0..nu-1 form K[U] and the new x[U], threads 64..64+nu-1 form M[:, live]; then the
+  // block update touches only the columns later steps still read: {θ,x,y} ∪ markers c+1.. .
   for (int c = 0; c < m; ++c) {
     const int pj = 3 + 2 * c;
-    if (tid == 0) {
-      double H0[5] = {0, 0, 0, 0, 0}, H1[5] = {0, 0, 0, 0, 0}, Si[4] = {0, 0, 0, 0}, nv[2] = {0, 0};
-      int sk = sh.skip[c];
-      if (!sk) {
-        // first sighting (slam.cpp:213-216); all copies of a repeated landmark are kept equal
-        if (!(d.flags & kNoInit) && sh.xU[pj] == 0.0 && sh.xU[pj + 1] == 0.0) {
-          const double ix = sh.xU[1] + d.z[c][0] * cos(d.z[c][1] + sh.xU[0]);
-          const double iy = sh.xU[2] + d.z[c][0] * sin(d.z[c][1] + sh.xU[0]);
-          const int jx = sh.u[pj];
-          for (int b = 3; b < nu; ++b) {
-            if (sh.u[b] == jx) sh.xU[b] = ix;
-            else if (sh.u[b] == jx + 1) sh.xU[b] = iy;
-          }
-        }
-        double zhat[2];
-        range_bearing(sh.xU, sh.xU[pj], sh.xU[pj + 1], zhat, H0, H1);
-        const int pA[5] = {0, 1, 2, pj, pj + 1};
-        double HP0[5], HP1[5];
-        for (int bb = 0; bb < 5; ++bb) {
-          double s0 = 0.0, s1 = 0.0;
-          for (int a = 0; a < 5; ++a) {
-            const double v = sh.P[pA[a]][pA[bb]];
-            s0 += H0[a] * v;
-            s1 += H1[a] * v;
-          }
-          HP0[bb] = s0;
-          HP1[bb] = s1;
-        }
-        double Sm[4] = {0, 0, 0, 0};
+    const int cur = c & 1, nxt = cur ^ 1;
+    const double* xc = sh.xU[cur];
+    const double z0 = d.z[c][0], z1 = d.z[c][1];
+    const double pose[3] = {xc[0], xc[1], xc[2]};
+    double lx = xc[pj], ly = xc[pj + 1];
+    bool sk = sh.skip[c] != 0;
+    bool init = false;
+    if (!sk && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
+      init = true;
+      lx = pose[1] + z0 * cos(z1 + pose[0]);
+      ly = pose[2] + z0 * sin(z1 + pose[0]);
+    }
+    const int pA[5] = {0, 1, 2, pj, pj + 1};
+    double H0[5], H1[5], Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
+    {
+      double zhat[2];
+      if (c == 0) EKF_STAMP(50);
+      range_bearing(pose, lx, ly, zhat, H0, H1);
+      if (c == 0) EKF_STAMP(51);
+      double HP0[5], HP1[5];
+#pragma unroll
+      for (int bb = 0; bb < 5; ++bb) {
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
         for (int a = 0; a < 5; ++a) {
-          Sm[0] += HP0[a] * H0[a];
-          Sm[1] += HP0[a] * H1[a];
-          Sm[2] += HP1[a] * H0[a];
-          Sm[3] += HP1[a] * H1[a];
+          const double v = sh.P[pA[a]][pA[bb]];
+          s0 += H0[a] * v;
+          s1 += H1[a] * v;
         }
-        Sm[0] += A.r;
-        Sm[3] += A.r;
-        if (inv2(Sm, Si)) {
-          nv[0] = d.z[c][0] - zhat[0];
-          nv[1] = normalize_angle(d.z[c][1] - zhat[1]);
-        } else {
-          sk = 1;
-          sh.status |= EKF_FLAG_NUMERIC_D;
+        HP0[bb] = s0;
+        HP1[bb] = s1;
+      }
+      double Sm[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        Sm[0] += HP0[a] * H0[a];
+        Sm[1] += HP0[a] * H1[a];
+        Sm[2] += HP1[a] * H0[a];
+        Sm[3] += HP1[a] * H1[a];
+      }
+      Sm[0] += A.r;
+      Sm[3] += A.r;
+      if (c == 0) EKF_STAMP(52);
+      if (!sk && inv2(Sm, Si)) {
+        nv0 = z0 - zhat[0];
+        nv1 = normalize_angle(z1 - zhat[1]);
+      } else {
+        if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every thread
+        sk = true;
+      }
+    }
+    if (c == 0) EKF_STAMP(53);
+    if (sk) {
+#pragma unroll
+      for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
+      Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
+      nv0 = nv1 = 0.0;
+    }
+    const int jx = sh.u[pj];
+    if (tid < kMaxU) {  // K[U] and x[U]; zero padding beyond nu keeps phase B branch-free
+      double K0 = 0.0, K1 = 0.0;
+      if (tid < nu) {
+        double kt0 = 0.0, kt1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          const double v = sh.P[tid][pA[a]];
+          kt0 += v * H0[a];
+          kt1 += v * H1[a];
+        }
+        K0 = kt0 * Si[0] + kt1 * Si[2];
+        K1 = kt0 * Si[1] + kt1 * Si[3];
+        double xt = xc[tid];
+        if (init) {
+          if (sh.u[tid] == jx) xt = lx;
+          else if (sh.u[tid] == jx + 1) xt = ly;
+        }
+        xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
+        if (tid == 0) xt = normalize_angle(xt);      // slam.cpp:267
+        sh.xU[nxt][tid] = xt;
+      }
+      sh.KU[c][tid][0] = K0;
+      sh.KU[c][tid][1] = K1;
+    } else if (tid >= 64 && tid < 64 + kMaxU) {  // M[:, live]
+      const int b = tid - 64;
+      double mm0 = 0.0, mm1 = 0.0;
+      if (b < nu && (b < 3 || b >= pj + 2)) {
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          const double v = sh.P[pA[a]][b];
+          mm0 += H0[a] * v;
+          mm1 += H1[a] * v;
         }
       }
-      if (sk) {
-        for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
-        Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
-        nv[0] = nv[1] = 0.0;
-      }
-      sh.skip[c] = sk;
+      sh.MU[c][b][0] = mm0;
+      sh.MU[c][b][1] = mm1;
+    }
+    EKF_STAMP(3 + 2 * c);
+    if (tid == 0) {
+#pragma unroll
       for (int a = 0; a < 5; ++a) {
         sh.H[c][a] = H0[a];
         sh.H[c][5 + a] = H1[a];
       }
+#pragma unroll
       for (int a = 0; a < 4; ++a) sh.Si[c][a] = Si[a];
-      sh.nu[c][0] = nv[0];
-      sh.nu[c][1] = nv[1];
+      sh.nu[c][0] = nv0;
+      sh.nu[c][1] = nv1;
     }
     __syncthreads();
-    if (tid < nu) {
-      const int pA[5] = {0, 1, 2, pj, pj + 1};
-      const double* H = sh.H[c];
-      const double* Si = sh.Si[c];
-      double kt0 = 0.0, kt1 = 0.0, mm0 = 0.0, mm1 = 0.0;
-      for (int a = 0; a < 5; ++a) {
-        const double v = sh.P[tid][pA[a]];
-        kt0 += v * H[a];
-        kt1 += v * H[5 + a];
+    // Σ_block ← Σ_block − K·M on the columns still live (slam.cpp:264-265 restricted to U)
+    const int live = 3 + (nu - pj - 2);
+    for (int a = tid >> 5; a < nu; a += 8) {
+      const double k0 = sh.KU[c][a][0], k1 = sh.KU[c][a][1];
+      for (int bi = tid & 31; bi < live; bi += 32) {
+        const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
+        sh.P[a][b] -= k0 * sh.MU[c][b][0] + k1 * sh.MU[c][b][1];
       }
-      for (int a = 0; a < 5; ++a) {
-        const double v = sh.P[pA[a]][tid];
-        mm0 += H[a] * v;
-        mm1 += H[5 + a] * v;
-      }
-      const double K0 = kt0 * Si[0] + kt1 * Si[2];
-      const double K1 = kt0 * Si[1] + kt1 * Si[3];
-      sh.KU[c][tid][0] = K0;
-      sh.KU[c][tid][1] = K1;
-      sh.MU[c][tid][0] = mm0;
-      sh.MU[c][tid][1] = mm1;
-      sh.xU[tid] = sh.xU[tid] + (K0 * sh.nu[c][0] + K1 * sh.nu[c][1]);
     }
     __syncthreads();
-    for (int e = tid; e < nu * nu; e += blockDim.x) {
-      const int a = e / nu, b = e - a * nu;
-      sh.P[a][b] -= sh.KU[c][a][0] * sh.MU[c][b][0] + sh.KU[c][a][1] * sh.MU[c][b][1];
-    }
-    if (tid == 0) sh.xU[0] = normalize_angle(sh.xU[0]);  // slam.cpp:267
-    __syncthreads();
+    EKF_STAMP(4 + 2 * c);
   }
+  const double* xfin = sh.xU[m & 1];
 
   if (blockIdx.x == 0 && tid == 0) {
     if (sh.status) atomicOr(&ctl->status, sh.status);
     if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
-      const Pose2 tmo = compose(Pose2{sh.xU[0], sh.xU[1], sh.xU[2]},
+      const Pose2 tmo = compose(Pose2{xfin[0], xfin[1], xfin[2]},
                                 inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
       ctl->tmo_next[0] = tmo.theta;
       ctl->tmo_next[1] = tmo.x;
@@ -286,6 +346,7 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
     }
   }
 
+  EKF_STAMP(40);
   // ---- phase B: one row or one column of Σ per thread ----------------------------------------
   const int gi = blockIdx.x * blockDim.x + tid;
   const double s00 = sh.s00;
@@ -294,19 +355,22 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
     const T* rowp = S + static_cast<size_t>(i) * ld;
     double r[kMaxU];
 #pragma unroll
-    for (int b = 0; b < kMaxU; ++b) r[b] = b < nu ? static_cast<double>(rowp[sh.u[b]]) : 0.0;
+    for (int b = 0; b < kMaxU; ++b) {
+      const double v = static_cast<double>(rowp[sh.u[b]]);
+      r[b] = b < nu ? v : 0.0;
+    }
     const double ai = first ? alpha_of(i, sh.a1, sh.a2) : 0.0;
     const double r0raw = r[0];
     if (first) {
 #pragma unroll
-      for (int b = 0; b < kMaxU; ++b) {
-        if (b < nu) {
-          double v = r[b] + ai * sh.row0raw[b];
-          v = v + (r0raw + ai * s00) * sh.alphaU[b];
-          if (i == sh.u[b] && i < 3) v += A.q;
-          r[b] = v;
-        }
+      for (int b = 0; b < 3; ++b) {  // only the pose columns carry α and Q̄ besides row 0's term
+        double v = r[b] + ai * sh.row0raw[b];
+        v = v + (r0raw + ai * s00) * sh.alphaU[b];
+        if (i == b) v += A.q;
+        r[b] = v;
       }
+#pragma unroll
+      for (int b = 3; b < kMaxU; ++b) r[b] = b < nu ? r[b] + ai * sh.row0raw[b] : 0.0;
     }
     kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
     kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
@@ -314,8 +378,20 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
 #pragma unroll
     for (int c = 0; c < kMaxChunk; ++c) {
       if (c < m) {
-        const double* H = sh.H[c];
-        const double* Si = sh.Si[c];
+        // all of this step's LDS operands first (one wait), then the arithmetic
+        double H[10], Si[4], nv[2], mu[kMaxU][2];
+#pragma unroll
+        for (int a = 0; a < 10; ++a) H[a] = sh.H[c][a];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) Si[a] = sh.Si[c][a];
+        nv[0] = sh.nu[c][0];
+        nv[1] = sh.nu[c][1];
+#pragma unroll
+        for (int b = 0; b < kMaxU; ++b)
+          if (b < 3 || b >= 5 + 2 * c) {
+            mu[b][0] = sh.MU[c][b][0];
+            mu[b][1] = sh.MU[c][b][1];
+          }
         const double v[5] = {r[0], r[1], r[2], r[3 + 2 * c], r[4 + 2 * c]};
         double kt0 = 0.0, kt1 = 0.0;
 #pragma unroll
@@ -327,42 +403,54 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
         const double K1 = kt0 * Si[1] + kt1 * Si[3];
         kc[(2 + 2 * c) * ldk + i] = static_cast<T>(K0);
         kc[(3 + 2 * c) * ldk + i] = static_cast<T>(K1);
-        xi = xi + (K0 * sh.nu[c][0] + K1 * sh.nu[c][1]);
+        xi = xi + (K0 * nv[0] + K1 * nv[1]);
 #pragma unroll
-        for (int b = 0; b < kMaxU; ++b)
-          if (b < nu) r[b] -= K0 * sh.MU[c][b][0] + K1 * sh.MU[c][b][1];
+        for (int b = 0; b < kMaxU; ++b)  // entries later steps read: {θ,x,y} ∪ markers c+1..
+          if (b < 3 || b >= 5 + 2 * c) r[b] -= K0 * mu[b][0] + K1 * mu[b][1];
       }
     }
     for (int k = 2 + 2 * m; k < kw; ++k) kc[k * ldk + i] = static_cast<T>(0);
+    EKF_STAMP(41);
     int pos = -1;
     for (int b = nu - 1; b >= 0; --b)
       if (sh.u[b] == i) pos = b;
-    xout[i] = pos >= 0 ? sh.xU[pos] : xi;
+    xout[i] = pos >= 0 ? xfin[pos] : xi;
+    EKF_STAMP(42);
   } else if (gi < 2 * n) {
     const int col = gi - n;
     double cl[kMaxU];
 #pragma unroll
-    for (int a = 0; a < kMaxU; ++a)
-      cl[a] = a < nu ? static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + col]) : 0.0;
+    for (int a = 0; a < kMaxU; ++a) {
+      const double v = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + col]);
+      cl[a] = a < nu ? v : 0.0;
+    }
     const double ac = first ? alpha_of(col, sh.a1, sh.a2) : 0.0;
     const double c0raw = cl[0];
     if (first) {
 #pragma unroll
-      for (int a = 0; a < kMaxU; ++a) {
-        if (a < nu) {
-          double v = cl[a] + sh.alphaU[a] * c0raw;
-          v = v + (sh.col0raw[a] + sh.alphaU[a] * s00) * ac;
-          if (sh.u[a] == col && col < 3) v += A.q;
-          cl[a] = v;
-        }
+      for (int a = 0; a < 3; ++a) {  // rows 1, 2 carry α; the pose diagonal carries Q̄
+        double v = cl[a] + sh.alphaU[a] * c0raw;
+        v = v + (sh.col0raw[a] + sh.alphaU[a] * s00) * ac;
+        if (a == col) v += A.q;
+        cl[a] = v;
       }
+#pragma unroll
+      for (int a = 3; a < kMaxU; ++a) cl[a] = a < nu ? cl[a] + sh.col0raw[a] * ac : 0.0;
     }
     mc[0 * ldk + col] = static_cast<T>(first ? c0raw : 0.0);
     mc[1 * ldk + col] = static_cast<T>(first ? ac : 0.0);
 #pragma unroll
     for (int c = 0; c < kMaxChunk; ++c) {
       if (c < m) {
-        const double* H = sh.H[c];
+        double H[10], ku[kMaxU][2];
+#pragma unroll
+        for (int a = 0; a < 10; ++a) H[a] = sh.H[c][a];
+#pragma unroll
+        for (int a = 0; a < kMaxU; ++a)
+          if (a < 3 || a >= 5 + 2 * c) {
+            ku[a][0] = sh.KU[c][a][0];
+            ku[a][1] = sh.KU[c][a][1];
+          }
         const double v[5] = {cl[0], cl[1], cl[2], cl[3 + 2 * c], cl[4 + 2 * c]};
         double mm0 = 0.0, mm1 = 0.0;
 #pragma unroll
@@ -374,7 +462,7 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
         mc[(3 + 2 * c) * ldk + col] = static_cast<T>(mm1);
 #pragma unroll
         for (int a = 0; a < kMaxU; ++a)
-          if (a < nu) cl[a] -= sh.KU[c][a][0] * mm0 + sh.KU[c][a][1] * mm1;
+          if (a < 3 || a >= 5 + 2 * c) cl[a] -= ku[a][0] * mm0 + ku[a][1] * mm1;
       }
     }
     for (int k = 2 + 2 * m; k < kw; ++k) mc[k * ldk + col] = static_cast<T>(0);

@@ -17,8 +17,19 @@ namespace ekfslam {
 
 constexpr double kPi = 3.14159265358979323846;
 
+// fmod(x, 2π) without the generic frexp loop: for |x| < 5π the result x − k·2π (k ≤ 2) is exact in
+// floating point (Sterbenz), so this returns fmod's bits, sign of zero included.
+__host__ __device__ inline double fmod_2pi(double x) {
+  const double y = 2.0 * kPi;
+  const double ax = fabs(x);
+  if (ax < y) return x;
+  if (ax < 2.0 * y) return copysign(ax - y, x);
+  if (ax < 2.5 * y) return copysign(ax - 2.0 * y, x);
+  return fmod(x, y);
+}
+
 __host__ __device__ inline double normalize_angle(double rad) {
-  const double d = fmod(rad + kPi, 2.0 * kPi);
+  const double d = fmod_2pi(rad + kPi);
   return d <= 0.0 ? d + kPi : d - kPi;
 }
 

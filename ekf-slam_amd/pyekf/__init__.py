@@ -26,7 +26,7 @@ EXPORTS = [
     "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_predict",
     "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_get_pose",
     "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status",
-    "ekf_profile_enable", "ekf_profile_read", "ekf_sigma_pass_bytes",
+    "ekf_profile_enable", "ekf_profile_read", "ekf_sigma_pass_bytes", "ekf_normalize_angle",
     "slam_create", "slam_destroy", "slam_joint_states", "slam_markers", "slam_initial_pose",
     "slam_odom", "slam_map_odom", "slam_filter", "slam_replay", "slam_integrate_odometry",
 ]
@@ -79,6 +79,7 @@ def lib():
             "ekf_profile_enable": (_i, [_vp, _i]),
             "ekf_profile_read": (_i, [_vp, _i, C.POINTER(C.c_longlong), _dp]),
             "ekf_sigma_pass_bytes": (C.c_double, [_vp, _i]),
+            "ekf_normalize_angle": (C.c_double, [_d]),
             "slam_create": (_i, [C.POINTER(_vp), C.POINTER(Config), _d, _d, _i]),
             "slam_destroy": (_i, [_vp]),
             "slam_joint_states": (_i, [_vp, _d, _d]),

@@ -114,6 +114,10 @@ int ekf_set_state(ekf_t h, int filter, const double* state, const double* sigma,
                   const double* t_map_odom, unsigned counter);
 int ekf_get_status(ekf_t h, int filter, unsigned* flags); /* and clears them */
 
+/* ---- helpers ---- */
+/* turtlelib::normalize_angle (geometry2d.cpp:5-14): maps into (-π, π], -π → π. */
+double ekf_normalize_angle(double rad);
+
 /* ---- measurement ---- */
 /* Per-kernel device time with HIP events on the handle's stream (0 = Σ pass, 1 = gain,
  * 2 = association). Adds two event records per timed launch; off by default. */

@@ -86,3 +86,18 @@ def test_fkin_kat(impl, case):
             out = dd.fkin(l, r)
         th, x, y = out
     assert abs(x - ex) < 1e-8 and abs(y - ey) < 1e-8 and abs(th - et) < 1e-8
+
+
+def test_product_normalize_angle_bit_exact_with_oracle():
+    """geom.hpp's fast fmod(x, 2π) path returns fmod's bits (normalize_angle is on every step)."""
+    import pyekf
+    L = pyekf.lib()
+    rng = np.random.default_rng(0)
+    xs = np.concatenate([rng.uniform(-40, 40, 20000), rng.uniform(-7, 7, 20000),
+                         np.array([0.0, -0.0, PI, -PI, 2 * PI, -2 * PI, 3 * PI, -3 * PI, 4 * PI,
+                                   -4 * PI, 5 * PI, -5 * PI, 1e-300, -1e-300, 1e6, -1e6]),
+                         np.nextafter(np.array([PI, -PI, 3 * PI, -3 * PI]), 10.0),
+                         np.nextafter(np.array([PI, -PI, 3 * PI, -3 * PI]), -10.0)])
+    for v in xs:
+        a, b = L.ekf_normalize_angle(float(v)), orc.normalize_angle(float(v))
+        assert a == b and np.signbit(a) == np.signbit(b), (v, a, b)

@@ -1,0 +1,90 @@
+// Dev tool (not shipped): times the gain kernel alone and prints per-phase s_memtime stamps of
+// block (0,0) thread 0. Build: hipcc -O3 --offload-arch=gfx950 -DEKF_DIAG_STAMPS -I../include
+//   -I../ekf-slam_amd/csrc gain_bench.hip -o gain_bench
+#include "../ekf-slam_amd/csrc/ekf_kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace ekfslam;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
+
+template <typename T>
+void run(int N, int m, int reps) {
+  const int n = 3 + 2 * N;
+  const int per_line = 128 / sizeof(T);
+  const int ld = (n + per_line - 1) / per_line * per_line, ldk = (n + 63) / 64 * 64;
+  std::vector<T> S(static_cast<size_t>(n) * ld, 0);
+  std::vector<double> x(n, 0);
+  srand(1);
+  for (int i = 0; i < n; ++i) S[static_cast<size_t>(i) * ld + i] = i < 3 ? 1e-2 : 1e-2;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < i; ++j) {
+      T v = static_cast<T>(1e-4 * ((rand() % 1000) / 1000.0 - 0.5));
+      S[static_cast<size_t>(i) * ld + j] = v;
+      S[static_cast<size_t>(j) * ld + i] = v;
+    }
+  for (int k = 0; k < N; ++k) { x[3 + 2 * k] = 1.0 + 0.1 * k; x[4 + 2 * k] = 0.5 - 0.05 * k; }
+  T *dS[2], *kc, *mc;
+  double* dx[2];
+  FilterCtl* ctl;
+  MsgDesc* dd;
+  for (int p = 0; p < 2; ++p) {
+    CK(hipMalloc(&dS[p], S.size() * sizeof(T)));
+    CK(hipMemcpy(dS[p], S.data(), S.size() * sizeof(T), hipMemcpyHostToDevice));
+    CK(hipMalloc(&dx[p], n * sizeof(double)));
+    CK(hipMemcpy(dx[p], x.data(), n * sizeof(double), hipMemcpyHostToDevice));
+  }
+  CK(hipMalloc(&kc, kMaxKW * ldk * sizeof(T)));
+  CK(hipMalloc(&mc, kMaxKW * ldk * sizeof(T)));
+  CK(hipMalloc(&ctl, sizeof(FilterCtl)));
+  CK(hipMemset(ctl, 0, sizeof(FilterCtl)));
+  MsgDesc d{};
+  d.m = m;
+  d.flags = kActive | kFirst | kLast;
+  d.parity = 0;
+  for (int c = 0; c < m; ++c) {
+    d.ids[c] = (c * 7) % N;
+    const double lx = x[3 + 2 * d.ids[c]], ly = x[4 + 2 * d.ids[c]];
+    d.z[c][0] = sqrt(lx * lx + ly * ly) + 0.001;
+    d.z[c][1] = atan2(ly, lx) + 0.001;
+  }
+  CK(hipMalloc(&dd, sizeof(MsgDesc)));
+  CK(hipMemcpy(dd, &d, sizeof(MsgDesc), hipMemcpyHostToDevice));
+  PassArgs<T> a{};
+  a.sig[0] = dS[0]; a.sig[1] = dS[1]; a.sig_stride = 0;
+  a.x[0] = dx[0]; a.x[1] = dx[1]; a.x_stride = 0;
+  a.kcat = kc; a.mcat = mc; a.km_stride = 0; a.ldk = ldk;
+  a.ctl = ctl; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0;
+  a.q = 1e-2; a.r = 1e-2; a.gate = 2.0;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  for (int i = 0; i < 5; ++i) CK(launch_gain<T>(a, 1, s));
+  CK(hipStreamSynchronize(s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < reps; ++i) CK(launch_gain<T>(a, 1, s));
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long st[64];
+  CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
+  printf("N=%d m=%d %s: gain %.2f us/launch | stamps (cycles from start): A0 %llu A1 %llu |",
+         N, m, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, st[1] - st[0], st[2] - st[0]);
+  for (int c = 0; c < m; ++c) printf(" s%d:%llu/%llu", c, st[3 + 2 * c] - st[0], st[4 + 2 * c] - st[0]);
+  printf(" | step0 sub: start %llu rb %llu S %llu inv %llu", st[50] - st[0], st[51] - st[0], st[52] - st[0], st[53] - st[0]);
+  printf(" | endA %llu B-rec %llu B-end %llu\n", st[40] - st[0], st[41] - st[0], st[42] - st[0]);
+}
+
+int main() {
+  run<double>(50, 4, 200);
+  run<double>(256, 16, 200);
+  run<float>(1024, 16, 200);
+  run<float>(1024, 1, 200);
+  return 0;
+}
