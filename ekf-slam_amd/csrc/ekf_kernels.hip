@@ -105,18 +105,30 @@ __device__ __forceinline__ bool inv2(const double* A, double* o) {
   return isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
 }
 
+// f64 MFMA 16×16×4: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15],
+// D[row = (lane>>4) + 4r][col = lane&15] (the f64 C/D map differs from the f32 one).
+typedef double d4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+constexpr int kZC = 2 * kMaxChunk;  // correction columns of Z / rows of Y (32)
+
 struct GainShared {
   int u[kMaxU];
   int skip[kMaxChunk];
   double alphaU[kMaxU];
   double row0raw[kMaxU];  // Σ_in[0][u_b]
   double col0raw[kMaxU];  // Σ_in[u_a][0]
-  double xU[2][kMaxU];  // ping-pong across steps (read in S1 while S2 writes)
-  double P[kMaxU][kMaxU + 1];
+  double xU[2][kMaxU];    // ping-pong across steps (read in S1 while S2 writes)
+  double P[kMaxU][kMaxU + 1];    // Σ[U,U] after c steps (rows all, columns live)
+  double Phi[kMaxU][kMaxU + 1];  // row map: r_c[U] = r_0[U]·Φ_c   (identity at c = 0)
+  double Psi[kMaxU][kMaxU + 1];  // column map: c_c[U] = Ψ_c·c_0[U] (identity at c = 0)
   double KU[kMaxChunk][kMaxU][2];
   double MU[kMaxChunk][kMaxU][2];
-  double H[kMaxChunk][10];
-  double Si[kMaxChunk][4];
+  double Z[kMaxU][kZC + 1];      // K_c[i] = r_0(i)[U] · Z[:, 2c..2c+1]
+  double Y[kZC][kMaxU + 1];      // M_c[:, j] = Y[2c..2c+1, :] · c_0(j)[U]
+  double Zx[kMaxU];              // Σ_c Z_c ν_c: x_i += r_0(i)[U] · Zx
   double nu[kMaxChunk][2];
   double pose[3];
   double a1, a2, s00;
@@ -134,21 +146,23 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   if (threadIdx.x < sizeof(MsgDesc) / 16)
     reinterpret_cast<uint4*>(&sdesc)[threadIdx.x] =
         reinterpret_cast<const uint4*>(&gd)[threadIdx.x];
-  __syncthreads();
   const MsgDesc& d = sdesc;
   const int f = A.f0 + blockIdx.y;
   const int tid = threadIdx.x;
   const int n = A.n, ld = A.ld, ldk = A.ldk;
-  const T* S = A.sig[d.parity] + f * A.sig_stride;
-  const double* xin = A.x[d.parity] + f * A.x_stride;
-  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
   T* kc = A.kcat + f * A.km_stride;
   T* mc = A.mcat + f * A.km_stride;
   FilterCtl* ctl = A.ctl + f;
+  // zero the GEMM operands (padding must be exactly 0, not stale LDS)
+  for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.Z[0][0])[e] = 0.0;
+  for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.Y[0][0])[e] = 0.0;
+  __syncthreads();
+  EKF_STAMP(0);
+  const T* S = A.sig[d.parity] + f * A.sig_stride;
+  const double* xin = A.x[d.parity] + f * A.x_stride;
+  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
   const int m = d.m;
   const bool first = (d.flags & kFirst) != 0;
-  const int kw = ((2 + 2 * m + 3) / 4) * 4;
-  EKF_STAMP(0);
 
   // ---- phase A0: predict pose, index set U --------------------------------------------------
   if (tid == 0) {
@@ -177,10 +191,12 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   EKF_STAMP(1);
   const int nu = sh.nu_cnt;
 
-  // ---- phase A1: gather the |U|×|U| block and x[U] --------------------------------------------
+  // ---- phase A1: gather the |U|×|U| block, x[U], identities ----------------------------------
   for (int e = tid; e < nu * nu; e += blockDim.x) {
     const int a = e / nu, b = e - a * nu;
     sh.P[a][b] = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]]);
+    sh.Phi[a][b] = a == b ? 1.0 : 0.0;
+    sh.Psi[a][b] = a == b ? 1.0 : 0.0;
   }
   if (tid < nu) {
     sh.xU[0][tid] = tid < 3 ? sh.pose[tid] : xin[sh.u[tid]];
@@ -204,12 +220,13 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
     }
   }
   __syncthreads();
-
   EKF_STAMP(2);
+
   // ---- phase A2: the m corrections on the block ---------------------------------------------
-  // Per step every thread recomputes ẑ, H, S⁻¹, ν redundantly (no serial section, no barrier);
-  // threads 0..nu-1 form K[U] and the new x[U], threads 64..64+nu-1 form M[:, live]; then the
-  // block update touches only the columns later steps still read: {θ,x,y} ∪ markers c+1.. .
+  // S1: every thread recomputes ẑ, H, S⁻¹, ν (no serial section). S2: K[U], Z (rows of Φ), x[U];
+  // M[:, live]; Y (columns of Ψ). S3: P, Φ (live columns) and Ψ (live rows) lose the step's
+  // rank-2 term. "Live" = what later steps still read: {θ,x,y} ∪ markers c+1.. .
+  const int s3a = tid / 7, s3j = tid - 7 * (tid / 7);  // S3 layout: 36 rows × 7 threads
   for (int c = 0; c < m; ++c) {
     const int pj = 3 + 2 * c;
     const int cur = c & 1, nxt = cur ^ 1;
@@ -228,9 +245,7 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
     double H0[5], H1[5], Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
     {
       double zhat[2];
-      if (c == 0) EKF_STAMP(50);
       range_bearing(pose, lx, ly, zhat, H0, H1);
-      if (c == 0) EKF_STAMP(51);
       double HP0[5], HP1[5];
 #pragma unroll
       for (int bb = 0; bb < 5; ++bb) {
@@ -254,7 +269,6 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       }
       Sm[0] += A.r;
       Sm[3] += A.r;
-      if (c == 0) EKF_STAMP(52);
       if (!sk && inv2(Sm, Si)) {
         nv0 = z0 - zhat[0];
         nv1 = normalize_angle(z1 - zhat[1]);
@@ -263,26 +277,37 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
         sk = true;
       }
     }
-    if (c == 0) EKF_STAMP(53);
     if (sk) {
 #pragma unroll
       for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
       Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
       nv0 = nv1 = 0.0;
     }
+    // W = Hᵀ·S⁻¹ (5×2): K = row[pA]·W
+    double W0[5], W1[5];
+#pragma unroll
+    for (int a = 0; a < 5; ++a) {
+      W0[a] = H0[a] * Si[0] + H1[a] * Si[2];
+      W1[a] = H0[a] * Si[1] + H1[a] * Si[3];
+    }
     const int jx = sh.u[pj];
-    if (tid < kMaxU) {  // K[U] and x[U]; zero padding beyond nu keeps phase B branch-free
-      double K0 = 0.0, K1 = 0.0;
+    if (tid < kMaxU) {  // K[U], Z_c, x[U]
+      double K0 = 0.0, K1 = 0.0, Z0 = 0.0, Z1 = 0.0;
       if (tid < nu) {
-        double kt0 = 0.0, kt1 = 0.0;
+        double kt0 = 0.0, kt1 = 0.0, zt0 = 0.0, zt1 = 0.0;
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
           const double v = sh.P[tid][pA[a]];
           kt0 += v * H0[a];
           kt1 += v * H1[a];
+          const double w = sh.Phi[tid][pA[a]];
+          zt0 += w * W0[a];
+          zt1 += w * W1[a];
         }
         K0 = kt0 * Si[0] + kt1 * Si[2];
         K1 = kt0 * Si[1] + kt1 * Si[3];
+        Z0 = zt0;
+        Z1 = zt1;
         double xt = xc[tid];
         if (init) {
           if (sh.u[tid] == jx) xt = lx;
@@ -294,6 +319,8 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       }
       sh.KU[c][tid][0] = K0;
       sh.KU[c][tid][1] = K1;
+      sh.Z[tid][2 * c] = Z0;
+      sh.Z[tid][2 * c + 1] = Z1;
     } else if (tid >= 64 && tid < 64 + kMaxU) {  // M[:, live]
       const int b = tid - 64;
       double mm0 = 0.0, mm1 = 0.0;
@@ -307,34 +334,54 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       }
       sh.MU[c][b][0] = mm0;
       sh.MU[c][b][1] = mm1;
-    }
-    EKF_STAMP(3 + 2 * c);
-    if (tid == 0) {
+    } else if (tid >= 128 && tid < 128 + kMaxU) {  // Y_c = H·Ψ[pA, :]
+      const int b = tid - 128;
+      double y0 = 0.0, y1 = 0.0;
+      if (b < nu) {
 #pragma unroll
-      for (int a = 0; a < 5; ++a) {
-        sh.H[c][a] = H0[a];
-        sh.H[c][5 + a] = H1[a];
+        for (int a = 0; a < 5; ++a) {
+          const double v = sh.Psi[pA[a]][b];
+          y0 += H0[a] * v;
+          y1 += H1[a] * v;
+        }
       }
-#pragma unroll
-      for (int a = 0; a < 4; ++a) sh.Si[c][a] = Si[a];
+      sh.Y[2 * c][b] = y0;
+      sh.Y[2 * c + 1][b] = y1;
+    }
+    if (tid == 0) {
       sh.nu[c][0] = nv0;
       sh.nu[c][1] = nv1;
     }
+    EKF_STAMP(3 + 2 * c);
     __syncthreads();
-    // Σ_block ← Σ_block − K·M on the columns still live (slam.cpp:264-265 restricted to U)
+    // S3: all operands of a thread are independent loads (issued together, one wait)
     const int live = 3 + (nu - pj - 2);
-    for (int a = tid >> 5; a < nu; a += 8) {
-      const double k0 = sh.KU[c][a][0], k1 = sh.KU[c][a][1];
-      for (int bi = tid & 31; bi < live; bi += 32) {
-        const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
-        sh.P[a][b] -= k0 * sh.MU[c][b][0] + k1 * sh.MU[c][b][1];
+    if (s3a < nu) {
+      const double ka0 = sh.KU[c][s3a][0], ka1 = sh.KU[c][s3a][1];
+      const double za0 = sh.Z[s3a][2 * c], za1 = sh.Z[s3a][2 * c + 1];
+      const double ya0 = sh.Y[2 * c][s3a], ya1 = sh.Y[2 * c + 1][s3a];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int bi = s3j + 7 * k;
+        if (bi < live) {
+          const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
+          const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
+          const double kb0 = sh.KU[c][b][0], kb1 = sh.KU[c][b][1];
+          sh.P[s3a][b] -= ka0 * mb0 + ka1 * mb1;
+          sh.Phi[s3a][b] -= za0 * mb0 + za1 * mb1;
+          sh.Psi[b][s3a] -= kb0 * ya0 + kb1 * ya1;
+        }
       }
     }
     __syncthreads();
     EKF_STAMP(4 + 2 * c);
   }
   const double* xfin = sh.xU[m & 1];
-
+  if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
+    double zx = 0.0;
+    for (int c = 0; c < m; ++c) zx += sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];
+    sh.Zx[tid] = zx;
+  }
   if (blockIdx.x == 0 && tid == 0) {
     if (sh.status) atomicOr(&ctl->status, sh.status);
     if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
@@ -345,132 +392,109 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       ctl->tmo_next[2] = tmo.y;
     }
   }
-
+  __syncthreads();
   EKF_STAMP(40);
-  // ---- phase B: one row or one column of Σ per thread ----------------------------------------
-  const int gi = blockIdx.x * blockDim.x + tid;
+
+  // ---- phase B: Kcat = R_pred·Z, Mcat = Y·C_pred on f64 MFMA, 16 rows (or columns) per wave ----
+  // R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j] (predict folded in as above).
+  const int lane = tid & 63;
+  const int wg = blockIdx.x * (blockDim.x >> 6) + (tid >> 6);  // global wave index
+  const int row_tiles = (n + 15) / 16;
+  const int ks = lane >> 4, l16 = lane & 15;
   const double s00 = sh.s00;
-  if (gi < n) {
-    const int i = gi;
-    const T* rowp = S + static_cast<size_t>(i) * ld;
-    double r[kMaxU];
-#pragma unroll
-    for (int b = 0; b < kMaxU; ++b) {
-      const double v = static_cast<double>(rowp[sh.u[b]]);
-      r[b] = b < nu ? v : 0.0;
-    }
+  if (wg < row_tiles) {
+    const int R0 = wg * 16;
+    const int i = R0 + l16;
+    const bool vi = i < n;
+    const T* rowp = S + static_cast<size_t>(vi ? i : 0) * ld;
+    const double r0raw = vi ? static_cast<double>(rowp[0]) : 0.0;
     const double ai = first ? alpha_of(i, sh.a1, sh.a2) : 0.0;
-    const double r0raw = r[0];
-    if (first) {
+    double av[9];
 #pragma unroll
-      for (int b = 0; b < 3; ++b) {  // only the pose columns carry α and Q̄ besides row 0's term
-        double v = r[b] + ai * sh.row0raw[b];
-        v = v + (r0raw + ai * s00) * sh.alphaU[b];
-        if (i == b) v += A.q;
-        r[b] = v;
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      double v = (vi && k < nu) ? static_cast<double>(rowp[sh.u[k]]) : 0.0;
+      if (first && vi && k < nu) {
+        v = v + ai * sh.row0raw[k];
+        v = v + (r0raw + ai * s00) * sh.alphaU[k];
+        if (i == sh.u[k] && i < 3) v += A.q;
       }
-#pragma unroll
-      for (int b = 3; b < kMaxU; ++b) r[b] = b < nu ? r[b] + ai * sh.row0raw[b] : 0.0;
+      av[s] = v;
     }
-    kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
-    kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
-    double xi = xin[i];
+    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
 #pragma unroll
-    for (int c = 0; c < kMaxChunk; ++c) {
-      if (c < m) {
-        // all of this step's LDS operands first (one wait), then the arithmetic
-        double H[10], Si[4], nv[2], mu[kMaxU][2];
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      const double z0 = k < kMaxU ? sh.Z[k][l16] : 0.0;
+      const double z1 = k < kMaxU ? sh.Z[k][16 + l16] : 0.0;
+      const double zx = (k < kMaxU && l16 == 0) ? sh.Zx[k] : 0.0;
+      acc0 = mfma_f64(av[s], z0, acc0);
+      acc1 = mfma_f64(av[s], z1, acc1);
+      acc2 = mfma_f64(av[s], zx, acc2);
+    }
+    if (vi && ks == 0) {  // the predict's two rank-1 factors (slam.cpp:198)
+      kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
+      kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
+    }
 #pragma unroll
-        for (int a = 0; a < 10; ++a) H[a] = sh.H[c][a];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) Si[a] = sh.Si[c][a];
-        nv[0] = sh.nu[c][0];
-        nv[1] = sh.nu[c][1];
-#pragma unroll
-        for (int b = 0; b < kMaxU; ++b)
-          if (b < 3 || b >= 5 + 2 * c) {
-            mu[b][0] = sh.MU[c][b][0];
-            mu[b][1] = sh.MU[c][b][1];
-          }
-        const double v[5] = {r[0], r[1], r[2], r[3 + 2 * c], r[4 + 2 * c]};
-        double kt0 = 0.0, kt1 = 0.0;
-#pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          kt0 += v[a] * H[a];
-          kt1 += v[a] * H[5 + a];
+    for (int r = 0; r < 4; ++r) {
+      const int row = R0 + ks + 4 * r;
+      if (row < n) {
+        kc[(2 + l16) * ldk + row] = static_cast<T>(acc0[r]);
+        kc[(18 + l16) * ldk + row] = static_cast<T>(acc1[r]);
+        if (l16 == 0) {
+          int pos = -1;
+          for (int b = nu - 1; b >= 0; --b)
+            if (sh.u[b] == row) pos = b;
+          xout[row] = pos >= 0 ? xfin[pos] : xin[row] + acc2[r];
         }
-        const double K0 = kt0 * Si[0] + kt1 * Si[2];
-        const double K1 = kt0 * Si[1] + kt1 * Si[3];
-        kc[(2 + 2 * c) * ldk + i] = static_cast<T>(K0);
-        kc[(3 + 2 * c) * ldk + i] = static_cast<T>(K1);
-        xi = xi + (K0 * nv[0] + K1 * nv[1]);
-#pragma unroll
-        for (int b = 0; b < kMaxU; ++b)  // entries later steps read: {θ,x,y} ∪ markers c+1..
-          if (b < 3 || b >= 5 + 2 * c) r[b] -= K0 * mu[b][0] + K1 * mu[b][1];
       }
     }
-    for (int k = 2 + 2 * m; k < kw; ++k) kc[k * ldk + i] = static_cast<T>(0);
-    EKF_STAMP(41);
-    int pos = -1;
-    for (int b = nu - 1; b >= 0; --b)
-      if (sh.u[b] == i) pos = b;
-    xout[i] = pos >= 0 ? xfin[pos] : xi;
-    EKF_STAMP(42);
-  } else if (gi < 2 * n) {
-    const int col = gi - n;
-    double cl[kMaxU];
+  } else if (wg < 2 * row_tiles) {
+    const int C0 = (wg - row_tiles) * 16;
+    const int j = C0 + l16;
+    const bool vj = j < n;
+    const int jj = vj ? j : 0;
+    const double c0raw = vj ? static_cast<double>(S[jj]) : 0.0;
+    const double aj = first ? alpha_of(j, sh.a1, sh.a2) : 0.0;
+    double bv[9];
 #pragma unroll
-    for (int a = 0; a < kMaxU; ++a) {
-      const double v = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + col]);
-      cl[a] = a < nu ? v : 0.0;
-    }
-    const double ac = first ? alpha_of(col, sh.a1, sh.a2) : 0.0;
-    const double c0raw = cl[0];
-    if (first) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {  // rows 1, 2 carry α; the pose diagonal carries Q̄
-        double v = cl[a] + sh.alphaU[a] * c0raw;
-        v = v + (sh.col0raw[a] + sh.alphaU[a] * s00) * ac;
-        if (a == col) v += A.q;
-        cl[a] = v;
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      double v = (vj && k < nu) ? static_cast<double>(S[static_cast<size_t>(sh.u[k]) * ld + jj]) : 0.0;
+      if (first && vj && k < nu) {
+        v = v + sh.alphaU[k] * c0raw;
+        v = v + (sh.col0raw[k] + sh.alphaU[k] * s00) * aj;
+        if (sh.u[k] == j && j < 3) v += A.q;
       }
-#pragma unroll
-      for (int a = 3; a < kMaxU; ++a) cl[a] = a < nu ? cl[a] + sh.col0raw[a] * ac : 0.0;
+      bv[s] = v;
     }
-    mc[0 * ldk + col] = static_cast<T>(first ? c0raw : 0.0);
-    mc[1 * ldk + col] = static_cast<T>(first ? ac : 0.0);
+    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-    for (int c = 0; c < kMaxChunk; ++c) {
-      if (c < m) {
-        double H[10], ku[kMaxU][2];
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      const double y0 = k < kMaxU ? sh.Y[l16][k] : 0.0;
+      const double y1 = k < kMaxU ? sh.Y[16 + l16][k] : 0.0;
+      acc0 = mfma_f64(y0, bv[s], acc0);
+      acc1 = mfma_f64(y1, bv[s], acc1);
+    }
+    if (vj && ks == 0) {
+      mc[0 * ldk + j] = static_cast<T>(first ? c0raw : 0.0);
+      mc[1 * ldk + j] = static_cast<T>(first ? aj : 0.0);
+    }
+    if (vj) {
 #pragma unroll
-        for (int a = 0; a < 10; ++a) H[a] = sh.H[c][a];
-#pragma unroll
-        for (int a = 0; a < kMaxU; ++a)
-          if (a < 3 || a >= 5 + 2 * c) {
-            ku[a][0] = sh.KU[c][a][0];
-            ku[a][1] = sh.KU[c][a][1];
-          }
-        const double v[5] = {cl[0], cl[1], cl[2], cl[3 + 2 * c], cl[4 + 2 * c]};
-        double mm0 = 0.0, mm1 = 0.0;
-#pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          mm0 += H[a] * v[a];
-          mm1 += H[5 + a] * v[a];
-        }
-        mc[(2 + 2 * c) * ldk + col] = static_cast<T>(mm0);
-        mc[(3 + 2 * c) * ldk + col] = static_cast<T>(mm1);
-#pragma unroll
-        for (int a = 0; a < kMaxU; ++a)
-          if (a < 3 || a >= 5 + 2 * c) cl[a] -= ku[a][0] * mm0 + ku[a][1] * mm1;
+      for (int r = 0; r < 4; ++r) {
+        const int kr = ks + 4 * r;
+        mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
+        mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
       }
     }
-    for (int k = 2 + 2 * m; k < kw; ++k) mc[k * ldk + col] = static_cast<T>(0);
   }
+  EKF_STAMP(41);
 }
 
 // ---- Σ pass on MFMA -------------------------------------------------------------------------
-typedef double d4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 template <typename T> struct Mfma;
@@ -734,7 +758,8 @@ __global__ void k_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
 // ---- launchers ------------------------------------------------------------------------------
 template <typename T>
 hipError_t launch_gain(const PassArgs<T>& a, int nf, hipStream_t s) {
-  const dim3 grid((2 * a.n + 255) / 256, nf);
+  const int waves = 2 * ((a.n + 15) / 16);  // 16 rows or 16 columns per wave
+  const dim3 grid((waves + 3) / 4, nf);
   hipLaunchKernelGGL(k_gain<T>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }

@@ -77,8 +77,8 @@ void run(int N, int m, int reps) {
   printf("N=%d m=%d %s: gain %.2f us/launch | stamps (cycles from start): A0 %llu A1 %llu |",
          N, m, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, st[1] - st[0], st[2] - st[0]);
   for (int c = 0; c < m; ++c) printf(" s%d:%llu/%llu", c, st[3 + 2 * c] - st[0], st[4 + 2 * c] - st[0]);
-  printf(" | step0 sub: start %llu rb %llu S %llu inv %llu", st[50] - st[0], st[51] - st[0], st[52] - st[0], st[53] - st[0]);
-  printf(" | endA %llu B-rec %llu B-end %llu\n", st[40] - st[0], st[41] - st[0], st[42] - st[0]);
+
+  printf(" | endA %llu B-end %llu\n", st[40] - st[0], st[41] - st[0]);
 }
 
 int main() {
