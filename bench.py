@@ -152,6 +152,7 @@ def main():
     ekf.replay(counts[ps], rel[ps], odom[ps], ids=ids[ps], actions=act[ps])
     n_sig, ms_sig = ekf.profile_read(0)
     n_gain, ms_gain = ekf.profile_read(1)
+    n_fac, ms_fac = ekf.profile_read(3)
     ekf.profile(False)
     bytes_per_launch = ekf.sigma_pass_bytes()
     avg_sig_s = ms_sig / max(n_sig, 1) / 1e3
@@ -186,7 +187,8 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "bytes_formula": f"2*n^2*w*F = 2*{n}^2*{wsz}*{F}",
                 "avg_launch_us": avg_sig_s * 1e6, "launches": n_sig,
-                "gain_kernel_avg_us": ms_gain / max(n_gain, 1) * 1e3,
+                "chain_kernel_avg_us": ms_gain / max(n_gain, 1) * 1e3,
+                "factor_kernel_avg_us": ms_fac / max(n_fac, 1) * 1e3,
             },
         }
     # ---- CPU baseline + parity (rank 0, N=1 only) ----

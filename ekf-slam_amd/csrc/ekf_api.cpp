@@ -47,18 +47,23 @@ struct ekf_ctx {
   ekf_config cfg{};
   int n = 0, ld = 0, ldk = 0, F = 0;
   size_t w = 8;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
+  hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
+  hipEvent_t ev_fac = nullptr, ev_sig = nullptr;
   void* sig[2] = {nullptr, nullptr};
   double* x[2] = {nullptr, nullptr};
   void* kcat = nullptr;
   void* mcat = nullptr;
   FilterCtl* ctl = nullptr;
+  ChunkRec* rec = nullptr;
   MsgDesc* ddesc = nullptr;
   size_t sig_stride = 0, x_stride = 0, km_stride = 0;
   // host mirror
   std::vector<Pose2> odom;
   std::vector<int> parity;
   std::vector<char> pending;
+  std::vector<int> prev_m;       // ≥ 0: last chunk was pipelined (its factors are in Kcat/Mcat)
+  std::vector<char> prev_first;
   // launch plan: descriptors for a whole call (or a whole replay) uploaded with ONE copy
   std::vector<MsgDesc> plan_d;
   std::vector<Launch> plan_l;
@@ -70,10 +75,10 @@ struct ekf_ctx {
   std::vector<std::vector<Marker>> msgs;
   // profiling
   bool prof = false;
-  ProfEvents pe[3];
+  ProfEvents pe[4];
   std::vector<hipEvent_t> pool;
-  long long prof_launches[3] = {0, 0, 0};
-  double prof_ms[3] = {0, 0, 0};
+  long long prof_launches[4] = {0, 0, 0, 0};
+  double prof_ms[4] = {0, 0, 0, 0};
 };
 
 #define HIPCHK(expr)                       \
@@ -97,6 +102,7 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.km_stride = h->km_stride;
   a.ldk = h->ldk;
   a.ctl = h->ctl;
+  a.rec = h->rec;
   a.desc = desc;
   a.n = h->n;
   a.ld = h->ld;
@@ -119,18 +125,19 @@ hipEvent_t pool_get(ekf_ctx* h) {
   return e;
 }
 
-// Launch `fn` bracketed by events when profiling (kind 0 = Σ pass, 1 = gain, 2 = association).
+// Launch `fn` bracketed by events when profiling (kind 0 = Σ pass, 1 = chain, 2 = association,
+// 3 = factors).
 template <typename Fn>
-int timed(ekf_ctx* h, int kind, Fn fn) {
+int timed(ekf_ctx* h, int kind, hipStream_t st, Fn fn) {
   hipEvent_t a = nullptr, b = nullptr;
   if (h->prof) {
     a = pool_get(h);
     b = pool_get(h);
-    if (a) hipEventRecord(a, h->stream);
+    if (a) hipEventRecord(a, st);
   }
   const hipError_t e = fn();
   if (h->prof && a && b) {
-    hipEventRecord(b, h->stream);
+    hipEventRecord(b, st);
     h->pe[kind].start.push_back(a);
     h->pe[kind].stop.push_back(b);
   }
@@ -153,26 +160,46 @@ inline void measure(double rx, double ry, double* zr, double* zb) {
   *zb = std::atan2(ry, rx);
 }
 
+// chain → (Σ_in ready) → factors on the main stream; the Σ pass on the bulk stream once the
+// factors exist, so it overlaps the next chunk's chain. pipelined = false keeps all on main.
 template <typename T>
-int launch_pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw) {
+int launch_pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pipelined) {
   const PassArgs<T> a = args<T>(h, dptr, f0);
-  int rc = timed(h, 1, [&] { return launch_gain<T>(a, nf, h->stream); });
+  hipStream_t ms = h->stream, bs = pipelined ? h->bulk : h->stream;
+  int rc = timed(h, 1, ms, [&] { return launch_chain<T>(a, nf, ms); });
   if (rc) return rc;
-  return timed(h, 0, [&] { return launch_sigma_pass<T>(a, nf, kw, h->stream); });
+  HIPCHK(hipStreamWaitEvent(ms, h->ev_sig, 0));  // factors gather Σ_in = previous Σ pass output
+  rc = timed(h, 3, ms, [&] { return launch_factors<T>(a, nf, ms); });
+  if (rc) return rc;
+  if (pipelined) {
+    HIPCHK(hipEventRecord(h->ev_fac, ms));
+    HIPCHK(hipStreamWaitEvent(bs, h->ev_fac, 0));
+  }
+  rc = timed(h, 0, bs, [&] { return launch_sigma_pass<T>(a, nf, kw, bs); });
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(h->ev_sig, bs));
+  return EKF_OK;
 }
 
-int pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw) {
-  return h->cfg.dtype == EKF_F32 ? launch_pair<float>(h, dptr, f0, nf, kw)
-                                 : launch_pair<double>(h, dptr, f0, nf, kw);
+int pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pipelined) {
+  return h->cfg.dtype == EKF_F32 ? launch_pair<float>(h, dptr, f0, nf, kw, pipelined)
+                                 : launch_pair<double>(h, dptr, f0, nf, kw, pipelined);
+}
+
+// Both streams idle (before host reads/writes of device state).
+int drain(ekf_ctx* h) {
+  HIPCHK(hipStreamSynchronize(h->bulk));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return EKF_OK;
 }
 
 int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
   if (h->cfg.dtype == EKF_F32) {
     const PassArgs<float> a = args<float>(h, dptr, f0);
-    return timed(h, 2, [&] { return launch_assoc<float>(a, nf, h->stream); });
+    return timed(h, 2, h->stream, [&] { return launch_assoc<float>(a, nf, h->stream); });
   }
   const PassArgs<double> a = args<double>(h, dptr, f0);
-  return timed(h, 2, [&] { return launch_assoc<double>(a, nf, h->stream); });
+  return timed(h, 2, h->stream, [&] { return launch_assoc<double>(a, nf, h->stream); });
 }
 
 // Known association, one message per filter in [f0, f0+nf): msgs[k] holds filter f0+k's markers.
@@ -199,7 +226,14 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
       int flags = kActive;
       if (chunk == 0 && (predict || h->pending[f])) flags |= kFirst;
       if (chunk == nchunks - 1 && predict) flags |= kLast;
+      if (h->prev_m[f] >= 0) {  // rebuild Σ_in from the previous chunk (its Σ pass may be running)
+        flags |= kLook;
+        if (h->prev_first[f]) flags |= kPrevFirst;
+      }
       fill_desc(d, m, flags, h->parity[f], h->odom[f]);
+      d->prev_m = h->prev_m[f];
+      h->prev_m[f] = m;
+      h->prev_first[f] = (flags & kFirst) ? 1 : 0;
       for (int i = 0; i < m; ++i) {
         d->ids[i] = mk[b + i].id;
         d->z[i][0] = mk[b + i].zr;
@@ -230,6 +264,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
         continue;
       }
       int flags = kActive | kNoInit;
+      h->prev_m[f] = -1;  // association chunks run unpipelined
       if (i == 0 && (predict || h->pending[f])) flags |= kFirst;
       if (i == std::max(mf, 1) - 1 && posterior) flags |= kLast;
       const int m = mf > 0 ? 1 : 0;
@@ -248,6 +283,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
 }
 
 void plan_posterior(ekf_ctx* h, int f) {
+  h->prev_m[f] = -1;
   const size_t off = h->plan_d.size();
   h->plan_d.resize(off + 1);
   fill_desc(&h->plan_d[off], 0, kActive, h->parity[f], h->odom[f]);
@@ -267,7 +303,7 @@ int flush(ekf_ctx* h) {
   const size_t nd = h->plan_d.size();
   if (nd == 0) return EKF_OK;
   if (nd > h->ddesc_cap) {  // grow the device descriptor buffer (kernels may still read the old one)
-    HIPCHK(hipStreamSynchronize(h->stream));
+    if (drain(h)) return EKF_E_HIP;
     if (h->ddesc) HIPCHK(hipFree(h->ddesc));
     h->ddesc = nullptr;
     const size_t cap = std::max(nd, 2 * h->ddesc_cap);
@@ -287,15 +323,22 @@ int flush(ekf_ctx* h) {
     sl.cap = cap;
   }
   std::memcpy(sl.p, h->plan_d.data(), nd * sizeof(MsgDesc));
+  HIPCHK(hipStreamWaitEvent(h->stream, h->ev_sig, 0));  // the bulk stream may still read descriptors
   HIPCHK(hipMemcpyAsync(h->ddesc, sl.p, nd * sizeof(MsgDesc), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipEventRecord(sl.ev, h->stream));
   sl.used = true;
   int rc = EKF_OK;
   for (const Launch& L : h->plan_l) {
     const MsgDesc* dp = h->ddesc + L.off;
-    if (L.kind == 1) rc = assoc(h, dp, L.f0, L.nf);
-    if (!rc && L.kind <= 1) rc = pair(h, dp, L.f0, L.nf, L.kw);
-    if (!rc && L.kind == 2) rc = posterior_launch(h, dp, L.f0, L.nf);
+    if (L.kind == 1) {
+      if (hipStreamWaitEvent(h->stream, h->ev_sig, 0) != hipSuccess) return EKF_E_HIP;
+      rc = assoc(h, dp, L.f0, L.nf);
+    }
+    if (!rc && L.kind <= 1) rc = pair(h, dp, L.f0, L.nf, L.kw, L.kind == 0);
+    if (!rc && L.kind == 2) {
+      if (hipStreamWaitEvent(h->stream, h->ev_sig, 0) != hipSuccess) return EKF_E_HIP;
+      rc = posterior_launch(h, dp, L.f0, L.nf);
+    }
     if (rc) break;
   }
   h->plan_d.clear();
@@ -313,7 +356,7 @@ int assoc_sync(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int m_m
     plan_assoc(h, f0, nf, predict, posterior && i1 == mm, i0, i1);
     int rc = flush(h);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(h->stream));
+    if (drain(h)) return EKF_E_HIP;
     for (int k = 0; k < nf; ++k) {
       FilterCtl c;
       HIPCHK(hipMemcpy(&c, h->ctl + f0 + k, sizeof(FilterCtl), hipMemcpyDeviceToHost));
@@ -410,13 +453,18 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   h->odom.assign(h->F, Pose2{});
   h->parity.assign(h->F, 0);
   h->pending.assign(h->F, 0);
+  h->prev_m.assign(h->F, -1);
+  h->prev_first.assign(h->F, 0);
   h->msgs.resize(h->F);
   auto fail = [&](int rc) {
     ekf_destroy(h);
     return rc;
   };
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->bulk, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_fac, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_sig, hipEventDisableTiming) != hipSuccess)
     return fail(EKF_E_HIP);
   const size_t sig_bytes = h->sig_stride * h->F * h->w;
   for (int p = 0; p < 2; ++p) {
@@ -428,6 +476,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipMalloc(&h->kcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->mcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->ctl, sizeof(FilterCtl) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
+  if (hipMalloc(&h->rec, sizeof(ChunkRec) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
   h->ddesc_cap = static_cast<size_t>(h->F) * 4;
   if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->ddesc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
   for (int i = 0; i < kRing; ++i)
@@ -456,6 +505,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
 int ekf_destroy(ekf_t h) {
   if (!h) return EKF_E_ARG;
   hipSetDevice(h->cfg.device);
+  if (h->bulk) hipStreamSynchronize(h->bulk);
   if (h->stream) hipStreamSynchronize(h->stream);
   for (int p = 0; p < 2; ++p) {
     if (h->sig[p]) hipFree(h->sig[p]);
@@ -464,6 +514,7 @@ int ekf_destroy(ekf_t h) {
   if (h->kcat) hipFree(h->kcat);
   if (h->mcat) hipFree(h->mcat);
   if (h->ctl) hipFree(h->ctl);
+  if (h->rec) hipFree(h->rec);
   if (h->ddesc) hipFree(h->ddesc);
   for (int i = 0; i < kRing; ++i) {
     if (h->ring[i].p) hipHostFree(h->ring[i].p);
@@ -474,6 +525,9 @@ int ekf_destroy(ekf_t h) {
     for (auto e : pe.stop) hipEventDestroy(e);
   }
   for (auto e : h->pool) hipEventDestroy(e);
+  if (h->ev_fac) hipEventDestroy(h->ev_fac);
+  if (h->ev_sig) hipEventDestroy(h->ev_sig);
+  if (h->bulk) hipStreamDestroy(h->bulk);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return EKF_OK;
@@ -532,6 +586,7 @@ int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int*
   if (rc) return rc;
   {
     unsigned fl = 0;
+    if (drain(h)) return EKF_E_HIP;
     HIPCHK(hipMemcpy(&fl, &h->ctl[f].status, sizeof(unsigned), hipMemcpyDeviceToHost));
     if (fl & EKF_FLAG_RANGE) return EKF_E_RANGE;
   }
@@ -580,7 +635,7 @@ int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, con
     if (out_pose) {
       rc = flush(h);
       if (rc) return rc;
-      HIPCHK(hipStreamSynchronize(h->stream));
+      if (drain(h)) return EKF_E_HIP;
       for (size_t f = 0; f < F; ++f)
         HIPCHK(hipMemcpy(out_pose + 3 * (F * t + f), h->x[h->parity[f]] + f * h->x_stride,
                          3 * sizeof(double), hipMemcpyDeviceToHost));
@@ -641,13 +696,12 @@ int ekf_posterior(ekf_t h, int f) {
 
 int ekf_sync(ekf_t h) {
   if (!h) return EKF_E_ARG;
-  HIPCHK(hipStreamSynchronize(h->stream));
-  return EKF_OK;
+  return drain(h);
 }
 
 int ekf_get_pose(ekf_t h, int f, double* p) {
   if (!valid(h, f) || !p) return EKF_E_ARG;
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (drain(h)) return EKF_E_HIP;
   HIPCHK(hipMemcpy(p, h->x[h->parity[f]] + f * h->x_stride, 3 * sizeof(double),
                    hipMemcpyDeviceToHost));
   return EKF_OK;
@@ -655,14 +709,14 @@ int ekf_get_pose(ekf_t h, int f, double* p) {
 
 int ekf_get_map_odom(ekf_t h, int f, double* p) {
   if (!valid(h, f) || !p) return EKF_E_ARG;
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (drain(h)) return EKF_E_HIP;
   HIPCHK(hipMemcpy(p, h->ctl[f].tmo, 3 * sizeof(double), hipMemcpyDeviceToHost));
   return EKF_OK;
 }
 
 int ekf_get_state(ekf_t h, int f, double* state, double* sigma, unsigned* counter) {
   if (!valid(h, f)) return EKF_E_ARG;
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (drain(h)) return EKF_E_HIP;
   const int p = h->parity[f];
   if (state)
     HIPCHK(hipMemcpy(state, h->x[p] + f * h->x_stride, h->n * sizeof(double),
@@ -686,7 +740,8 @@ int ekf_get_state(ekf_t h, int f, double* state, double* sigma, unsigned* counte
 int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, const double* tmo,
                   unsigned counter) {
   if (!valid(h, f)) return EKF_E_ARG;
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (drain(h)) return EKF_E_HIP;
+  h->prev_m[f] = -1;
   const int p = h->parity[f];
   if (state)
     HIPCHK(hipMemcpy(h->x[p] + f * h->x_stride, state, h->n * sizeof(double),
@@ -713,7 +768,7 @@ int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, cons
 
 int ekf_get_status(ekf_t h, int f, unsigned* flags) {
   if (!valid(h, f) || !flags) return EKF_E_ARG;
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (drain(h)) return EKF_E_HIP;
   HIPCHK(hipMemcpy(flags, &h->ctl[f].status, sizeof(unsigned), hipMemcpyDeviceToHost));
   const unsigned z = 0;
   HIPCHK(hipMemcpy(&h->ctl[f].status, &z, sizeof(unsigned), hipMemcpyHostToDevice));
@@ -727,8 +782,8 @@ int ekf_profile_enable(ekf_t h, int enable) {
 }
 
 int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
-  if (!h || kind < 0 || kind > 2) return EKF_E_ARG;
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (!h || kind < 0 || kind > 3) return EKF_E_ARG;
+  if (drain(h)) return EKF_E_HIP;
   auto& pe = h->pe[kind];
   for (size_t i = 0; i < pe.start.size(); ++i) {
     float ms = 0.f;

@@ -15,12 +15,16 @@ constexpr int kMaxChunk = 16;                    // markers folded into one Σ p
 constexpr int kMaxU = 3 + 2 * kMaxChunk;         // touched rows/cols of one chunk: pose + 2 per marker
 constexpr int kMaxKW = ((2 + 2 * kMaxChunk + 3) / 4) * 4;  // rank of the fused update, padded to 4
 constexpr int kMaxAssoc = 64;                    // association slots per filter per upload
+constexpr int kZC = 2 * kMaxChunk;               // correction columns of Z / rows of Y
 
 // MsgDesc.flags
 constexpr int kFirst = 1;    // chunk carries the predict (slam.cpp:184-198) for this message
 constexpr int kLast = 2;     // chunk ends the message: posterior t_map_odom (slam.cpp:273-291)
 constexpr int kNoInit = 4;   // association path: no first-sighting init in the correction
 constexpr int kActive = 8;   // filter takes part in this launch
+constexpr int kLook = 16;    // Σ_in not materialised yet: rebuild the block from the previous
+                             // chunk's Σ_in (other buffer) and factors (Kcat/Mcat, prev_m)
+constexpr int kPrevFirst = 32;  // the previous chunk carried a predict (Q̄ in its Σ pass)
 
 // One chunk of one message for one filter (uploaded by the host, read by every kernel of the pair).
 struct alignas(16) MsgDesc {
@@ -29,18 +33,34 @@ struct alignas(16) MsgDesc {
   int parity;        // which Σ / x copy is "in"
   int assoc_slot;    // association: index into FilterCtl::assoc_j for ids[c] < 0
   double odom[3];    // t_odom_robot (θ, x, y) at this message
-  double pad0;
+  int prev_m;        // kLook: markers of the previous chunk (its factor rank)
+  int pad1;
   int ids[kMaxChunk];        // landmark ids; < 0 ⇒ taken from FilterCtl::assoc_j[assoc_slot + c]
   double z[kMaxChunk][2];    // measured (range, bearing), computed on the host like slam.cpp:208-210
 };
 
 struct alignas(16) FilterCtl {
   double tmo[3];       // t_map_odom (θ, x, y), slam.cpp:659
-  double tmo_next[3];  // posterior written by the gain kernel, committed by the Σ pass
   unsigned counter;    // counter_obstacles, slam.cpp:670
   unsigned status;     // EKF_FLAG_* bits
   int assoc_j[kMaxAssoc];
   int assoc_new[kMaxAssoc];
+};
+
+// What the chain kernel (the sequential part of a chunk) hands to the factor kernel: with
+// r(i) = Σ_pred[i][U] and c(j) = Σ_pred[U][j], K_c[i] = r(i)·Z[:, 2c..2c+1] and
+// M_c[:, j] = Y[2c..2c+1, :]·c(j); x_i += r(i)·Zx for rows outside U, xU for rows in U.
+struct alignas(16) ChunkRec {
+  int m, nu, flags, pad;
+  int u[kMaxU + 1];
+  double a1, a2, s00;                // predict: At(1,0) = a1, At(2,0) = a2; Σ_in[0][0]
+  double alphaU[kMaxU];
+  double row0raw[kMaxU];             // Σ_in[0][u_b]
+  double col0raw[kMaxU];             // Σ_in[u_a][0]
+  double Zx[kMaxU];
+  double xU[kMaxU];
+  double Z[kMaxU][kZC];
+  double Y[kZC][kMaxU];
 };
 
 }  // namespace ekfslam

@@ -31,7 +31,7 @@ namespace ekfslam {
 
 // Diagnostic build only (tools/gain_bench.hip): s_memtime stamps of block (0,0), thread 0.
 #ifdef EKF_DIAG_STAMPS
-__device__ unsigned long long g_stamps[64];
+__device__ unsigned long long g_stamps[160];
 #define EKF_STAMP(i)                                                              \
   do {                                                                            \
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                   \
@@ -72,15 +72,33 @@ __device__ __forceinline__ void predicted_pose(const FilterCtl* ctl, const MsgDe
   }
 }
 
+// 1/x and 1/√x from the hardware estimate plus two Newton steps (≤ 1 ulp; the f64 division
+// sequence is ~3× longer and sits on the correction chain).
+__device__ __forceinline__ double rcp_refined(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double rsq_refined(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double e = fma(-h * y, y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-h * y, y, 0.5);
+  return fma(y, e, y);
+}
+
 // Range-bearing model for landmark at (lx, ly) seen from pose: ẑ and the 2×5 H over
 // {θ, x, y, jx, jy} (slam.cpp:219-249).
 __device__ __forceinline__ void range_bearing(const double* pose, double lx, double ly,
                                               double* zhat, double* H0, double* H1) {
   const double ex = lx - pose[1], ey = ly - pose[2];
-  zhat[0] = sqrt(ex * ex + ey * ey);
-  zhat[1] = normalize_angle(atan2(ey, ex) - pose[0]);
   const double d = ex * ex + ey * ey;
-  const double isd = 1.0 / sqrt(d), id = 1.0 / d;  // one division each instead of four
+  const double isd = rsq_refined(d), id = isd * isd;
+  zhat[0] = d * isd;
+  zhat[1] = normalize_angle(atan2_fast(ey, ex) - pose[0]);
   H0[0] = 0.0;
   H0[1] = -ex * isd;
   H0[2] = -ey * isd;
@@ -97,7 +115,7 @@ __device__ __forceinline__ void range_bearing(const double* pose, double lx, dou
 __device__ __forceinline__ bool inv2(const double* A, double* o) {
   const double det = A[0] * A[3] - A[1] * A[2];
   if (!(fabs(det) > 0.0)) return false;
-  const double idet = 1.0 / det;
+  const double idet = rcp_refined(det);
   o[0] = A[3] * idet;
   o[1] = -A[1] * idet;
   o[2] = -A[2] * idet;
@@ -112,33 +130,43 @@ __device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-constexpr int kZC = 2 * kMaxChunk;  // correction columns of Z / rows of Y (32)
 
-struct GainShared {
+// v − (k0·m0 + k1·m1) with one fixed evaluation order, so a value rebuilt on the fly from the
+// previous buffer is bit-identical to the one the block update stores.
+__device__ __forceinline__ double rank2_sub(double v, double k0, double k1, double m0, double m1) {
+  return v - fma(k0, m0, k1 * m1);
+}
+
+struct ChainShared {
   int u[kMaxU];
   int skip[kMaxChunk];
   double alphaU[kMaxU];
   double row0raw[kMaxU];  // Σ_in[0][u_b]
   double col0raw[kMaxU];  // Σ_in[u_a][0]
-  double xU[2][kMaxU];    // ping-pong across steps (read in S1 while S2 writes)
-  double P[kMaxU][kMaxU + 1];    // Σ[U,U] after c steps (rows all, columns live)
-  double Phi[kMaxU][kMaxU + 1];  // row map: r_c[U] = r_0[U]·Φ_c   (identity at c = 0)
-  double Psi[kMaxU][kMaxU + 1];  // column map: c_c[U] = Ψ_c·c_0[U] (identity at c = 0)
+  double xU[2][kMaxU];    // ping-pong across steps
+  double P[1][kMaxU][kMaxU + 1];    // Σ[U,U] (rows all, columns live)
+  double Phi[1][kMaxU][kMaxU + 1];  // row map: r_c[U] = r_0[U]·Φ_c   (identity at c = 0)
+  double Psi[1][kMaxU][kMaxU + 1];  // column map: c_c[U] = Ψ_c·c_0[U] (identity at c = 0)
   double KU[kMaxChunk][kMaxU][2];
   double MU[kMaxChunk][kMaxU][2];
   double Z[kMaxU][kZC + 1];      // K_c[i] = r_0(i)[U] · Z[:, 2c..2c+1]
   double Y[kZC][kMaxU + 1];      // M_c[:, j] = Y[2c..2c+1, :] · c_0(j)[U]
   double Zx[kMaxU];              // Σ_c Z_c ν_c: x_i += r_0(i)[U] · Zx
   double nu[kMaxChunk][2];
+  double LK[kMaxKW][kMaxU];      // kLook: previous chunk's Kcat / Mcat at U
+  double LM[kMaxKW][kMaxU];
   double pose[3];
   double a1, a2, s00;
   int nu_cnt;
   unsigned status;
 };
 
+constexpr int kChainThreads = 256;
+
+// One workgroup per filter: the chunk's m sequential corrections on the |U|×|U| block.
 template <typename T>
-__global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
-  __shared__ GainShared sh;
+__global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
+  __shared__ ChainShared sh;
   __shared__ MsgDesc sdesc;  // the descriptor is read every step: keep it in LDS, not global
   static_assert(sizeof(MsgDesc) % 16 == 0, "MsgDesc copied as uint4");
   const MsgDesc& gd = A.desc[blockIdx.y];
@@ -149,22 +177,18 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   const MsgDesc& d = sdesc;
   const int f = A.f0 + blockIdx.y;
   const int tid = threadIdx.x;
-  const int n = A.n, ld = A.ld, ldk = A.ldk;
-  T* kc = A.kcat + f * A.km_stride;
-  T* mc = A.mcat + f * A.km_stride;
+  const int ld = A.ld;
   FilterCtl* ctl = A.ctl + f;
-  // zero the GEMM operands (padding must be exactly 0, not stale LDS)
   for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.Z[0][0])[e] = 0.0;
   for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.Y[0][0])[e] = 0.0;
   __syncthreads();
   EKF_STAMP(0);
   const T* S = A.sig[d.parity] + f * A.sig_stride;
   const double* xin = A.x[d.parity] + f * A.x_stride;
-  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
   const int m = d.m;
   const bool first = (d.flags & kFirst) != 0;
 
-  // ---- phase A0: predict pose, index set U --------------------------------------------------
+  // ---- A0: predict pose, index set U --------------------------------------------------------
   if (tid == 0) {
     double a1, a2;
     predicted_pose(ctl, d, xin, sh.pose, &a1, &a2);
@@ -191,12 +215,39 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   EKF_STAMP(1);
   const int nu = sh.nu_cnt;
 
-  // ---- phase A1: gather the |U|×|U| block, x[U], identities ----------------------------------
-  for (int e = tid; e < nu * nu; e += blockDim.x) {
-    const int a = e / nu, b = e - a * nu;
-    sh.P[a][b] = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]]);
-    sh.Phi[a][b] = a == b ? 1.0 : 0.0;
-    sh.Psi[a][b] = a == b ? 1.0 : 0.0;
+  // ---- A1: gather the |U|×|U| block, x[U], identities --------------------------------------
+  // kLook: the previous chunk's Σ pass may still be running, so rebuild Σ_in[U,U] from that
+  // chunk's Σ_in (the other buffer) and its factors, in the Σ pass's own order (Σ + Q̄, then one
+  // fma per rank-1 term in k order, in T) — the values the Σ pass writes.
+  if (d.flags & kLook) {
+    const T* Sp = A.sig[d.parity ^ 1] + f * A.sig_stride;
+    const T* kcp = A.kcat + f * A.km_stride;
+    const T* mcp = A.mcat + f * A.km_stride;
+    const int kwp = ((2 + 2 * d.prev_m + 3) / 4) * 4;
+    for (int e = tid; e < kwp * nu; e += blockDim.x) {
+      const int k = e / nu, a = e - k * nu;
+      sh.LK[k][a] = static_cast<double>(kcp[static_cast<size_t>(k) * A.ldk + sh.u[a]]);
+      sh.LM[k][a] = static_cast<double>(mcp[static_cast<size_t>(k) * A.ldk + sh.u[a]]);
+    }
+    __syncthreads();
+    const T q = static_cast<T>(A.q);
+    for (int e = tid; e < nu * nu; e += blockDim.x) {
+      const int a = e / nu, b = e - a * nu;
+      T acc = Sp[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]];
+      if ((d.flags & kPrevFirst) && sh.u[a] == sh.u[b] && sh.u[a] < 3) acc += q;
+      for (int k = 0; k < kwp; ++k)
+        acc = fma(-static_cast<T>(sh.LK[k][a]), static_cast<T>(sh.LM[k][b]), acc);
+      sh.P[0][a][b] = static_cast<double>(acc);
+      sh.Phi[0][a][b] = a == b ? 1.0 : 0.0;
+      sh.Psi[0][a][b] = a == b ? 1.0 : 0.0;
+    }
+  } else {
+    for (int e = tid; e < nu * nu; e += blockDim.x) {
+      const int a = e / nu, b = e - a * nu;
+      sh.P[0][a][b] = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]]);
+      sh.Phi[0][a][b] = a == b ? 1.0 : 0.0;
+      sh.Psi[0][a][b] = a == b ? 1.0 : 0.0;
+    }
   }
   if (tid < nu) {
     sh.xU[0][tid] = tid < 3 ? sh.pose[tid] : xin[sh.u[tid]];
@@ -204,31 +255,33 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
   }
   __syncthreads();
   if (tid < nu) {
-    sh.row0raw[tid] = sh.P[0][tid];
-    sh.col0raw[tid] = sh.P[tid][0];
+    sh.row0raw[tid] = sh.P[0][0][tid];
+    sh.col0raw[tid] = sh.P[0][tid][0];
   }
-  if (tid == 0) sh.s00 = sh.P[0][0];
+  if (tid == 0) sh.s00 = sh.P[0][0][0];
   __syncthreads();
   // predict folded in: P ← A P Aᵀ + Q̄ on the block (slam.cpp:198)
   if (first) {
     for (int e = tid; e < nu * nu; e += blockDim.x) {
       const int a = e / nu, b = e - a * nu;
-      double v = sh.P[a][b] + sh.alphaU[a] * sh.row0raw[b];
+      double v = sh.P[0][a][b] + sh.alphaU[a] * sh.row0raw[b];
       v = v + (sh.col0raw[a] + sh.alphaU[a] * sh.s00) * sh.alphaU[b];
       if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
-      sh.P[a][b] = v;
+      sh.P[0][a][b] = v;
     }
   }
   __syncthreads();
   EKF_STAMP(2);
 
-  // ---- phase A2: the m corrections on the block ---------------------------------------------
-  // S1: every thread recomputes ẑ, H, S⁻¹, ν (no serial section). S2: K[U], Z (rows of Φ), x[U];
-  // M[:, live]; Y (columns of Ψ). S3: P, Φ (live columns) and Ψ (live rows) lose the step's
-  // rank-2 term. "Live" = what later steps still read: {θ,x,y} ∪ markers c+1.. .
-  const int s3a = tid / 7, s3j = tid - 7 * (tid / 7);  // S3 layout: 36 rows × 7 threads
+  // ---- A2: the m corrections -----------------------------------------------------------------
+  // Per step: S1 every wave recomputes ẑ, H, S⁻¹, ν (one wave per SIMD, no serial section); S2
+  // wave 0 forms K[U], Z_c, x[U], wave 1 M[:, live], wave 2 Y_c; S3 all threads apply the step's
+  // rank-2 term to P and Φ (live columns) and Ψ (live rows). "Live" = what later steps still read.
+  const int wave = tid >> 6, lane = tid & 63;
+  const int s3a = tid / 7, s3j = tid - 7 * (tid / 7);  // S3: 36 rows × 7 threads
   for (int c = 0; c < m; ++c) {
     const int pj = 3 + 2 * c;
+    EKF_STAMP(64 + 6 * c);
     const int cur = c & 1, nxt = cur ^ 1;
     const double* xc = sh.xU[cur];
     const double z0 = d.z[c][0], z1 = d.z[c][1];
@@ -246,13 +299,14 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
     {
       double zhat[2];
       range_bearing(pose, lx, ly, zhat, H0, H1);
+      EKF_STAMP(65 + 6 * c);
       double HP0[5], HP1[5];
 #pragma unroll
       for (int bb = 0; bb < 5; ++bb) {
         double s0 = 0.0, s1 = 0.0;
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
-          const double v = sh.P[pA[a]][pA[bb]];
+          const double v = sh.P[0][pA[a]][pA[bb]];
           s0 += H0[a] * v;
           s1 += H1[a] * v;
         }
@@ -283,64 +337,62 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
       nv0 = nv1 = 0.0;
     }
-    // W = Hᵀ·S⁻¹ (5×2): K = row[pA]·W
-    double W0[5], W1[5];
-#pragma unroll
-    for (int a = 0; a < 5; ++a) {
-      W0[a] = H0[a] * Si[0] + H1[a] * Si[2];
-      W1[a] = H0[a] * Si[1] + H1[a] * Si[3];
-    }
     const int jx = sh.u[pj];
-    if (tid < kMaxU) {  // K[U], Z_c, x[U]
+    EKF_STAMP(66 + 6 * c);
+    if (wave == 0 && lane < kMaxU) {  // K[U], Z_c = Φ[:, pA]·Hᵀ·S⁻¹, x[U]
       double K0 = 0.0, K1 = 0.0, Z0 = 0.0, Z1 = 0.0;
-      if (tid < nu) {
-        double kt0 = 0.0, kt1 = 0.0, zt0 = 0.0, zt1 = 0.0;
+      if (lane < nu) {
+        double ka = 0.0, kb = 0.0, pa = 0.0, pb = 0.0;
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
-          const double v = sh.P[tid][pA[a]];
-          kt0 += v * H0[a];
-          kt1 += v * H1[a];
-          const double w = sh.Phi[tid][pA[a]];
-          zt0 += w * W0[a];
-          zt1 += w * W1[a];
+          const double v = sh.P[0][lane][pA[a]];
+          const double w = sh.Phi[0][lane][pA[a]];
+          ka += v * H0[a];
+          kb += v * H1[a];
+          pa += w * H0[a];
+          pb += w * H1[a];
         }
-        K0 = kt0 * Si[0] + kt1 * Si[2];
-        K1 = kt0 * Si[1] + kt1 * Si[3];
-        Z0 = zt0;
-        Z1 = zt1;
-        double xt = xc[tid];
+        K0 = ka * Si[0] + kb * Si[2];
+        K1 = ka * Si[1] + kb * Si[3];
+        Z0 = pa * Si[0] + pb * Si[2];
+        Z1 = pa * Si[1] + pb * Si[3];
+        double xt = xc[lane];
         if (init) {
-          if (sh.u[tid] == jx) xt = lx;
-          else if (sh.u[tid] == jx + 1) xt = ly;
+          if (sh.u[lane] == jx) xt = lx;
+          else if (sh.u[lane] == jx + 1) xt = ly;
         }
         xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
-        if (tid == 0) xt = normalize_angle(xt);      // slam.cpp:267
-        sh.xU[nxt][tid] = xt;
+        if (lane == 0) xt = normalize_angle(xt);     // slam.cpp:267
+        sh.xU[nxt][lane] = xt;
       }
-      sh.KU[c][tid][0] = K0;
-      sh.KU[c][tid][1] = K1;
-      sh.Z[tid][2 * c] = Z0;
-      sh.Z[tid][2 * c + 1] = Z1;
-    } else if (tid >= 64 && tid < 64 + kMaxU) {  // M[:, live]
-      const int b = tid - 64;
+      sh.KU[c][lane][0] = K0;
+      sh.KU[c][lane][1] = K1;
+      sh.Z[lane][2 * c] = Z0;
+      sh.Z[lane][2 * c + 1] = Z1;
+      if (lane == 0) {
+        sh.nu[c][0] = nv0;
+        sh.nu[c][1] = nv1;
+      }
+    } else if (wave == 1 && lane < kMaxU) {  // M[:, live]
+      const int b = lane;
       double mm0 = 0.0, mm1 = 0.0;
       if (b < nu && (b < 3 || b >= pj + 2)) {
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
-          const double v = sh.P[pA[a]][b];
+          const double v = sh.P[0][pA[a]][b];
           mm0 += H0[a] * v;
           mm1 += H1[a] * v;
         }
       }
       sh.MU[c][b][0] = mm0;
       sh.MU[c][b][1] = mm1;
-    } else if (tid >= 128 && tid < 128 + kMaxU) {  // Y_c = H·Ψ[pA, :]
-      const int b = tid - 128;
+    } else if (wave == 2 && lane < kMaxU) {  // Y_c = H·Ψ[pA, :]
+      const int b = lane;
       double y0 = 0.0, y1 = 0.0;
       if (b < nu) {
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
-          const double v = sh.Psi[pA[a]][b];
+          const double v = sh.Psi[0][pA[a]][b];
           y0 += H0[a] * v;
           y1 += H1[a] * v;
         }
@@ -348,13 +400,9 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       sh.Y[2 * c][b] = y0;
       sh.Y[2 * c + 1][b] = y1;
     }
-    if (tid == 0) {
-      sh.nu[c][0] = nv0;
-      sh.nu[c][1] = nv1;
-    }
-    EKF_STAMP(3 + 2 * c);
+    EKF_STAMP(67 + 6 * c);
     __syncthreads();
-    // S3: all operands of a thread are independent loads (issued together, one wait)
+    EKF_STAMP(68 + 6 * c);
     const int live = 3 + (nu - pj - 2);
     if (s3a < nu) {
       const double ka0 = sh.KU[c][s3a][0], ka1 = sh.KU[c][s3a][1];
@@ -367,14 +415,14 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
           const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
           const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
           const double kb0 = sh.KU[c][b][0], kb1 = sh.KU[c][b][1];
-          sh.P[s3a][b] -= ka0 * mb0 + ka1 * mb1;
-          sh.Phi[s3a][b] -= za0 * mb0 + za1 * mb1;
-          sh.Psi[b][s3a] -= kb0 * ya0 + kb1 * ya1;
+          sh.P[0][s3a][b] = rank2_sub(sh.P[0][s3a][b], ka0, ka1, mb0, mb1);
+          sh.Phi[0][s3a][b] = rank2_sub(sh.Phi[0][s3a][b], za0, za1, mb0, mb1);
+          sh.Psi[0][b][s3a] = rank2_sub(sh.Psi[0][b][s3a], kb0, kb1, ya0, ya1);
         }
       }
     }
+    EKF_STAMP(69 + 6 * c);
     __syncthreads();
-    EKF_STAMP(4 + 2 * c);
   }
   const double* xfin = sh.xU[m & 1];
   if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
@@ -382,19 +430,98 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
     for (int c = 0; c < m; ++c) zx += sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];
     sh.Zx[tid] = zx;
   }
-  if (blockIdx.x == 0 && tid == 0) {
+  if (tid == 0) {
     if (sh.status) atomicOr(&ctl->status, sh.status);
     if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
       const Pose2 tmo = compose(Pose2{xfin[0], xfin[1], xfin[2]},
                                 inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
-      ctl->tmo_next[0] = tmo.theta;
-      ctl->tmo_next[1] = tmo.x;
-      ctl->tmo_next[2] = tmo.y;
+      ctl->tmo[0] = tmo.theta;
+      ctl->tmo[1] = tmo.x;
+      ctl->tmo[2] = tmo.y;
     }
   }
   __syncthreads();
+  // hand the chunk to the factor kernel
+  ChunkRec* rec = A.rec + f;
+  for (int e = tid; e < kMaxU * kZC; e += blockDim.x) {
+    const int b = e / kZC, k = e - b * kZC;
+    rec->Z[b][k] = sh.Z[b][k];
+  }
+  for (int e = tid; e < kZC * kMaxU; e += blockDim.x) {
+    const int k = e / kMaxU, b = e - k * kMaxU;
+    rec->Y[k][b] = sh.Y[k][b];
+  }
+  if (tid < kMaxU) {
+    const bool in = tid < nu;
+    rec->u[tid] = sh.u[tid];
+    rec->alphaU[tid] = in ? sh.alphaU[tid] : 0.0;
+    rec->row0raw[tid] = in ? sh.row0raw[tid] : 0.0;
+    rec->col0raw[tid] = in ? sh.col0raw[tid] : 0.0;
+    rec->Zx[tid] = sh.Zx[tid];
+    rec->xU[tid] = in ? xfin[tid] : 0.0;
+  }
+  if (tid == 0) {
+    rec->m = m;
+    rec->nu = nu;
+    rec->flags = d.flags;
+    rec->a1 = sh.a1;
+    rec->a2 = sh.a2;
+    rec->s00 = sh.s00;
+  }
   EKF_STAMP(40);
+}
 
+struct FactorShared {
+  int u[kMaxU + 1];
+  double alphaU[kMaxU], row0raw[kMaxU], col0raw[kMaxU], Zx[kMaxU], xU[kMaxU];
+  double Z[kMaxU][kZC + 1];
+  double Y[kZC][kMaxU + 1];
+  double a1, a2, s00;
+  int nu;
+};
+
+// Kcat = R_pred·Z (rows) and Mcat = Y·C_pred (columns) on f64 MFMA, plus the new state.
+// 16 rows or 16 columns per wave; R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j].
+template <typename T>
+__global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
+  __shared__ FactorShared sh;
+  const MsgDesc& d = A.desc[blockIdx.y];
+  if (!(d.flags & kActive)) return;
+  const int f = A.f0 + blockIdx.y;
+  const int tid = threadIdx.x;
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const T* S = A.sig[d.parity] + f * A.sig_stride;
+  const double* xin = A.x[d.parity] + f * A.x_stride;
+  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
+  T* kc = A.kcat + f * A.km_stride;
+  T* mc = A.mcat + f * A.km_stride;
+  const ChunkRec* rec = A.rec + f;
+  const bool first = (d.flags & kFirst) != 0;
+  for (int e = tid; e < kMaxU * kZC; e += blockDim.x) {
+    const int b = e / kZC, k = e - b * kZC;
+    sh.Z[b][k] = rec->Z[b][k];
+  }
+  for (int e = tid; e < kZC * kMaxU; e += blockDim.x) {
+    const int k = e / kMaxU, b = e - k * kMaxU;
+    sh.Y[k][b] = rec->Y[k][b];
+  }
+  if (tid < kMaxU) {
+    sh.u[tid] = rec->u[tid];
+    sh.alphaU[tid] = rec->alphaU[tid];
+    sh.row0raw[tid] = rec->row0raw[tid];
+    sh.col0raw[tid] = rec->col0raw[tid];
+    sh.Zx[tid] = rec->Zx[tid];
+    sh.xU[tid] = rec->xU[tid];
+  }
+  if (tid == 0) {
+    sh.a1 = rec->a1;
+    sh.a2 = rec->a2;
+    sh.s00 = rec->s00;
+    sh.nu = rec->nu;
+  }
+  __syncthreads();
+  const int nu = sh.nu;
+  const double* xfin = sh.xU;
   // ---- phase B: Kcat = R_pred·Z, Mcat = Y·C_pred on f64 MFMA, 16 rows (or columns) per wave ----
   // R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j] (predict folded in as above).
   const int lane = tid & 63;
@@ -491,8 +618,8 @@ __global__ __launch_bounds__(256) void k_gain(PassArgs<T> A) {
       }
     }
   }
-  EKF_STAMP(41);
 }
+
 
 // ---- Σ pass on MFMA -------------------------------------------------------------------------
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -532,13 +659,6 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles) {
   const bool first = (d.flags & kFirst) != 0;
   const T q = static_cast<T>(A.q);
   const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
-
-  if (blockIdx.x == 0 && threadIdx.x == 0 && (d.flags & kLast)) {
-    FilterCtl* ctl = A.ctl + f;
-    ctl->tmo[0] = ctl->tmo_next[0];
-    ctl->tmo[1] = ctl->tmo_next[1];
-    ctl->tmo[2] = ctl->tmo_next[2];
-  }
 
   const int tr = blockIdx.x / tiles, tc = blockIdx.x - tr * tiles;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -757,10 +877,16 @@ __global__ void k_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
 
 // ---- launchers ------------------------------------------------------------------------------
 template <typename T>
-hipError_t launch_gain(const PassArgs<T>& a, int nf, hipStream_t s) {
+hipError_t launch_chain(const PassArgs<T>& a, int nf, hipStream_t s) {
+  hipLaunchKernelGGL(k_chain<T>, dim3(1, nf), dim3(kChainThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s) {
   const int waves = 2 * ((a.n + 15) / 16);  // 16 rows or 16 columns per wave
   const dim3 grid((waves + 3) / 4, nf);
-  hipLaunchKernelGGL(k_gain<T>, grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_factors<T>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -793,7 +919,8 @@ hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
 }
 
 #define EKF_INSTANTIATE(T)                                                              \
-  template hipError_t launch_gain<T>(const PassArgs<T>&, int, hipStream_t);             \
+  template hipError_t launch_chain<T>(const PassArgs<T>&, int, hipStream_t);            \
+  template hipError_t launch_factors<T>(const PassArgs<T>&, int, hipStream_t);          \
   template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, int, hipStream_t);  \
   template hipError_t launch_assoc<T>(const PassArgs<T>&, int, hipStream_t);            \
   template hipError_t launch_posterior<T>(const PassArgs<T>&, int, hipStream_t);              \

@@ -21,15 +21,20 @@ struct PassArgs {
   size_t km_stride;
   int ldk;
   FilterCtl* ctl;
+  ChunkRec* rec;        // one per filter
   const MsgDesc* desc;
   int n, ld, N, f0;
   double q, r, gate;
 };
 
-// Fused gain kernel: small-block sequential corrections + per-row/per-column recursions that emit
-// Kcat/Mcat and the new state. Grid (ceil(2n/256), filters).
+// Chain kernel: the chunk's sequential corrections on the |U|×|U| block (predict folded in),
+// one workgroup per filter → ChunkRec.
 template <typename T>
-hipError_t launch_gain(const PassArgs<T>& a, int n_filters, hipStream_t s);
+hipError_t launch_chain(const PassArgs<T>& a, int n_filters, hipStream_t s);
+
+// Factor kernel: Kcat = R·Z, Mcat = Y·C on f64 MFMA and the new state. 16 rows / columns per wave.
+template <typename T>
+hipError_t launch_factors(const PassArgs<T>& a, int n_filters, hipStream_t s);
 
 // Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, 64×64 tiles. kw = padded rank for this launch.
 template <typename T>

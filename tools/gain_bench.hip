@@ -30,6 +30,7 @@ void run(int N, int m, int reps) {
   T *dS[2], *kc, *mc;
   double* dx[2];
   FilterCtl* ctl;
+  ChunkRec* rec;
   MsgDesc* dd;
   for (int p = 0; p < 2; ++p) {
     CK(hipMalloc(&dS[p], S.size() * sizeof(T)));
@@ -41,6 +42,7 @@ void run(int N, int m, int reps) {
   CK(hipMalloc(&mc, kMaxKW * ldk * sizeof(T)));
   CK(hipMalloc(&ctl, sizeof(FilterCtl)));
   CK(hipMemset(ctl, 0, sizeof(FilterCtl)));
+  CK(hipMalloc(&rec, sizeof(ChunkRec)));
   MsgDesc d{};
   d.m = m;
   d.flags = kActive | kFirst | kLast;
@@ -57,28 +59,44 @@ void run(int N, int m, int reps) {
   a.sig[0] = dS[0]; a.sig[1] = dS[1]; a.sig_stride = 0;
   a.x[0] = dx[0]; a.x[1] = dx[1]; a.x_stride = 0;
   a.kcat = kc; a.mcat = mc; a.km_stride = 0; a.ldk = ldk;
-  a.ctl = ctl; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0;
+  a.ctl = ctl; a.rec = rec; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0;
   a.q = 1e-2; a.r = 1e-2; a.gate = 2.0;
   hipStream_t s;
   CK(hipStreamCreate(&s));
-  for (int i = 0; i < 5; ++i) CK(launch_gain<T>(a, 1, s));
+  for (int i = 0; i < 5; ++i) CK(launch_chain<T>(a, 1, s));
   CK(hipStreamSynchronize(s));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, s));
-  for (int i = 0; i < reps; ++i) CK(launch_gain<T>(a, 1, s));
+  for (int i = 0; i < reps; ++i) CK(launch_chain<T>(a, 1, s));
   CK(hipEventRecord(e1, s));
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
-  unsigned long long st[64];
+  unsigned long long st[160];
   CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
-  printf("N=%d m=%d %s: gain %.2f us/launch | stamps (cycles from start): A0 %llu A1 %llu |",
-         N, m, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, st[1] - st[0], st[2] - st[0]);
-  for (int c = 0; c < m; ++c) printf(" s%d:%llu/%llu", c, st[3 + 2 * c] - st[0], st[4 + 2 * c] - st[0]);
-
-  printf(" | endA %llu B-end %llu\n", st[40] - st[0], st[41] - st[0]);
+  printf("N=%d m=%d %s: chain %.2f us/launch | A0 %llu A1 %llu endA %llu | per step (avg cycles):",
+         N, m, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, st[1] - st[0], st[2] - st[0],
+         st[40] - st[0]);
+  const char* nm[6] = {"rb", "S+inv", "S2", "bar1", "S3", "bar2"};
+  const int pts[7] = {64, 65, 66, 67, 68, 69, 70};
+  for (int p = 0; p < 6; ++p) {
+    double acc = 0;
+    for (int c = 0; c < m; ++c) {
+      const unsigned long long a0 = st[pts[p] + 6 * c];
+      const unsigned long long a1 = p < 5 ? st[pts[p + 1] + 6 * c] : (c + 1 < m ? st[64 + 6 * (c + 1)] : st[40]);
+      acc += static_cast<double>(a1 - a0);
+    }
+    printf(" %s %.0f", nm[p], acc / m);
+  }
+  printf("\n");
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < reps; ++i) CK(launch_factors<T>(a, 1, s));
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("    factors %.2f us/launch\n", ms * 1e3 / reps);
 }
 
 int main() {
