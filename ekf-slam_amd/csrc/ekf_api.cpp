@@ -1,8 +1,10 @@
 // Host runtime behind include/ekf.h: device memory, the handle's HIP stream, message staging and
 // the launch sequence for the reference's two callbacks (nuslam/src/slam.cpp:180-316, :318-530).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -184,6 +186,38 @@ int launch_pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pi
 int pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pipelined) {
   return h->cfg.dtype == EKF_F32 ? launch_pair<float>(h, dptr, f0, nf, kw, pipelined)
                                  : launch_pair<double>(h, dptr, f0, nf, kw, pipelined);
+}
+
+// The chain → factors kernels of a message are a latency-bound critical path; the Σ pass of the
+// previous chunk runs beside them on the bulk stream and, sharing their CUs, slowed the chain by
+// ~35 %. With few filters the two streams get disjoint CU masks: the main stream kCuSplit CUs per
+// XCD, the bulk stream the rest (a CU mask must leave every XCD at least one CU; mask bit b lands on
+// XCD b mod 8). EKF_CU_SPLIT=<CUs per XCD> overrides, 0 disables.
+constexpr int kCuSplit = 4;
+constexpr int kCuSplitMaxFilters = 32;
+
+int create_streams(ekf_ctx* h) {
+  int split = h->F <= kCuSplitMaxFilters ? kCuSplit : 0;
+  if (const char* e = std::getenv("EKF_CU_SPLIT")) split = std::atoi(e);
+  hipDeviceProp_t prop;
+  int cus = 0;
+  if (split > 0 && hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess)
+    cus = prop.multiProcessorCount;
+  constexpr int kXcd = 8;
+  if (split > 0 && cus % kXcd == 0 && split * kXcd < cus) {
+    const int words = (cus + 31) / 32;
+    std::vector<uint32_t> mmain(words, 0), mbulk(words, 0);
+    for (int b = 0; b < cus; ++b) (b < split * kXcd ? mmain : mbulk)[b / 32] |= 1u << (b % 32);
+    if (hipExtStreamCreateWithCUMask(&h->stream, words, mmain.data()) == hipSuccess &&
+        hipExtStreamCreateWithCUMask(&h->bulk, words, mbulk.data()) == hipSuccess)
+      return EKF_OK;
+    if (h->stream) hipStreamDestroy(h->stream);
+    h->stream = nullptr;
+  }
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->bulk, hipStreamNonBlocking) != hipSuccess)
+    return EKF_E_HIP;
+  return EKF_OK;
 }
 
 // Both streams idle (before host reads/writes of device state).
@@ -461,8 +495,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     return rc;
   };
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->bulk, hipStreamNonBlocking) != hipSuccess ||
+  if (create_streams(h) != EKF_OK ||
       hipEventCreateWithFlags(&h->ev_fac, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_sig, hipEventDisableTiming) != hipSuccess)
     return fail(EKF_E_HIP);

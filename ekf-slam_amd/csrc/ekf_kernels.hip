@@ -43,6 +43,25 @@ __device__ unsigned long long g_stamps[160];
   } while (0)
 #endif
 
+// Diagnostic build only (tools/sigma_bench.hip): s_memrealtime (100 MHz) per Σ-pass workgroup.
+#ifdef EKF_DIAG_STAMPS
+__device__ unsigned long long g_sig_stamps[4096][5];
+#define SIG_STAMP(i)                                                                   \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4096) {                    \
+      g_sig_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();                  \
+      if (i == 0)                                                                      \
+        g_sig_stamps[blockIdx.x][4] =                                                  \
+            (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11))) << 32) | \
+            __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));                \
+    }                                                                                  \
+  } while (0)
+#else
+#define SIG_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 #define EKF_FLAG_RANGE_D 1u
 #define EKF_FLAG_NUMERIC_D 2u
 
@@ -622,85 +641,119 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
 
 
 // ---- Σ pass on MFMA -------------------------------------------------------------------------
-typedef float f4 __attribute__((ext_vector_type(4)));
+// Σ_out = Σ_in + Q̄ − Σ_k Kcat[k]ᵀ ⊗ Mcat[k]. Block tile 64×64, four waves of 32×32. Every operand
+// of a wave is loaded before the first MFMA (one wait), and the accumulator layout makes each load
+// / store instruction cover whole 128-B rows:
+//   fp64  v_mfma_f64_16x16x4_f64 (2×2 tiles): D[row = (lane>>4) + 4r][col = lane&15] → 4 rows × 128 B
+//   fp32  v_mfma_f32_32x32x2_f32 (1 tile):    D[row = (r&3) + 8(r>>2) + 4(lane>>5)][col = lane&31]
+//         → 2 rows × 128 B
+// Loads are unconditional — Kcat/Mcat hold kMaxKW rows × ldk columns, Σ indices are clamped — since
+// a predicated load becomes a branch with its own wait. Clamped lanes only feed D elements that
+// are never stored (an MFMA's D[i][j] reads only C[i][j], A[i][:], B[:][j]); rows ≥ kw are skipped
+// a whole k-step at a time.
+// A/B lane maps: 16x16x4 A[i = lane&15][k = lane>>4]; 32x32x2 A[i = lane&31][k = lane>>5].
+typedef float f16v __attribute__((ext_vector_type(16)));
 
-template <typename T> struct Mfma;
-template <> struct Mfma<double> {
-  using acc_t = d4;
-  // v_mfma_f64_16x16x4_f64: D[row = (lane>>4) + 4r][col = lane&15]
-  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
-  static __device__ __forceinline__ acc_t op(double a, double b, acc_t c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+__device__ __forceinline__ void sigma_tile(const double* Sin, double* Sout, const double* kc,
+                                           const double* mc, int n, int ld, int ldk, int kw,
+                                           bool first, double q, int R0, int C0, int lane) {
+  const int kr = lane >> 4, kcol = lane & 15;
+  double a[2][9], b[2][9];
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const double* krow = kc + static_cast<size_t>(4 * s + kr) * ldk;
+    const double* mrow = mc + static_cast<size_t>(4 * s + kr) * ldk;
+    a[0][s] = -krow[R0 + kcol];
+    a[1][s] = -krow[R0 + 16 + kcol];
+    b[0][s] = mrow[C0 + kcol];
+    b[1][s] = mrow[C0 + 16 + kcol];
   }
-};
-template <> struct Mfma<float> {
-  using acc_t = f4;
-  // v_mfma_f32_16x16x4_f32: D[row = 4(lane>>4) + r][col = lane&15]
-  static __device__ __forceinline__ int row(int lane, int r) { return 4 * (lane >> 4) + r; }
-  static __device__ __forceinline__ acc_t op(float a, float b, acc_t c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-};
-
-// Block tile 64×64, four waves of 32×32 (2×2 MFMA tiles of 16×16). A operand lane map for both
-// shapes: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15].
-template <typename T>
-__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles) {
-  using M = Mfma<T>;
-  using acc_t = typename M::acc_t;
-  const MsgDesc& d = A.desc[blockIdx.y];
-  if (!(d.flags & kActive)) return;
-  const int f = A.f0 + blockIdx.y;
-  const int n = A.n, ld = A.ld, ldk = A.ldk;
-  const T* Sin = A.sig[d.parity] + f * A.sig_stride;
-  T* Sout = A.sig[d.parity ^ 1] + f * A.sig_stride;
-  const T* kc = A.kcat + f * A.km_stride;
-  const T* mc = A.mcat + f * A.km_stride;
-  const bool first = (d.flags & kFirst) != 0;
-  const T q = static_cast<T>(A.q);
-  const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
-
-  const int tr = blockIdx.x / tiles, tc = blockIdx.x - tr * tiles;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int R0 = tr * 64 + (w >> 1) * 32, C0 = tc * 64 + (w & 1) * 32;
-  if (R0 >= n || C0 >= n) return;
-
-  acc_t acc[2][2];
+  d4 acc[2][2];
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
     for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = R0 + 16 * ti + M::row(lane, r);
-        const int col = C0 + 16 * tj + (lane & 15);
-        T v = (row < n && col < n) ? Sin[static_cast<size_t>(row) * ld + col] : static_cast<T>(0);
+        const int row = R0 + 16 * ti + kr + 4 * r;
+        const int col = C0 + 16 * tj + kcol;
+        double v = Sin[static_cast<size_t>(min(row, n - 1)) * ld + min(col, n - 1)];
         if (first && row == col && row < 3) v += q;
         acc[ti][tj][r] = v;
       }
-
-  const int kr = lane >> 4, kcol = lane & 15;
-  for (int s = 0; s < kw; s += 4) {
-    const T* krow = kc + static_cast<size_t>(s + kr) * ldk;
-    const T* mrow = mc + static_cast<size_t>(s + kr) * ldk;
-    T a0 = -krow[R0 + kcol], a1 = -krow[R0 + 16 + kcol];
-    T b0 = mrow[C0 + kcol], b1 = mrow[C0 + 16 + kcol];
-    acc[0][0] = M::op(a0, b0, acc[0][0]);
-    acc[0][1] = M::op(a0, b1, acc[0][1]);
-    acc[1][0] = M::op(a1, b0, acc[1][0]);
-    acc[1][1] = M::op(a1, b1, acc[1][1]);
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    if (4 * s < kw) {
+      acc[0][0] = mfma_f64(a[0][s], b[0][s], acc[0][0]);
+      acc[0][1] = mfma_f64(a[0][s], b[1][s], acc[0][1]);
+      acc[1][0] = mfma_f64(a[1][s], b[0][s], acc[1][0]);
+      acc[1][1] = mfma_f64(a[1][s], b[1][s], acc[1][1]);
+    }
   }
-
+  SIG_STAMP(2);
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
     for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = R0 + 16 * ti + M::row(lane, r);
-        const int col = C0 + 16 * tj + (lane & 15);
+        const int row = R0 + 16 * ti + kr + 4 * r;
+        const int col = C0 + 16 * tj + kcol;
         if (row < n && col < n) Sout[static_cast<size_t>(row) * ld + col] = acc[ti][tj][r];
       }
+}
+
+__device__ __forceinline__ void sigma_tile(const float* Sin, float* Sout, const float* kc,
+                                           const float* mc, int n, int ld, int ldk, int kw,
+                                           bool first, double qd, int R0, int C0, int lane) {
+  const int kr = lane >> 5, kcol = lane & 31;
+  const float q = static_cast<float>(qd);
+  float a[18], b[18];
+#pragma unroll
+  for (int s = 0; s < 18; ++s) {
+    a[s] = -kc[static_cast<size_t>(2 * s + kr) * ldk + R0 + kcol];
+    b[s] = mc[static_cast<size_t>(2 * s + kr) * ldk + C0 + kcol];
+  }
+  f16v acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
+    const int col = C0 + kcol;
+    float v = Sin[static_cast<size_t>(min(row, n - 1)) * ld + min(col, n - 1)];
+    if (first && row == col && row < 3) v += q;
+    acc[r] = v;
+  }
+#pragma unroll
+  for (int s = 0; s < 18; ++s)
+    if (2 * s < kw) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+  SIG_STAMP(2);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
+    const int col = C0 + kcol;
+    if (row < n && col < n) Sout[static_cast<size_t>(row) * ld + col] = acc[r];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles) {
+  SIG_STAMP(0);
+  const MsgDesc& d = A.desc[blockIdx.y];
+  if (!(d.flags & kActive)) return;
+  SIG_STAMP(1);
+  const int f = A.f0 + blockIdx.y;
+  const int n = A.n;
+  const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
+  // One 32×32 tile per wave, tiles row-major over a tiles × tiles grid.
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (t >= tiles * tiles) return;
+  const int tr = t / tiles, tc = t - tr * tiles;
+  const int R0 = tr * 32, C0 = tc * 32;
+  sigma_tile(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
+             A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, n, A.ld, A.ldk, kw,
+             (d.flags & kFirst) != 0, A.q, R0, C0, lane);
+  SIG_STAMP(3);
 }
 
 // ---- association ------------------------------------------------------------------------------
@@ -890,12 +943,15 @@ hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s) {
   return hipGetLastError();
 }
 
+int g_sigma_waves = 4;  // waves per Σ-pass workgroup
+
 template <typename T>
 hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s) {
-  const int tiles = (a.n + 63) / 64;
-  const dim3 grid(tiles * tiles, nf);
+  const int tiles = (a.n + 31) / 32;
+  const int wpb = g_sigma_waves;
+  const dim3 grid((tiles * tiles + wpb - 1) / wpb, nf);
   (void)kw;
-  hipLaunchKernelGGL(k_sigma_pass<T>, grid, dim3(256), 0, s, a, tiles);
+  hipLaunchKernelGGL(k_sigma_pass<T>, grid, dim3(64 * wpb), 0, s, a, tiles);
   return hipGetLastError();
 }
 
