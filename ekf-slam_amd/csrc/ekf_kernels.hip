@@ -162,7 +162,7 @@ struct ChainShared {
   double alphaU[kMaxU];
   double row0raw[kMaxU];  // Σ_in[0][u_b]
   double col0raw[kMaxU];  // Σ_in[u_a][0]
-  double xU[2][kMaxU];    // ping-pong across steps
+  double xU[1][kMaxU];    // x[U], owned by wave 0 during the corrections
   double P[1][kMaxU][kMaxU + 1];    // Σ[U,U] (rows all, columns live)
   double Phi[1][kMaxU][kMaxU + 1];  // row map: r_c[U] = r_0[U]·Φ_c   (identity at c = 0)
   double Psi[1][kMaxU][kMaxU + 1];  // column map: c_c[U] = Ψ_c·c_0[U] (identity at c = 0)
@@ -172,13 +172,34 @@ struct ChainShared {
   double Y[kZC][kMaxU + 1];      // M_c[:, j] = Y[2c..2c+1, :] · c_0(j)[U]
   double Zx[kMaxU];              // Σ_c Z_c ν_c: x_i += r_0(i)[U] · Zx
   double nu[kMaxChunk][2];
+  double Hs[kMaxChunk][2][5];    // H_c over pA (published for waves 1–2)
+  double Sis[kMaxChunk][4];      // S_c⁻¹
   double LK[kMaxKW][kMaxU];      // kLook: previous chunk's Kcat / Mcat at U
   double LM[kMaxKW][kMaxU];
   double pose[3];
   double a1, a2, s00;
   int nu_cnt;
   unsigned status;
+  int pub;    // steps whose K, M, H, S⁻¹ wave 0 has published
+  int pdone;  // steps wave 3 has applied outside the cross
 };
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), l);
+  return __hiloint2double(hi, lo);
+}
+
+// Intra-workgroup hand-off through LDS (waves on different SIMDs; no s_barrier).
+__device__ __forceinline__ void lds_publish(int* flag, int v) {
+  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
+  while (__builtin_amdgcn_readfirstlane(
+             __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < v)
+    __builtin_amdgcn_s_sleep(1);
+}
 
 constexpr int kChainThreads = 256;
 
@@ -293,88 +314,100 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
   EKF_STAMP(2);
 
   // ---- A2: the m corrections -----------------------------------------------------------------
-  // Per step: S1 every wave recomputes ẑ, H, S⁻¹, ν (one wave per SIMD, no serial section); S2
-  // wave 0 forms K[U], Z_c, x[U], wave 1 M[:, live], wave 2 Y_c; S3 all threads apply the step's
-  // rank-2 term to P and Φ (live columns) and Ψ (live rows). "Live" = what later steps still read.
+  // The dependent chain (ẑ, H, S⁻¹, ν → K, M, x → next marker) runs on wave 0 alone, with no
+  // workgroup barrier. After step c it publishes K_c, M_c, H_c, S_c⁻¹ and applies the step's rank-2
+  // term only to the "cross" of the next marker (all rows × its 5 columns, its 5 rows × the later
+  // columns) — the entries step c+1 reads. The other waves follow through LDS flags:
+  //   wave 3  the rest of P (rows ∉ next, columns of markers ≥ c+2), one step behind wave 0;
+  //   wave 1  Z_c = Φ_c[:, pA]·Hᵀ·S⁻¹, then Φ −= Z_c·M_c (live columns);
+  //   wave 2  Y_c = H·Ψ_c[pA, :],      then Ψ −= K_c·Y_c (live rows).
+  // Φ, Ψ, Z, Y feed only the factor kernel, so waves 1–2 may lag the chain freely. "Live" = what
+  // later steps still read (pose and later markers).
   const int wave = tid >> 6, lane = tid & 63;
-  const int s3a = tid / 7, s3j = tid - 7 * (tid / 7);  // S3: 36 rows × 7 threads
-  for (int c = 0; c < m; ++c) {
-    const int pj = 3 + 2 * c;
-    EKF_STAMP(64 + 6 * c);
-    const int cur = c & 1, nxt = cur ^ 1;
-    const double* xc = sh.xU[cur];
-    const double z0 = d.z[c][0], z1 = d.z[c][1];
-    const double pose[3] = {xc[0], xc[1], xc[2]};
-    double lx = xc[pj], ly = xc[pj + 1];
-    bool sk = sh.skip[c] != 0;
-    bool init = false;
-    if (!sk && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
-      init = true;
-      lx = pose[1] + z0 * cos(z1 + pose[0]);
-      ly = pose[2] + z0 * sin(z1 + pose[0]);
-    }
-    const int pA[5] = {0, 1, 2, pj, pj + 1};
-    double H0[5], H1[5], Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
-    {
-      double zhat[2];
-      range_bearing(pose, lx, ly, zhat, H0, H1);
-      EKF_STAMP(65 + 6 * c);
-      double HP0[5], HP1[5];
+  if (tid == 0) {
+    sh.pub = 0;
+    sh.pdone = 0;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    for (int c = 0; c < m; ++c) {
+      const int pj = 3 + 2 * c;
+      EKF_STAMP(64 + 6 * c);
+      const double* xc = sh.xU[0];
+      const double z0 = d.z[c][0], z1 = d.z[c][1];
+      const double pose[3] = {xc[0], xc[1], xc[2]};
+      double lx = xc[pj], ly = xc[pj + 1];
+      bool sk = sh.skip[c] != 0;
+      bool init = false;
+      if (!sk && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
+        init = true;
+        lx = pose[1] + z0 * cos(z1 + pose[0]);
+        ly = pose[2] + z0 * sin(z1 + pose[0]);
+      }
+      const int pA[5] = {0, 1, 2, pj, pj + 1};
+      double H0[5], H1[5], Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
+      {
+        double zhat[2];
+        range_bearing(pose, lx, ly, zhat, H0, H1);
+        EKF_STAMP(65 + 6 * c);
+        double HP0[5], HP1[5];
 #pragma unroll
-      for (int bb = 0; bb < 5; ++bb) {
-        double s0 = 0.0, s1 = 0.0;
+        for (int bb = 0; bb < 5; ++bb) {
+          double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+          for (int a = 0; a < 5; ++a) {
+            const double v = sh.P[0][pA[a]][pA[bb]];
+            s0 += H0[a] * v;
+            s1 += H1[a] * v;
+          }
+          HP0[bb] = s0;
+          HP1[bb] = s1;
+        }
+        double Sm[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
-          const double v = sh.P[0][pA[a]][pA[bb]];
-          s0 += H0[a] * v;
-          s1 += H1[a] * v;
+          Sm[0] += HP0[a] * H0[a];
+          Sm[1] += HP0[a] * H1[a];
+          Sm[2] += HP1[a] * H0[a];
+          Sm[3] += HP1[a] * H1[a];
         }
-        HP0[bb] = s0;
-        HP1[bb] = s1;
+        Sm[0] += A.r;
+        Sm[3] += A.r;
+        if (!sk && inv2(Sm, Si)) {
+          nv0 = z0 - zhat[0];
+          nv1 = normalize_angle(z1 - zhat[1]);
+        } else {
+          if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every lane
+          sk = true;
+        }
       }
-      double Sm[4] = {0.0, 0.0, 0.0, 0.0};
+      if (sk) {
 #pragma unroll
-      for (int a = 0; a < 5; ++a) {
-        Sm[0] += HP0[a] * H0[a];
-        Sm[1] += HP0[a] * H1[a];
-        Sm[2] += HP1[a] * H0[a];
-        Sm[3] += HP1[a] * H1[a];
+        for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
+        Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
+        nv0 = nv1 = 0.0;
       }
-      Sm[0] += A.r;
-      Sm[3] += A.r;
-      if (!sk && inv2(Sm, Si)) {
-        nv0 = z0 - zhat[0];
-        nv1 = normalize_angle(z1 - zhat[1]);
-      } else {
-        if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every thread
-        sk = true;
-      }
-    }
-    if (sk) {
-#pragma unroll
-      for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
-      Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
-      nv0 = nv1 = 0.0;
-    }
-    const int jx = sh.u[pj];
-    EKF_STAMP(66 + 6 * c);
-    if (wave == 0 && lane < kMaxU) {  // K[U], Z_c = Φ[:, pA]·Hᵀ·S⁻¹, x[U]
-      double K0 = 0.0, K1 = 0.0, Z0 = 0.0, Z1 = 0.0;
-      if (lane < nu) {
-        double ka = 0.0, kb = 0.0, pa = 0.0, pb = 0.0;
+      const int jx = sh.u[pj];
+      EKF_STAMP(66 + 6 * c);
+      double K0 = 0.0, K1 = 0.0, mm0 = 0.0, mm1 = 0.0;  // row / column `lane` of this step
+      if (lane < nu) {  // K[U] = Σ[U, pA]·Hᵀ·S⁻¹, M[:, live] = H·Σ[pA, live], x[U]
+        double ka = 0.0, kb = 0.0;
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
           const double v = sh.P[0][lane][pA[a]];
-          const double w = sh.Phi[0][lane][pA[a]];
           ka += v * H0[a];
           kb += v * H1[a];
-          pa += w * H0[a];
-          pb += w * H1[a];
         }
         K0 = ka * Si[0] + kb * Si[2];
         K1 = ka * Si[1] + kb * Si[3];
-        Z0 = pa * Si[0] + pb * Si[2];
-        Z1 = pa * Si[1] + pb * Si[3];
+        if (lane < 3 || lane >= pj + 2) {
+#pragma unroll
+          for (int a = 0; a < 5; ++a) {
+            const double v = sh.P[0][pA[a]][lane];
+            mm0 += H0[a] * v;
+            mm1 += H1[a] * v;
+          }
+        }
         double xt = xc[lane];
         if (init) {
           if (sh.u[lane] == jx) xt = lx;
@@ -382,68 +415,177 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
         }
         xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
         if (lane == 0) xt = normalize_angle(xt);     // slam.cpp:267
-        sh.xU[nxt][lane] = xt;
+        sh.xU[0][lane] = xt;
       }
-      sh.KU[c][lane][0] = K0;
-      sh.KU[c][lane][1] = K1;
-      sh.Z[lane][2 * c] = Z0;
-      sh.Z[lane][2 * c + 1] = Z1;
+      if (lane < kMaxU) {
+        sh.KU[c][lane][0] = K0;
+        sh.KU[c][lane][1] = K1;
+        sh.MU[c][lane][0] = mm0;
+        sh.MU[c][lane][1] = mm1;
+      }
       if (lane == 0) {
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          sh.Hs[c][0][a] = H0[a];
+          sh.Hs[c][1][a] = H1[a];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sh.Sis[c][k] = Si[k];
         sh.nu[c][0] = nv0;
         sh.nu[c][1] = nv1;
       }
-    } else if (wave == 1 && lane < kMaxU) {  // M[:, live]
-      const int b = lane;
-      double mm0 = 0.0, mm1 = 0.0;
-      if (b < nu && (b < 3 || b >= pj + 2)) {
+      lds_publish(&sh.pub, c + 1);
+      EKF_STAMP(67 + 6 * c);
+      if (c + 1 < m) {
+        const int nx = pj + 2;  // next marker's columns; Bx = {0, 1, 2, nx, nx+1}
+        // K and M of the five Bx rows / columns, broadcast from their lanes
+        double kx0[5], kx1[5], mx0[5], mx1[5];
 #pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          const double v = sh.P[0][pA[a]][b];
-          mm0 += H0[a] * v;
-          mm1 += H1[a] * v;
+        for (int k = 0; k < 5; ++k) {
+          const int l = k < 3 ? k : nx + k - 3;
+          kx0[k] = readlane_f64(K0, l);
+          kx1[k] = readlane_f64(K1, l);
+          mx0[k] = readlane_f64(mm0, l);
+          mx1[k] = readlane_f64(mm1, l);
+        }
+        lds_wait_ge(&sh.pdone, c);  // wave 3 has applied step c−1 outside this step's cross
+        EKF_STAMP(68 + 6 * c);
+        if (lane < nu) {  // all rows × Bx columns
+#pragma unroll
+          for (int k = 0; k < 5; ++k) {
+            const int b = k < 3 ? k : nx + k - 3;
+            sh.P[0][lane][b] = rank2_sub(sh.P[0][lane][b], K0, K1, mx0[k], mx1[k]);
+          }
+        }
+        if (lane >= nx + 2 && lane < nu) {  // Bx rows × columns of markers ≥ c+2
+#pragma unroll
+          for (int k = 0; k < 5; ++k) {
+            const int a = k < 3 ? k : nx + k - 3;
+            sh.P[0][a][lane] = rank2_sub(sh.P[0][a][lane], kx0[k], kx1[k], mm0, mm1);
+          }
         }
       }
-      sh.MU[c][b][0] = mm0;
-      sh.MU[c][b][1] = mm1;
-    } else if (wave == 2 && lane < kMaxU) {  // Y_c = H·Ψ[pA, :]
-      const int b = lane;
-      double y0 = 0.0, y1 = 0.0;
-      if (b < nu) {
-#pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          const double v = sh.Psi[0][pA[a]][b];
-          y0 += H0[a] * v;
-          y1 += H1[a] * v;
-        }
-      }
-      sh.Y[2 * c][b] = y0;
-      sh.Y[2 * c + 1][b] = y1;
+      EKF_STAMP(69 + 6 * c);
     }
-    EKF_STAMP(67 + 6 * c);
-    __syncthreads();
-    EKF_STAMP(68 + 6 * c);
-    const int live = 3 + (nu - pj - 2);
-    if (s3a < nu) {
-      const double ka0 = sh.KU[c][s3a][0], ka1 = sh.KU[c][s3a][1];
-      const double za0 = sh.Z[s3a][2 * c], za1 = sh.Z[s3a][2 * c + 1];
-      const double ya0 = sh.Y[2 * c][s3a], ya1 = sh.Y[2 * c + 1][s3a];
+  } else if (wave == 3) {  // P outside the cross: rows ∉ next marker, columns of markers ≥ c+2
+    // lane → column nx+2+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
+    const int hb = lane & 31, hr = lane >> 5;
+    for (int c = 0; c + 1 < m; ++c) {
+      lds_wait_ge(&sh.pub, c + 1);
+      const int nx = 5 + 2 * c;
+      const int b = nx + 2 + hb;
+      if (b < nu) {
+        const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
+        double pv[16], k0[16], k1[16];
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const int bi = s3j + 7 * k;
-        if (bi < live) {
+        for (int i = 0; i < 16; ++i) {
+          const int a = 3 + hr + 2 * i;
+          if (a < nu) {
+            pv[i] = sh.P[0][a][b];
+            k0[i] = sh.KU[c][a][0];
+            k1[i] = sh.KU[c][a][1];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int a = 3 + hr + 2 * i;
+          if (a < nu && a != nx && a != nx + 1)
+            sh.P[0][a][b] = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
+        }
+      }
+      lds_publish(&sh.pdone, c + 1);
+    }
+  } else if (wave == 1) {  // Z_c and Φ (live columns)
+    const int hb = lane & 31, hr = lane >> 5;
+    for (int c = 0; c < m; ++c) {
+      lds_wait_ge(&sh.pub, c + 1);
+      const int pj = 3 + 2 * c;
+      const int pA[5] = {0, 1, 2, pj, pj + 1};
+      if (lane < kMaxU) {
+        double Z0 = 0.0, Z1 = 0.0;
+        if (lane < nu) {
+          double pa = 0.0, pb = 0.0;
+#pragma unroll
+          for (int a = 0; a < 5; ++a) {
+            const double w = sh.Phi[0][lane][pA[a]];
+            pa += w * sh.Hs[c][0][a];
+            pb += w * sh.Hs[c][1][a];
+          }
+          Z0 = pa * sh.Sis[c][0] + pb * sh.Sis[c][2];
+          Z1 = pa * sh.Sis[c][1] + pb * sh.Sis[c][3];
+        }
+        sh.Z[lane][2 * c] = Z0;
+        sh.Z[lane][2 * c + 1] = Z1;
+      }
+      if (c + 1 < m) {
+        const int live = 3 + (nu - pj - 2);
+        for (int bi = hb; bi < live; bi += 32) {  // Φ[a][b] −= Z_c[a]·M_c[b], all rows a
           const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
           const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
-          const double kb0 = sh.KU[c][b][0], kb1 = sh.KU[c][b][1];
-          sh.P[0][s3a][b] = rank2_sub(sh.P[0][s3a][b], ka0, ka1, mb0, mb1);
-          sh.Phi[0][s3a][b] = rank2_sub(sh.Phi[0][s3a][b], za0, za1, mb0, mb1);
-          sh.Psi[0][b][s3a] = rank2_sub(sh.Psi[0][b][s3a], kb0, kb1, ya0, ya1);
+          double pv[18], z0[18], z1[18];
+#pragma unroll
+          for (int i = 0; i < 18; ++i) {
+            const int a = hr + 2 * i;
+            if (a < nu) {
+              pv[i] = sh.Phi[0][a][b];
+              z0[i] = sh.Z[a][2 * c];
+              z1[i] = sh.Z[a][2 * c + 1];
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 18; ++i) {
+            const int a = hr + 2 * i;
+            if (a < nu) sh.Phi[0][a][b] = rank2_sub(pv[i], z0[i], z1[i], mb0, mb1);
+          }
         }
       }
     }
-    EKF_STAMP(69 + 6 * c);
-    __syncthreads();
+  } else {  // wave 2: Y_c and Ψ (live rows)
+    const int ha = lane & 31, hr = lane >> 5;
+    for (int c = 0; c < m; ++c) {
+      lds_wait_ge(&sh.pub, c + 1);
+      const int pj = 3 + 2 * c;
+      const int pA[5] = {0, 1, 2, pj, pj + 1};
+      if (lane < kMaxU) {
+        double y0 = 0.0, y1 = 0.0;
+        if (lane < nu) {
+#pragma unroll
+          for (int a = 0; a < 5; ++a) {
+            const double v = sh.Psi[0][pA[a]][lane];
+            y0 += sh.Hs[c][0][a] * v;
+            y1 += sh.Hs[c][1][a] * v;
+          }
+        }
+        sh.Y[2 * c][lane] = y0;
+        sh.Y[2 * c + 1][lane] = y1;
+      }
+      if (c + 1 < m) {
+        const int live = 3 + (nu - pj - 2);
+        for (int a = ha; a < nu; a += 32) {  // Ψ[b][a] −= K_c[b]·Y_c[a], live rows b
+          const double ya0 = sh.Y[2 * c][a], ya1 = sh.Y[2 * c + 1][a];
+          double pv[17], k0[17], k1[17];
+#pragma unroll
+          for (int i = 0; i < 17; ++i) {
+            const int bi = hr + 2 * i;
+            const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
+            if (bi < live) {
+              pv[i] = sh.Psi[0][b][a];
+              k0[i] = sh.KU[c][b][0];
+              k1[i] = sh.KU[c][b][1];
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 17; ++i) {
+            const int bi = hr + 2 * i;
+            const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
+            if (bi < live) sh.Psi[0][b][a] = rank2_sub(pv[i], k0[i], k1[i], ya0, ya1);
+          }
+        }
+      }
+    }
   }
-  const double* xfin = sh.xU[m & 1];
+  __syncthreads();
+  const double* xfin = sh.xU[0];
   if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
     double zx = 0.0;
     for (int c = 0; c < m; ++c) zx += sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];

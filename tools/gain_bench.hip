@@ -79,16 +79,17 @@ void run(int N, int m, int reps) {
   printf("N=%d m=%d %s: chain %.2f us/launch | A0 %llu A1 %llu endA %llu | per step (avg cycles):",
          N, m, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, st[1] - st[0], st[2] - st[0],
          st[40] - st[0]);
-  const char* nm[6] = {"rb", "S+inv", "S2", "bar1", "S3", "bar2"};
+  const char* nm[6] = {"rb", "S+inv", "KMx+pub", "wait", "cross", "loop"};
   const int pts[7] = {64, 65, 66, 67, 68, 69, 70};
   for (int p = 0; p < 6; ++p) {
     double acc = 0;
-    for (int c = 0; c < m; ++c) {
+    const int steps = m > 1 ? m - 1 : 1;  // stamps 68/69 exist only when a next step follows
+    for (int c = 0; c < steps; ++c) {
       const unsigned long long a0 = st[pts[p] + 6 * c];
       const unsigned long long a1 = p < 5 ? st[pts[p + 1] + 6 * c] : (c + 1 < m ? st[64 + 6 * (c + 1)] : st[40]);
       acc += static_cast<double>(a1 - a0);
     }
-    printf(" %s %.0f", nm[p], acc / m);
+    printf(" %s %.0f", nm[p], acc / (m > 1 ? m - 1 : 1));
   }
   printf("\n");
   CK(hipEventRecord(e0, s));
