@@ -44,10 +44,60 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--workload", default="n1024_fp32", choices=sorted(WORKLOADS))
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    p.add_argument("--cpu-messages", type=int, default=1,
+    p.add_argument("--cpu-messages", type=int, default=3,
                    help="messages in the CPU baseline sample (literal dense)")
     p.add_argument("--parity-messages", type=int, default=10)
+    p.add_argument("--traffic", choices=["auto", "off"], default="auto",
+                   help="auto: measure the Σ pass's HBM bytes with two rocprofv3 --pmc child runs")
     return p.parse_args()
+
+
+def pmc_traffic(args):
+    """HBM-side bytes per k_sigma_pass launch from PMC counters (MI355X_MICROARCH.md, HBM):
+    FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes (they do not fit one pass), FETCH_SIZE
+    doubled on gfx950. Runs short child benches before this process touches the GPU; any failure
+    gives None with the reason (a measurement gap, never a different compute path)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, "rocprofv3 not found"
+    vals = {}
+    # the workload's own instantiation (the fp32 workload's fp64 warm-up lap is excluded)
+    kname = "k_sigma_pass<float>" if WORKLOADS[args.workload][1] == "f32" else "k_sigma_pass<double>"
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="ekf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = [exe, "--pmc", counter, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--workload", args.workload,
+               "--steps", "8", "--warmup", "2", "--no-cpu", "--traffic", "off"]
+        env = dict(os.environ, EKF_SERIAL="1")  # one stream: counters belong to one dispatch
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+        except subprocess.TimeoutExpired:
+            return None, f"rocprofv3 --pmc {counter} timed out"
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode})"
+        per = []
+        with open(files[0]) as fh:
+            for row in csv.DictReader(fh):
+                if kname in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    per.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not per:
+            return None, f"no k_sigma_pass dispatches with {counter}"
+        vals[counter] = float(np.mean(per))
+    # counters are in KB (rocprofv3 derived FETCH_SIZE / WRITE_SIZE)
+    fetch = 2.0 * vals["FETCH_SIZE"] * 1024.0
+    write = vals["WRITE_SIZE"] * 1024.0
+    return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "note": "FETCH_SIZE x2 (gfx950 correction, calibrated for this kernel's loads in "
+                    "profiles/r1/pmc_calibration.md) + WRITE_SIZE; separate --pmc passes over a "
+                    "short child run with every kernel on one stream (EKF_SERIAL=1); mean over "
+                    "k_sigma_pass dispatches"}, None
 
 
 def build_inputs(N, F, msgs, seed, m):
@@ -80,6 +130,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic, traffic_err = None, "not measured (--traffic off or N>1)"
+    if args.traffic == "auto" and world == 1:
+        traffic, traffic_err = pmc_traffic(args)
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -132,17 +185,9 @@ def main():
     elapsed = time.perf_counter() - t0
     corrections = int(np.count_nonzero((act[ts] == 0) & (np.arange(act.shape[2]) <
                                                           counts[ts][..., None])))
+    poses = np.stack([ekf.pose(f) for f in range(F)])
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([corrections], dtype=torch.float64, device="cuda")
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        total_corr = float(c.item())
-        # the one collective of the path: gather every filter's final pose to rank 0 (RCCL)
-        poses = torch.tensor(np.stack([ekf.pose(f) for f in range(F)]), device="cuda")
-        gathered = [torch.zeros_like(poses) for _ in range(world)]
-        dist.all_gather(gathered, poses)
+        elapsed, total_corr, _ = reduce_ranks(elapsed, corrections, poses, "cuda")
     else:
         total_corr = float(corrections)
 
@@ -183,7 +228,8 @@ def main():
             "roofline": {
                 "kernel": "k_sigma_pass", "bound": "hbm", "achieved": achieved,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": traffic["bytes_per_launch"] if traffic else None,
+                "traffic_detail": traffic if traffic else traffic_err,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "bytes_formula": f"2*n^2*w*F = 2*{n}^2*{wsz}*{F}",
                 "avg_launch_us": avg_sig_s * 1e6, "launches": n_sig,
@@ -204,6 +250,22 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def reduce_ranks(elapsed, corrections, poses, device):
+    """Whole-job numbers across ranks: the slowest rank's time (MAX), the corrections of all ranks
+    (SUM), and every filter's final pose gathered to all ranks — the path's one collective (RCCL on
+    the GPU box; gloo in tests/test_multirank.py)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([float(corrections)], dtype=torch.float64, device=device)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    p = torch.tensor(poses, dtype=torch.float64, device=device)
+    gathered = [torch.zeros_like(p) for _ in range(dist.get_world_size())]
+    dist.all_gather(gathered, p)
+    return float(t.item()), float(c.item()), np.concatenate([g.cpu().numpy() for g in gathered])
 
 
 def ekf_first_poses(args, N, dtype, ws, counts, ids, act, rel, odom, t0s, device):
@@ -234,7 +296,7 @@ def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
     x, S, tmo, cnt = ws
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     out = {}
-    for literal, k in ((True, args.cpu_messages), (False, 5)):
+    for literal, k in ((True, args.cpu_messages), (False, args.steps)):
         ref = orc.OracleEKF(n_landmarks=N, literal=literal)
         ref.set(x, S, tmo, x[:3], cnt)
         ncorr = 0

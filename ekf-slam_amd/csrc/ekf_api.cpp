@@ -51,6 +51,7 @@ struct ekf_ctx {
   size_t w = 8;
   hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
+  bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
   hipEvent_t ev_fac = nullptr, ev_sig = nullptr;
   void* sig[2] = {nullptr, nullptr};
   double* x[2] = {nullptr, nullptr};
@@ -131,15 +132,14 @@ hipEvent_t pool_get(ekf_ctx* h) {
 // 3 = factors).
 template <typename Fn>
 int timed(ekf_ctx* h, int kind, hipStream_t st, Fn fn) {
+  (void)st;
   hipEvent_t a = nullptr, b = nullptr;
   if (h->prof) {
     a = pool_get(h);
     b = pool_get(h);
-    if (a) hipEventRecord(a, st);
   }
-  const hipError_t e = fn();
+  const hipError_t e = fn(a && b ? a : nullptr, a && b ? b : nullptr);
   if (h->prof && a && b) {
-    hipEventRecord(b, st);
     h->pe[kind].start.push_back(a);
     h->pe[kind].stop.push_back(b);
   }
@@ -167,17 +167,19 @@ inline void measure(double rx, double ry, double* zr, double* zb) {
 template <typename T>
 int launch_pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pipelined) {
   const PassArgs<T> a = args<T>(h, dptr, f0);
-  hipStream_t ms = h->stream, bs = pipelined ? h->bulk : h->stream;
-  int rc = timed(h, 1, ms, [&] { return launch_chain<T>(a, nf, ms); });
+  hipStream_t ms = h->stream, bs = pipelined && !h->serial ? h->bulk : h->stream;
+  int rc = timed(h, 1, ms, [&](hipEvent_t e0, hipEvent_t e1) { return launch_chain<T>(a, nf, ms, e0, e1); });
   if (rc) return rc;
   HIPCHK(hipStreamWaitEvent(ms, h->ev_sig, 0));  // factors gather Σ_in = previous Σ pass output
-  rc = timed(h, 3, ms, [&] { return launch_factors<T>(a, nf, ms); });
+  rc = timed(h, 3, ms, [&](hipEvent_t e0, hipEvent_t e1) { return launch_factors<T>(a, nf, ms, e0, e1); });
   if (rc) return rc;
   if (pipelined) {
     HIPCHK(hipEventRecord(h->ev_fac, ms));
     HIPCHK(hipStreamWaitEvent(bs, h->ev_fac, 0));
   }
-  rc = timed(h, 0, bs, [&] { return launch_sigma_pass<T>(a, nf, kw, bs); });
+  rc = timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
+    return launch_sigma_pass<T>(a, nf, kw, bs, e0, e1);
+  });
   if (rc) return rc;
   HIPCHK(hipEventRecord(h->ev_sig, bs));
   return EKF_OK;
@@ -230,10 +232,14 @@ int drain(ekf_ctx* h) {
 int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
   if (h->cfg.dtype == EKF_F32) {
     const PassArgs<float> a = args<float>(h, dptr, f0);
-    return timed(h, 2, h->stream, [&] { return launch_assoc<float>(a, nf, h->stream); });
+    return timed(h, 2, h->stream, [&](hipEvent_t e0, hipEvent_t e1) {
+      return launch_assoc<float>(a, nf, h->stream, e0, e1);
+    });
   }
   const PassArgs<double> a = args<double>(h, dptr, f0);
-  return timed(h, 2, h->stream, [&] { return launch_assoc<double>(a, nf, h->stream); });
+  return timed(h, 2, h->stream, [&](hipEvent_t e0, hipEvent_t e1) {
+    return launch_assoc<double>(a, nf, h->stream, e0, e1);
+  });
 }
 
 // Known association, one message per filter in [f0, f0+nf): msgs[k] holds filter f0+k's markers.
@@ -495,6 +501,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     return rc;
   };
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
+  if (const char* e = std::getenv("EKF_SERIAL")) h->serial = std::atoi(e) != 0;
   if (create_streams(h) != EKF_OK ||
       hipEventCreateWithFlags(&h->ev_fac, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_sig, hipEventDisableTiming) != hipSuccess)

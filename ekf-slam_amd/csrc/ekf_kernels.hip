@@ -17,6 +17,7 @@
 //
 // Equal to the reference's sequential dense algebra in exact arithmetic; the summation order
 // differs (tolerances in tests/). Unknown association adds k_assoc before each single-marker pair.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -1071,35 +1072,48 @@ __global__ void k_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
 }
 
 // ---- launchers ------------------------------------------------------------------------------
+// With events, the launch carries them in its dispatch (hipExtLaunchKernelGGL): they time the
+// kernel's own execution, not the queueing / dispatch latency around it.
+template <typename K, typename... Args>
+void launch(K kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+            Args... args) {
+  if (e0 && e1)
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+}
+
 template <typename T>
-hipError_t launch_chain(const PassArgs<T>& a, int nf, hipStream_t s) {
-  hipLaunchKernelGGL(k_chain<T>, dim3(1, nf), dim3(kChainThreads), 0, s, a);
+hipError_t launch_chain(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a);
   return hipGetLastError();
 }
 
 template <typename T>
-hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s) {
+hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0,
+                          hipEvent_t e1) {
   const int waves = 2 * ((a.n + 15) / 16);  // 16 rows or 16 columns per wave
   const dim3 grid((waves + 3) / 4, nf);
-  hipLaunchKernelGGL(k_factors<T>, grid, dim3(256), 0, s, a);
+  launch(k_factors<T>, grid, dim3(256), s, e0, e1, a);
   return hipGetLastError();
 }
 
 int g_sigma_waves = 4;  // waves per Σ-pass workgroup
 
 template <typename T>
-hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s) {
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s, hipEvent_t e0,
+                             hipEvent_t e1) {
   const int tiles = (a.n + 31) / 32;
   const int wpb = g_sigma_waves;
   const dim3 grid((tiles * tiles + wpb - 1) / wpb, nf);
   (void)kw;
-  hipLaunchKernelGGL(k_sigma_pass<T>, grid, dim3(64 * wpb), 0, s, a, tiles);
+  launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles);
   return hipGetLastError();
 }
 
 template <typename T>
-hipError_t launch_assoc(const PassArgs<T>& a, int nf, hipStream_t s) {
-  hipLaunchKernelGGL(k_assoc<T>, dim3(1, nf), dim3(256), 0, s, a);
+hipError_t launch_assoc(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  launch(k_assoc<T>, dim3(1, nf), dim3(256), s, e0, e1, a);
   return hipGetLastError();
 }
 
@@ -1117,10 +1131,12 @@ hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
 }
 
 #define EKF_INSTANTIATE(T)                                                              \
-  template hipError_t launch_chain<T>(const PassArgs<T>&, int, hipStream_t);            \
-  template hipError_t launch_factors<T>(const PassArgs<T>&, int, hipStream_t);          \
-  template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, int, hipStream_t);  \
-  template hipError_t launch_assoc<T>(const PassArgs<T>&, int, hipStream_t);            \
+  template hipError_t launch_chain<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t, hipEvent_t); \
+  template hipError_t launch_factors<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t,          \
+                                        hipEvent_t);                                               \
+  template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, int, hipStream_t, hipEvent_t,  \
+                                           hipEvent_t);                                            \
+  template hipError_t launch_assoc<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t, hipEvent_t); \
   template hipError_t launch_posterior<T>(const PassArgs<T>&, int, hipStream_t);              \
   template hipError_t launch_init_diag<T>(T*, size_t, int, int, double, int, hipStream_t);
 EKF_INSTANTIATE(double)

@@ -1,4 +1,5 @@
 // Kernel launchers (defined in ekf_kernels.hip, called by the host runtime in ekf_api.cpp).
+// Optional e0/e1: timing events carried by the dispatch itself (kernel execution time).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -30,19 +31,23 @@ struct PassArgs {
 // Chain kernel: the chunk's sequential corrections on the |U|×|U| block (predict folded in),
 // one workgroup per filter → ChunkRec.
 template <typename T>
-hipError_t launch_chain(const PassArgs<T>& a, int n_filters, hipStream_t s);
+hipError_t launch_chain(const PassArgs<T>& a, int n_filters, hipStream_t s,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // Factor kernel: Kcat = R·Z, Mcat = Y·C on f64 MFMA and the new state. 16 rows / columns per wave.
 template <typename T>
-hipError_t launch_factors(const PassArgs<T>& a, int n_filters, hipStream_t s);
+hipError_t launch_factors(const PassArgs<T>& a, int n_filters, hipStream_t s,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, 64×64 tiles. kw = padded rank for this launch.
 template <typename T>
-hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, int kw, hipStream_t s);
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, int kw, hipStream_t s,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // Mahalanobis nearest-neighbour association for one marker per filter (one workgroup each).
 template <typename T>
-hipError_t launch_assoc(const PassArgs<T>& a, int n_filters, hipStream_t s);
+hipError_t launch_assoc(const PassArgs<T>& a, int n_filters, hipStream_t s,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // Posterior t_map_odom for filters with no pending Σ pass.
 template <typename T>

@@ -119,8 +119,9 @@ int ekf_get_status(ekf_t h, int filter, unsigned* flags); /* and clears them */
 double ekf_normalize_angle(double rad);
 
 /* ---- measurement ---- */
-/* Per-kernel device time with HIP events on the handle's stream (0 = Σ pass, 1 = chain,
- * 2 = association, 3 = factors). Adds two event records per timed launch; off by default. */
+/* Per-kernel device time (0 = Σ pass, 1 = chain, 2 = association, 3 = factors) from HIP events
+ * carried by each timed dispatch (hipExtLaunchKernelGGL start/stop events: the kernel's own
+ * execution, on the stream it runs on). Off by default. */
 int ekf_profile_enable(ekf_t h, int enable);
 int ekf_profile_read(ekf_t h, int kernel, long long* launches, double* total_ms);
 /* Bytes the Σ pass must move per launch for the current handle (2·n²·w·F). */

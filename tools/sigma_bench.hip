@@ -9,6 +9,7 @@
 #include <algorithm>
 
 using namespace ekfslam;
+static int g_pingpong = 0;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 
 template <typename V>
@@ -34,9 +35,11 @@ void run(int N, int F, int reps) {
   CK(hipMemcpy(mc, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
   std::vector<MsgDesc> d(F);
   for (int f = 0; f < F; ++f) { std::memset(&d[f], 0, sizeof(MsgDesc)); d[f].m = 16; d[f].flags = kActive | kFirst; }
-  MsgDesc* dd;
-  CK(hipMalloc(&dd, F * sizeof(MsgDesc)));
+  MsgDesc* dd;  // [2][F]: parity 0 and parity 1 descriptors (ping-pong like the product)
+  CK(hipMalloc(&dd, 2 * F * sizeof(MsgDesc)));
   CK(hipMemcpy(dd, d.data(), F * sizeof(MsgDesc), hipMemcpyHostToDevice));
+  for (int f = 0; f < F; ++f) d[f].parity = 1;
+  CK(hipMemcpy(dd + F, d.data(), F * sizeof(MsgDesc), hipMemcpyHostToDevice));
   FilterCtl* ctl;
   CK(hipMalloc(&ctl, F * sizeof(FilterCtl)));
   PassArgs<T> a{};
@@ -63,7 +66,11 @@ void run(int N, int F, int reps) {
   printf("N=%d F=%d %s: copy %.2f us (%.0f GB/s)", N, F, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, cbytes / (ms / reps * 1e-3) / 1e9);
   for (int i = 0; i < 3; ++i) CK(launch_sigma_pass<T>(a, F, 36, s));
   CK(hipEventRecord(e0, s));
-  for (int i = 0; i < reps; ++i) CK(launch_sigma_pass<T>(a, F, 36, s));
+  for (int i = 0; i < reps; ++i) {
+    if (g_pingpong) a.desc = dd + (i & 1) * F;
+    CK(launch_sigma_pass<T>(a, F, 36, s));
+  }
+  a.desc = dd;
   CK(hipEventRecord(e1, s));
   CK(hipEventSynchronize(e1));
   CK(hipEventElapsedTime(&ms, e0, e1));
@@ -103,6 +110,7 @@ void run(int N, int F, int reps) {
 
 int main(int argc, char** argv) {
   if (argc > 1) g_sigma_waves = atoi(argv[1]);
+  if (argc > 2) g_pingpong = atoi(argv[2]);
   printf("waves/WG %d\n", g_sigma_waves);
   run<float>(1024, 1, 200);
   run<double>(1024, 1, 200);
