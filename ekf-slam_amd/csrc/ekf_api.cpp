@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -52,7 +53,12 @@ struct ekf_ctx {
   hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
-  hipEvent_t ev_fac = nullptr, ev_sig = nullptr;
+  hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
+  hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
+  bool devsync = false;                   // streams synchronise through device epochs
+  unsigned* sync = nullptr;               // device epochs: Σ pass done, its ticket, chains done
+  hipEvent_t ev_sig[2] = {nullptr, nullptr};  // bulk → main: Σ pass of launch s, by s & 1
+  long long seq = 0;                      // launch pairs issued
   void* sig[2] = {nullptr, nullptr};
   double* x[2] = {nullptr, nullptr};
   void* kcat = nullptr;
@@ -65,8 +71,8 @@ struct ekf_ctx {
   std::vector<Pose2> odom;
   std::vector<int> parity;
   std::vector<char> pending;
-  std::vector<int> prev_m;       // ≥ 0: last chunk was pipelined (its factors are in Kcat/Mcat)
-  std::vector<char> prev_first;
+  std::vector<int> prev_m;       // ≥ 0: last chunk was a pipelined pair (its record is valid)
+  std::vector<std::array<int, kMaxChunk>> prev_ids;  // that chunk's landmark ids
   // launch plan: descriptors for a whole call (or a whole replay) uploaded with ONE copy
   std::vector<MsgDesc> plan_d;
   std::vector<Launch> plan_l;
@@ -106,6 +112,8 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.ldk = h->ldk;
   a.ctl = h->ctl;
   a.rec = h->rec;
+  a.rec_stride = static_cast<size_t>(h->F);
+  a.sync = h->sync;
   a.desc = desc;
   a.n = h->n;
   a.ld = h->ld;
@@ -162,26 +170,54 @@ inline void measure(double rx, double ry, double* zr, double* zb) {
   *zb = std::atan2(ry, rx);
 }
 
-// chain → (Σ_in ready) → factors on the main stream; the Σ pass on the bulk stream once the
-// factors exist, so it overlaps the next chunk's chain. pipelined = false keeps all on main.
+// Main waits for everything issued to the bulk stream so far.
+int join_bulk(ekf_ctx* h) {
+  if (hipEventRecord(h->ev_join, h->bulk) != hipSuccess ||
+      hipStreamWaitEvent(h->stream, h->ev_join, 0) != hipSuccess)
+    return EKF_E_HIP;
+  return EKF_OK;
+}
+
+// The main stream runs the chains back to back; the bulk stream runs each chunk's factors and Σ
+// pass. With disjoint CU masks (devsync) the two streams synchronise on the device only: a chain
+// polls the Σ-pass epoch (it needs the pass two launches back: Σ_in and x of the chunk before the
+// previous one, and this parity's ChunkRec free again), the factor kernel polls its filter's chain
+// epoch. A hipStreamWaitEvent hop between the queues costs 6–12 µs, a device poll ≈ 1–2 µs.
+// Without the CU split a spinning factor grid could hold every CU the chain needs, so events are
+// used instead (the kernels' polls are then satisfied on arrival).
 template <typename T>
 int launch_pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pipelined) {
-  const PassArgs<T> a = args<T>(h, dptr, f0);
-  hipStream_t ms = h->stream, bs = pipelined && !h->serial ? h->bulk : h->stream;
-  int rc = timed(h, 1, ms, [&](hipEvent_t e0, hipEvent_t e1) { return launch_chain<T>(a, nf, ms, e0, e1); });
-  if (rc) return rc;
-  HIPCHK(hipStreamWaitEvent(ms, h->ev_sig, 0));  // factors gather Σ_in = previous Σ pass output
-  rc = timed(h, 3, ms, [&](hipEvent_t e0, hipEvent_t e1) { return launch_factors<T>(a, nf, ms, e0, e1); });
-  if (rc) return rc;
+  PassArgs<T> a = args<T>(h, dptr, f0);
+  const unsigned s = static_cast<unsigned>(h->seq);
+  a.seq = s;
+  const bool two = pipelined && !h->serial;
+  hipStream_t ms = h->stream, bs = two ? h->bulk : h->stream;
   if (pipelined) {
-    HIPCHK(hipEventRecord(h->ev_fac, ms));
-    HIPCHK(hipStreamWaitEvent(bs, h->ev_fac, 0));
+    a.need_sigma = s >= 2 ? s - 1 : 0;  // epoch of the Σ pass two launches back
+    if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s & 1], 0));
+  } else {
+    a.need_sigma = 0;
+    if (join_bulk(h)) return EKF_E_HIP;
   }
+  int rc = timed(h, 1, ms, [&](hipEvent_t e0, hipEvent_t e1) {
+    return launch_chain<T>(a, nf, ms, e0, e1);
+  });
+  if (rc) return rc;
+  if (two && !h->devsync) {
+    HIPCHK(hipEventRecord(h->ev_chain, ms));
+    HIPCHK(hipStreamWaitEvent(bs, h->ev_chain, 0));
+  }
+  // factors gather the materialised Σ_in (the previous Σ pass, same stream) and the chain's record
+  rc = timed(h, 3, bs, [&](hipEvent_t e0, hipEvent_t e1) {
+    return launch_factors<T>(a, nf, bs, e0, e1);
+  });
+  if (rc) return rc;
   rc = timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
     return launch_sigma_pass<T>(a, nf, kw, bs, e0, e1);
   });
   if (rc) return rc;
-  HIPCHK(hipEventRecord(h->ev_sig, bs));
+  if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[s & 1], bs));
+  ++h->seq;
   return EKF_OK;
 }
 
@@ -211,8 +247,11 @@ int create_streams(ekf_ctx* h) {
     std::vector<uint32_t> mmain(words, 0), mbulk(words, 0);
     for (int b = 0; b < cus; ++b) (b < split * kXcd ? mmain : mbulk)[b / 32] |= 1u << (b % 32);
     if (hipExtStreamCreateWithCUMask(&h->stream, words, mmain.data()) == hipSuccess &&
-        hipExtStreamCreateWithCUMask(&h->bulk, words, mbulk.data()) == hipSuccess)
+        hipExtStreamCreateWithCUMask(&h->bulk, words, mbulk.data()) == hipSuccess) {
+      const char* e = std::getenv("EKF_DEVSYNC");
+      h->devsync = !(e && std::atoi(e) == 0);
       return EKF_OK;
+    }
     if (h->stream) hipStreamDestroy(h->stream);
     h->stream = nullptr;
   }
@@ -266,18 +305,16 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
       int flags = kActive;
       if (chunk == 0 && (predict || h->pending[f])) flags |= kFirst;
       if (chunk == nchunks - 1 && predict) flags |= kLast;
-      if (h->prev_m[f] >= 0) {  // rebuild Σ_in from the previous chunk (its Σ pass may be running)
-        flags |= kLook;
-        if (h->prev_first[f]) flags |= kPrevFirst;
-      }
+      if (h->prev_m[f] >= 0) flags |= kLook;  // rebuild from the chunk before (its Σ pass may run)
       fill_desc(d, m, flags, h->parity[f], h->odom[f]);
       d->prev_m = h->prev_m[f];
+      for (int i = 0; i < kMaxChunk; ++i) d->prev_ids[i] = h->prev_ids[f][i];
       h->prev_m[f] = m;
-      h->prev_first[f] = (flags & kFirst) ? 1 : 0;
       for (int i = 0; i < m; ++i) {
         d->ids[i] = mk[b + i].id;
         d->z[i][0] = mk[b + i].zr;
         d->z[i][1] = mk[b + i].zb;
+        h->prev_ids[f][i] = mk[b + i].id;
       }
       h->parity[f] ^= 1;
       kw = std::max(kw, ((2 + 2 * m + 3) / 4) * 4);
@@ -363,20 +400,23 @@ int flush(ekf_ctx* h) {
     sl.cap = cap;
   }
   std::memcpy(sl.p, h->plan_d.data(), nd * sizeof(MsgDesc));
-  HIPCHK(hipStreamWaitEvent(h->stream, h->ev_sig, 0));  // the bulk stream may still read descriptors
+  if (join_bulk(h)) return EKF_E_HIP;  // the bulk stream may still read descriptors
   HIPCHK(hipMemcpyAsync(h->ddesc, sl.p, nd * sizeof(MsgDesc), hipMemcpyHostToDevice, h->stream));
+  // the bulk stream reads these descriptors too: one main → bulk hop per upload
+  HIPCHK(hipEventRecord(h->ev_chain, h->stream));
+  HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
   HIPCHK(hipEventRecord(sl.ev, h->stream));
   sl.used = true;
   int rc = EKF_OK;
   for (const Launch& L : h->plan_l) {
     const MsgDesc* dp = h->ddesc + L.off;
     if (L.kind == 1) {
-      if (hipStreamWaitEvent(h->stream, h->ev_sig, 0) != hipSuccess) return EKF_E_HIP;
+      if (join_bulk(h)) return EKF_E_HIP;
       rc = assoc(h, dp, L.f0, L.nf);
     }
     if (!rc && L.kind <= 1) rc = pair(h, dp, L.f0, L.nf, L.kw, L.kind == 0);
     if (!rc && L.kind == 2) {
-      if (hipStreamWaitEvent(h->stream, h->ev_sig, 0) != hipSuccess) return EKF_E_HIP;
+      if (join_bulk(h)) return EKF_E_HIP;
       rc = posterior_launch(h, dp, L.f0, L.nf);
     }
     if (rc) break;
@@ -494,7 +534,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   h->parity.assign(h->F, 0);
   h->pending.assign(h->F, 0);
   h->prev_m.assign(h->F, -1);
-  h->prev_first.assign(h->F, 0);
+  h->prev_ids.assign(h->F, std::array<int, kMaxChunk>{});
   h->msgs.resize(h->F);
   auto fail = [&](int rc) {
     ekf_destroy(h);
@@ -503,8 +543,10 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
   if (const char* e = std::getenv("EKF_SERIAL")) h->serial = std::atoi(e) != 0;
   if (create_streams(h) != EKF_OK ||
-      hipEventCreateWithFlags(&h->ev_fac, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_sig, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->ev_chain, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_sig[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_sig[1], hipEventDisableTiming) != hipSuccess)
     return fail(EKF_E_HIP);
   const size_t sig_bytes = h->sig_stride * h->F * h->w;
   for (int p = 0; p < 2; ++p) {
@@ -516,7 +558,10 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipMalloc(&h->kcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->mcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->ctl, sizeof(FilterCtl) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
-  if (hipMalloc(&h->rec, sizeof(ChunkRec) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
+  if (hipMalloc(&h->rec, 2 * sizeof(ChunkRec) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
+  const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + h->F);
+  if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
+  if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
   h->ddesc_cap = static_cast<size_t>(h->F) * 4;
   if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->ddesc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
   for (int i = 0; i < kRing; ++i)
@@ -565,8 +610,11 @@ int ekf_destroy(ekf_t h) {
     for (auto e : pe.stop) hipEventDestroy(e);
   }
   for (auto e : h->pool) hipEventDestroy(e);
-  if (h->ev_fac) hipEventDestroy(h->ev_fac);
-  if (h->ev_sig) hipEventDestroy(h->ev_sig);
+  if (h->ev_chain) hipEventDestroy(h->ev_chain);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
+  if (h->sync) hipFree(h->sync);
+  for (hipEvent_t e : h->ev_sig)
+    if (e) hipEventDestroy(e);
   if (h->bulk) hipStreamDestroy(h->bulk);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;

@@ -17,14 +17,17 @@ constexpr int kMaxKW = ((2 + 2 * kMaxChunk + 3) / 4) * 4;  // rank of the fused 
 constexpr int kMaxAssoc = 64;                    // association slots per filter per upload
 constexpr int kZC = 2 * kMaxChunk;               // correction columns of Z / rows of Y
 
+// Device epochs (unsigned words of the handle's sync buffer, each polled word on its own line):
+constexpr int kSyncSigma = 0;    // epoch (seq + 1) of the last complete Σ pass (k_sigma_epoch)
+constexpr int kSyncChain = 64;   // [F]: epoch of each filter's last complete chain
+
 // MsgDesc.flags
 constexpr int kFirst = 1;    // chunk carries the predict (slam.cpp:184-198) for this message
 constexpr int kLast = 2;     // chunk ends the message: posterior t_map_odom (slam.cpp:273-291)
 constexpr int kNoInit = 4;   // association path: no first-sighting init in the correction
 constexpr int kActive = 8;   // filter takes part in this launch
-constexpr int kLook = 16;    // Σ_in not materialised yet: rebuild the block from the previous
-                             // chunk's Σ_in (other buffer) and factors (Kcat/Mcat, prev_m)
-constexpr int kPrevFirst = 32;  // the previous chunk carried a predict (Q̄ in its Σ pass)
+constexpr int kLook = 16;    // Σ_in not materialised yet: rebuild the chain's block from the
+                             // previous chunk's Σ_in (other buffer) and ChunkRec
 
 // One chunk of one message for one filter (uploaded by the host, read by every kernel of the pair).
 struct alignas(16) MsgDesc {
@@ -33,10 +36,11 @@ struct alignas(16) MsgDesc {
   int parity;        // which Σ / x copy is "in"
   int assoc_slot;    // association: index into FilterCtl::assoc_j for ids[c] < 0
   double odom[3];    // t_odom_robot (θ, x, y) at this message
-  int prev_m;        // kLook: markers of the previous chunk (its factor rank)
+  int prev_m;        // kLook: markers of the previous chunk
   int pad1;
   int ids[kMaxChunk];        // landmark ids; < 0 ⇒ taken from FilterCtl::assoc_j[assoc_slot + c]
   double z[kMaxChunk][2];    // measured (range, bearing), computed on the host like slam.cpp:208-210
+  int prev_ids[kMaxChunk];   // kLook: the previous chunk's ids (its index set U', known up front)
 };
 
 struct alignas(16) FilterCtl {

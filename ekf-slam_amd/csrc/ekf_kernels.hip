@@ -72,11 +72,11 @@ __device__ __forceinline__ double alpha_of(int idx, double a1, double a2) {
 
 // Predicted pose and the two nonzeros of At (slam.cpp:184-196). xin = posterior of the last
 // message = filter_previous_configuration (slam.cpp:291).
-__device__ __forceinline__ void predicted_pose(const FilterCtl* ctl, const MsgDesc& d,
+__device__ __forceinline__ void predicted_pose(const double* tmo, const MsgDesc& d,
                                                const double* xin, double* pose, double* a1,
                                                double* a2) {
   if (d.flags & kFirst) {
-    const Pose2 cur = compose(Pose2{ctl->tmo[0], ctl->tmo[1], ctl->tmo[2]},
+    const Pose2 cur = compose(Pose2{tmo[0], tmo[1], tmo[2]},
                               Pose2{d.odom[0], d.odom[1], d.odom[2]});
     *a1 = -(cur.y - xin[2]);
     *a2 = cur.x - xin[1];
@@ -175,9 +175,25 @@ struct ChainShared {
   double nu[kMaxChunk][2];
   double Hs[kMaxChunk][2][5];    // H_c over pA (published for waves 1–2)
   double Sis[kMaxChunk][4];      // S_c⁻¹
-  double LK[kMaxKW][kMaxU];      // kLook: previous chunk's Kcat / Mcat at U
-  double LM[kMaxKW][kMaxU];
+  // kLook: the previous chunk's record and the blocks rebuilt from it
+  struct {
+    int u[kMaxU];
+    int nu, m, first;
+    double a1, a2, s00;
+    double xU[kMaxU], Zx[kMaxU];
+    // k (over U') padded to kMaxU + 1 = 36 with zeros, so MFMA operand reads need no predicate
+    double Z[kMaxU + 1][kZC + 1];
+    double Y[kZC][kMaxU + 1];
+    double R[kMaxU][kMaxU + 1];       // Σ_pred'[U][U']  (U' = previous chunk's index set)
+    double C[kMaxU + 1][kMaxU + 1];   // Σ_pred'[U'][U]
+    double K[kMaxU][kZC + 1];     // R·Z'  = the previous K_c at U
+    double M[kZC][kMaxU + 1];     // Y'·C  = the previous M_c at U
+    double r0U[kMaxU], c0U[kMaxU], r0P[kMaxU], c0P[kMaxU];
+    double xg[kMaxU];             // x_in'[u] for this chunk's U (rows the previous chunk missed)
+  } pv;
   double pose[3];
+  double xpose[3];  // x_in pose (posterior of the previous chunk)
+  double tmo[3];    // t_map_odom
   double a1, a2, s00;
   int nu_cnt;
   unsigned status;
@@ -190,6 +206,48 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
   const int hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), l);
   return __hiloint2double(hi, lo);
+}
+
+// ---- cross-queue hand-offs (chain on the main stream, factors + Σ pass on the bulk stream) ----
+// Protocol of cdna_hip_programming.md §6 Guideline 16: the producer stores its payload write-through
+// (sc1), every storing wave drains (s_waitcnt vmcnt(0)), a workgroup barrier, then ONE lane stores
+// or adds to an agent-scope epoch word; the consumer polls that word relaxed, takes ONE agent
+// acquire, drains, barriers, then loads plainly. Polls are bounded (EKF_FLAG_TIMEOUT).
+#define EKF_FLAG_TIMEOUT_D 4u
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ unsigned epoch_load(const unsigned* p) {
+  return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void epoch_store(unsigned* p, unsigned v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// One lane: wait until the epoch word reaches v (wrap-safe), then acquire. false on timeout.
+__device__ __noinline__ bool epoch_wait_acquire(const unsigned* p, unsigned v) {
+  bool ok = false;
+  for (unsigned i = 0; i < (1u << 22); ++i) {
+    if (static_cast<int>(epoch_load(p) - v) >= 0) {
+      ok = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return ok;
+}
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// write-through stores of hand-off payload
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store((gu64*)p, static_cast<unsigned long long>(__double_as_longlong(v)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(int* p, int v) {
+  __hip_atomic_store((gu32*)p, static_cast<unsigned>(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Intra-workgroup hand-off through LDS (waves on different SIMDs; no s_barrier).
@@ -220,8 +278,18 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
   const int tid = threadIdx.x;
   const int ld = A.ld;
   FilterCtl* ctl = A.ctl + f;
+  // Σ_in / x / records this chain reads come from the Σ pass two launches back (bulk stream)
+  if (A.need_sigma && tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, A.need_sigma))
+    atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
   for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.Z[0][0])[e] = 0.0;
   for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.Y[0][0])[e] = 0.0;
+  for (int e = tid; e < kMaxU * (kMaxU + 1); e += blockDim.x) {  // Φ = Ψ = I
+    const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
+    (&sh.Phi[0][0][0])[e] = a == b ? 1.0 : 0.0;
+    (&sh.Psi[0][0][0])[e] = a == b ? 1.0 : 0.0;
+  }
+  if (tid == 0) sh.status = 0;
+  drain_stores();
   __syncthreads();
   EKF_STAMP(0);
   const T* S = A.sig[d.parity] + f * A.sig_stride;
@@ -229,73 +297,273 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
   const int m = d.m;
   const bool first = (d.flags & kFirst) != 0;
 
-  // ---- A0: predict pose, index set U --------------------------------------------------------
-  if (tid == 0) {
-    double a1, a2;
-    predicted_pose(ctl, d, xin, sh.pose, &a1, &a2);
-    sh.a1 = a1;
-    sh.a2 = a2;
-    sh.u[0] = 0;
-    sh.u[1] = 1;
-    sh.u[2] = 2;
-    unsigned st = 0;
-    for (int c = 0; c < m; ++c) {
-      const int id = d.ids[c] >= 0 ? d.ids[c] : ctl->assoc_j[d.assoc_slot + c];
+  // kLook: this chunk's Σ_in is still being written by the previous chunk's Σ pass. Rebuild what
+  // the chain needs from the chunk before: Σ_in' (the other buffer, complete) and its record.
+  const bool look = (d.flags & kLook) != 0;
+  const ChunkRec* rp = A.rec + static_cast<size_t>(d.parity ^ 1) * A.rec_stride + f;
+
+  // ---- A0: index sets U (this chunk) and U' (kLook: the previous chunk, from the descriptor) ----
+  if (tid < kMaxU) {  // u[3+2c], u[4+2c] = the columns of marker c's landmark (bad id → slot 0's)
+    int u = tid < 3 ? tid : 0;  // padding 0: loads stay in bounds
+    if (tid >= 3 && tid < 3 + 2 * m) {
+      const int c = (tid - 3) >> 1, idd = d.ids[c];
+      const int id = idd >= 0 ? idd : ctl->assoc_j[d.assoc_slot + c];
       const bool bad = id < 0 || id >= A.N;
-      sh.skip[c] = bad ? 1 : 0;
-      if (bad && d.ids[c] >= 0) st |= EKF_FLAG_RANGE_D;  // association skips were flagged already
-      const int j = bad ? 3 : 3 + 2 * id;
-      sh.u[3 + 2 * c] = j;
-      sh.u[4 + 2 * c] = j + 1;
+      u = (bad ? 3 : 3 + 2 * id) + ((tid - 3) & 1);
+      if (((tid - 3) & 1) == 0) {
+        sh.skip[c] = bad ? 1 : 0;
+        if (bad && idd >= 0) atomicOr(&sh.status, EKF_FLAG_RANGE_D);  // association: flagged already
+      }
     }
-    for (int b = 3 + 2 * m; b < kMaxU; ++b) sh.u[b] = 0;  // padding: loads stay in bounds
-    sh.nu_cnt = 3 + 2 * m;
-    sh.status = st;
+    sh.u[tid] = u;
+  }
+  if (tid == 0) sh.nu_cnt = 3 + 2 * m;
+  if (look && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0's columns)
+    const int pm = d.prev_m;
+    int u = 0;
+    if (tid < 3) {
+      u = tid;
+    } else if (tid < 3 + 2 * pm) {
+      const int c = (tid - 3) >> 1, id = d.prev_ids[c];
+      u = (id < 0 || id >= A.N ? 3 : 3 + 2 * id) + ((tid - 3) & 1);
+    }
+    sh.pv.u[tid] = u;
+    if (tid == 0) {
+      sh.pv.nu = 3 + 2 * pm;
+      sh.pv.m = pm;
+    }
   }
   __syncthreads();
   EKF_STAMP(1);
   const int nu = sh.nu_cnt;
 
-  // ---- A1: gather the |U|×|U| block, x[U], identities --------------------------------------
-  // kLook: the previous chunk's Σ pass may still be running, so rebuild Σ_in[U,U] from that
-  // chunk's Σ_in (the other buffer) and its factors, in the Σ pass's own order (Σ + Q̄, then one
-  // fma per rank-1 term in k order, in T) — the values the Σ pass writes.
-  if (d.flags & kLook) {
+  // ---- A1: every global load of the prologue in one round ---------------------------------------
+  // Each thread issues all of its loads before its first LDS store: indices are clamped rather
+  // than predicated (a predicated load becomes a branch with its own wait), so the loads of a
+  // thread are in flight together instead of one memory round trip per loop iteration.
+  constexpr int kW = kMaxU + 1;  // block entries are indexed e = a·36 + b (constant divisor)
+  constexpr int kPer = (kW * kW + kChainThreads - 1) / kChainThreads;  // 6
+  const int wv = tid >> 6, ln = tid & 63, i16 = ln & 15, k4 = ln >> 4;
+  if (look) {
+    // Σ_in[U,U] = Σ_pred'[U,U] − K'·M' with Σ_pred' = A'·Σ_in'·A'ᵀ + Q̄' (the previous chunk's
+    // predict, if it had one), K'[a] = Σ_pred'[u_a, U']·Z', M'[:, b] = Y'·Σ_pred'[U', u_b]: the
+    // factor kernel's formulas evaluated at U only.
     const T* Sp = A.sig[d.parity ^ 1] + f * A.sig_stride;
-    const T* kcp = A.kcat + f * A.km_stride;
-    const T* mcp = A.mcat + f * A.km_stride;
-    const int kwp = ((2 + 2 * d.prev_m + 3) / 4) * 4;
-    for (int e = tid; e < kwp * nu; e += blockDim.x) {
-      const int k = e / nu, a = e - k * nu;
-      sh.LK[k][a] = static_cast<double>(kcp[static_cast<size_t>(k) * A.ldk + sh.u[a]]);
-      sh.LM[k][a] = static_cast<double>(mcp[static_cast<size_t>(k) * A.ldk + sh.u[a]]);
+    const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
+    const int np = sh.pv.nu;
+    double vz[kPer], vy[kPer], vd[kPer], vr[kPer], vc[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads;
+      vz[i] = (&rp->Z[0][0])[e < kMaxU * kZC ? e : 0];
+      vy[i] = (&rp->Y[0][0])[e < kZC * kMaxU ? e : 0];
+      const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);  // clamped: in bounds
+      const size_t ua = static_cast<size_t>(sh.u[a]) * ld, pa = static_cast<size_t>(sh.pv.u[b]);
+      vd[i] = static_cast<double>(Sp[ua + sh.u[b]]);
+      vr[i] = static_cast<double>(Sp[ua + pa]);
+      vc[i] = static_cast<double>(Sp[pa * ld + sh.u[a]]);
+    }
+    // raw row 0 / column 0 of Σ_in' at U and U' (for the previous predict), x', record scalars
+    const int tc = tid < kMaxU ? tid : 0;
+    const int uu = sh.u[tc], pu = sh.pv.u[tc];
+    const double r0u = static_cast<double>(Sp[uu]);
+    const double c0u = static_cast<double>(Sp[static_cast<size_t>(uu) * ld]);
+    const double r0p = static_cast<double>(Sp[pu]);
+    const double c0p = static_cast<double>(Sp[static_cast<size_t>(pu) * ld]);
+    const double x0 = rp->xU[tc], x1 = rp->Zx[tc], x2 = xp[uu];
+    const int pflags = rp->flags;
+    const double pa1 = rp->a1, pa2 = rp->a2;
+    const double tq = ctl->tmo[tid < 3 ? tid : 0];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads;
+      if (e < kMaxU * kZC) (&sh.pv.Z[0][0])[(e / kZC) * (kZC + 1) + e % kZC] = vz[i];
+      if (e < kZC * kMaxU) (&sh.pv.Y[0][0])[(e / kMaxU) * (kMaxU + 1) + e % kMaxU] = vy[i];
+    }
+    if (tid < kZC) {  // the 36th k row / column
+      sh.pv.Z[kMaxU][tid] = 0.0;
+      sh.pv.Y[tid][kMaxU] = 0.0;
+    }
+    if (tid < kMaxU) {
+      sh.pv.r0U[tid] = r0u;
+      sh.pv.c0U[tid] = c0u;
+      sh.pv.r0P[tid] = r0p;
+      sh.pv.c0P[tid] = c0p;
+      sh.pv.xU[tid] = x0;
+      sh.pv.Zx[tid] = x1;
+      sh.pv.xg[tid] = x2;
+    }
+    if (tid == 0) {
+      sh.pv.first = (pflags & kFirst) != 0;
+      sh.pv.a1 = pa1;
+      sh.pv.a2 = pa2;
+    }
+    if (tid < 3) sh.tmo[tid] = tq;
+    __syncthreads();
+    // the previous predict on the gathered values: v + α_i·Σ[0][j] + (Σ[i][0] + α_i·Σ00)·α_j + Q̄;
+    // R / C columns k ≥ |U'| up to 36 are zeroed (MFMA k padding)
+    const bool pf = sh.pv.first != 0;
+    const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads;
+      const int a = e / kW, b = e % kW;
+      if (a < nu && b < nu) {
+        double v = vd[i];
+        if (pf) {
+          const double ai = alpha_of(sh.u[a], qa1, qa2), aj = alpha_of(sh.u[b], qa1, qa2);
+          v = v + ai * sh.pv.r0U[b];
+          v = v + (sh.pv.c0U[a] + ai * s00) * aj;
+          if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
+        }
+        sh.P[0][a][b] = v;
+      }
+      if (a < nu && b < kW) {  // b = k over U'
+        double v = 0.0, w = 0.0;
+        if (b < np) {
+          v = vr[i];
+          w = vc[i];
+          if (pf) {
+            const double ai = alpha_of(sh.u[a], qa1, qa2), ak = alpha_of(sh.pv.u[b], qa1, qa2);
+            v = v + ai * sh.pv.r0P[b];
+            v = v + (sh.pv.c0U[a] + ai * s00) * ak;
+            w = w + ak * sh.pv.r0U[a];
+            w = w + (sh.pv.c0P[b] + ak * s00) * ai;
+            if (sh.u[a] == sh.pv.u[b] && sh.u[a] < 3) {
+              v += A.q;
+              w += A.q;
+            }
+          }
+        }
+        sh.pv.R[a][b] = v;
+        sh.pv.C[b][a] = w;
+      }
     }
     __syncthreads();
-    const T q = static_cast<T>(A.q);
-    for (int e = tid; e < nu * nu; e += blockDim.x) {
-      const int a = e / nu, b = e - a * nu;
-      T acc = Sp[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]];
-      if ((d.flags & kPrevFirst) && sh.u[a] == sh.u[b] && sh.u[a] < 3) acc += q;
-      for (int k = 0; k < kwp; ++k)
-        acc = fma(-static_cast<T>(sh.LK[k][a]), static_cast<T>(sh.LM[k][b]), acc);
-      sh.P[0][a][b] = static_cast<double>(acc);
-      sh.Phi[0][a][b] = a == b ? 1.0 : 0.0;
-      sh.Psi[0][a][b] = a == b ? 1.0 : 0.0;
+    EKF_STAMP(3);
+    EKF_STAMP(4);
+    // K' (48×32: 6 tiles of R·Z') and M' (32×48: 6 tiles of Y'·C) on f64 MFMA, 12 tiles over the 4
+    // waves. Operand reads are unconditional (clamped rows / columns feed only discarded outputs,
+    // k ≥ |U'| is zero-padded), all issued before the tile's first MFMA.
+    for (int tt = wv; tt < 12; tt += 4) {
+      double av[9], bv[9];
+      const bool kt = tt < 6;
+      const int ti = kt ? tt >> 1 : (tt - 6) / 3, tj = kt ? tt & 1 : (tt - 6) % 3;
+      const int ar = min(16 * ti + i16, kMaxU - 1), bc = min(16 * tj + i16, kMaxU - 1);
+      if (kt) {
+#pragma unroll
+        for (int s0 = 0; s0 < 9; ++s0) {
+          av[s0] = sh.pv.R[ar][4 * s0 + k4];
+          bv[s0] = sh.pv.Z[4 * s0 + k4][16 * tj + i16];
+        }
+      } else {
+#pragma unroll
+        for (int s0 = 0; s0 < 9; ++s0) {
+          av[s0] = sh.pv.Y[16 * ti + i16][4 * s0 + k4];
+          bv[s0] = sh.pv.C[4 * s0 + k4][bc];
+        }
+      }
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s0 = 0; s0 < 9; ++s0)
+        if (4 * s0 < np) acc = mfma_f64(av[s0], bv[s0], acc);
+      if (kt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * ti + k4 + 4 * r;
+          if (row < kMaxU) sh.pv.K[row][16 * tj + i16] = acc[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (16 * tj + i16 < kMaxU) sh.pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[r];
+      }
+    }
+    if (tid < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
+      const int u = sh.u[tid];
+      int pos = -1;
+      double acc = 0.0;
+#pragma unroll
+      for (int k = kMaxU - 1; k >= 0; --k) {
+        const bool hit = k < np && sh.pv.u[k] == u;
+        pos = hit ? k : pos;
+      }
+#pragma unroll
+      for (int k = 0; k < kMaxU; ++k) acc = fma(sh.pv.R[tid][k], sh.pv.Zx[k], acc);  // R[·][k ≥ |U'|] = 0
+      sh.xU[0][tid] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[tid] + acc;
+    }
+    if (tid < 3) sh.xpose[tid] = sh.pv.xU[tid];  // pose ∈ U' always
+    __syncthreads();
+    EKF_STAMP(5);
+    if (tid == 192) {  // wave 3 has one P tile fewer: the predicted pose (slam.cpp:184-196) here
+      double a1, a2;
+      predicted_pose(sh.tmo, d, sh.xpose, sh.pose, &a1, &a2);
+      sh.a1 = a1;
+      sh.a2 = a2;
+    }
+    // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
+    // ≥ 2m' are zero because Z' / Y' are)
+    const int zc = 2 * sh.pv.m;
+    for (int tt = wv; tt < 9; tt += 4) {
+      const int ti = tt / 3, tj = tt % 3;
+      const int col = 16 * tj + i16, ar = min(16 * ti + i16, kMaxU - 1), cc = min(col, kMaxU - 1);
+      double av[8], bv[8];
+#pragma unroll
+      for (int s0 = 0; s0 < 8; ++s0) {
+        av[s0] = -sh.pv.K[ar][4 * s0 + k4];
+        bv[s0] = sh.pv.M[4 * s0 + k4][cc];
+      }
+      d4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = min(16 * ti + k4 + 4 * r, kMaxU - 1);
+        acc[r] = sh.P[0][row][cc];
+      }
+#pragma unroll
+      for (int s0 = 0; s0 < 8; ++s0)
+        if (4 * s0 < zc) acc = mfma_f64(av[s0], bv[s0], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * ti + k4 + 4 * r;
+        if (row < nu && col < nu) sh.P[0][row][col] = acc[r];
+      }
     }
   } else {
-    for (int e = tid; e < nu * nu; e += blockDim.x) {
-      const int a = e / nu, b = e - a * nu;
-      sh.P[0][a][b] = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]]);
-      sh.Phi[0][a][b] = a == b ? 1.0 : 0.0;
-      sh.Psi[0][a][b] = a == b ? 1.0 : 0.0;
+    double vd[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads;
+      const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
+      vd[i] = static_cast<double>(S[static_cast<size_t>(sh.u[a]) * ld + sh.u[b]]);
+    }
+    const double xv = xin[sh.u[tid < nu ? tid : 0]];
+    const double xq = xin[tid < 3 ? tid : 0];
+    const double tq = ctl->tmo[tid < 3 ? tid : 0];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads;
+      const int a = e / kW, b = e % kW;
+      if (a < nu && b < nu) sh.P[0][a][b] = vd[i];
+    }
+    if (tid < nu) sh.xU[0][tid] = xv;
+    if (tid < 3) {
+      sh.xpose[tid] = xq;
+      sh.tmo[tid] = tq;
+    }
+    __syncthreads();
+    if (tid == 192) {
+      double a1, a2;
+      predicted_pose(sh.tmo, d, sh.xpose, sh.pose, &a1, &a2);
+      sh.a1 = a1;
+      sh.a2 = a2;
     }
   }
-  if (tid < nu) {
-    sh.xU[0][tid] = tid < 3 ? sh.pose[tid] : xin[sh.u[tid]];
-    sh.alphaU[tid] = first ? alpha_of(sh.u[tid], sh.a1, sh.a2) : 0.0;
-  }
+  EKF_STAMP(6);
+  // ---- A3: x[U] pose, α, this chunk's predict folded in: P ← A P Aᵀ + Q̄ (slam.cpp:198) --------
   __syncthreads();
   if (tid < nu) {
+    if (tid < 3) sh.xU[0][tid] = sh.pose[tid];
+    sh.alphaU[tid] = first ? alpha_of(sh.u[tid], sh.a1, sh.a2) : 0.0;
     sh.row0raw[tid] = sh.P[0][0][tid];
     sh.col0raw[tid] = sh.P[0][tid][0];
   }
@@ -303,8 +571,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
   __syncthreads();
   // predict folded in: P ← A P Aᵀ + Q̄ on the block (slam.cpp:198)
   if (first) {
-    for (int e = tid; e < nu * nu; e += blockDim.x) {
-      const int a = e / nu, b = e - a * nu;
+    for (int e = tid; e < kW * kW; e += blockDim.x) {
+      const int a = e / kW, b = e % kW;
+      if (a >= nu || b >= nu) continue;
       double v = sh.P[0][a][b] + sh.alphaU[a] * sh.row0raw[b];
       v = v + (sh.col0raw[a] + sh.alphaU[a] * sh.s00) * sh.alphaU[b];
       if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
@@ -603,33 +872,36 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
     }
   }
   __syncthreads();
-  // hand the chunk to the factor kernel
-  ChunkRec* rec = A.rec + f;
+  // hand the chunk to the factor kernel (and the next chain): write-through record, then the epoch
+  ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
   for (int e = tid; e < kMaxU * kZC; e += blockDim.x) {
     const int b = e / kZC, k = e - b * kZC;
-    rec->Z[b][k] = sh.Z[b][k];
+    st_wt(&rec->Z[b][k], sh.Z[b][k]);
   }
   for (int e = tid; e < kZC * kMaxU; e += blockDim.x) {
     const int k = e / kMaxU, b = e - k * kMaxU;
-    rec->Y[k][b] = sh.Y[k][b];
+    st_wt(&rec->Y[k][b], sh.Y[k][b]);
   }
   if (tid < kMaxU) {
     const bool in = tid < nu;
-    rec->u[tid] = sh.u[tid];
-    rec->alphaU[tid] = in ? sh.alphaU[tid] : 0.0;
-    rec->row0raw[tid] = in ? sh.row0raw[tid] : 0.0;
-    rec->col0raw[tid] = in ? sh.col0raw[tid] : 0.0;
-    rec->Zx[tid] = sh.Zx[tid];
-    rec->xU[tid] = in ? xfin[tid] : 0.0;
+    st_wt(&rec->u[tid], sh.u[tid]);
+    st_wt(&rec->alphaU[tid], in ? sh.alphaU[tid] : 0.0);
+    st_wt(&rec->row0raw[tid], in ? sh.row0raw[tid] : 0.0);
+    st_wt(&rec->col0raw[tid], in ? sh.col0raw[tid] : 0.0);
+    st_wt(&rec->Zx[tid], sh.Zx[tid]);
+    st_wt(&rec->xU[tid], in ? xfin[tid] : 0.0);
   }
   if (tid == 0) {
-    rec->m = m;
-    rec->nu = nu;
-    rec->flags = d.flags;
-    rec->a1 = sh.a1;
-    rec->a2 = sh.a2;
-    rec->s00 = sh.s00;
+    st_wt(&rec->m, m);
+    st_wt(&rec->nu, nu);
+    st_wt(&rec->flags, d.flags);
+    st_wt(&rec->a1, sh.a1);
+    st_wt(&rec->a2, sh.a2);
+    st_wt(&rec->s00, sh.s00);
   }
+  drain_stores();
+  __syncthreads();
+  if (tid == 0) epoch_store(A.sync + kSyncChain + f, A.seq + 1u);
   EKF_STAMP(40);
 }
 
@@ -657,8 +929,13 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
   double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
   T* kc = A.kcat + f * A.km_stride;
   T* mc = A.mcat + f * A.km_stride;
-  const ChunkRec* rec = A.rec + f;
+  const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
   const bool first = (d.flags & kFirst) != 0;
+  // the chain of this chunk runs on the other stream: wait for its record
+  if (tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
+    atomicOr(&A.ctl[f].status, EKF_FLAG_TIMEOUT_D);
+  drain_stores();
+  __syncthreads();
   for (int e = tid; e < kMaxU * kZC; e += blockDim.x) {
     const int b = e / kZC, k = e - b * kZC;
     sh.Z[b][k] = rec->Z[b][k];
@@ -882,21 +1159,26 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles) {
   SIG_STAMP(0);
   const MsgDesc& d = A.desc[blockIdx.y];
-  if (!(d.flags & kActive)) return;
-  SIG_STAMP(1);
-  const int f = A.f0 + blockIdx.y;
-  const int n = A.n;
-  const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
   // One 32×32 tile per wave, tiles row-major over a tiles × tiles grid.
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (t >= tiles * tiles) return;
-  const int tr = t / tiles, tc = t - tr * tiles;
-  const int R0 = tr * 32, C0 = tc * 32;
-  sigma_tile(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
-             A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, n, A.ld, A.ldk, kw,
-             (d.flags & kFirst) != 0, A.q, R0, C0, lane);
+  if ((d.flags & kActive) && t < tiles * tiles) {
+    SIG_STAMP(1);
+    const int f = A.f0 + blockIdx.y;
+    const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
+    const int tr = t / tiles, tc = t - tr * tiles;
+    sigma_tile(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
+               A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
+               (d.flags & kFirst) != 0, A.q, tr * 32, tc * 32, lane);
+  }
   SIG_STAMP(3);
+}
+
+// Σ-pass epoch for the chains on the other stream, launched right behind the Σ pass on its stream:
+// the kernel boundary's release has written the pass's Σ_out (and the factor kernel's x, Kcat,
+// Mcat) back before this store, so the pass itself keeps plain stores and no per-block release.
+__global__ void k_sigma_epoch(unsigned* sync, unsigned epoch) {
+  if (threadIdx.x == 0) epoch_store(sync + kSyncSigma, epoch);
 }
 
 // ---- association ------------------------------------------------------------------------------
@@ -921,7 +1203,7 @@ __global__ __launch_bounds__(256) void k_assoc(PassArgs<T> A) {
   const int slot = d.assoc_slot;
   if (tid == 0) {
     double a1, a2;
-    predicted_pose(ctl, d, x, s_pose, &a1, &a2);
+    predicted_pose(ctl->tmo, d, x, s_pose, &a1, &a2);
     s_a[0] = a1;
     s_a[1] = a2;
     double raw[3][3];
@@ -1108,6 +1390,7 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s
   const dim3 grid((tiles * tiles + wpb - 1) / wpb, nf);
   (void)kw;
   launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles);
+  hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();
 }
 

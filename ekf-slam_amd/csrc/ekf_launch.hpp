@@ -22,7 +22,11 @@ struct PassArgs {
   size_t km_stride;
   int ldk;
   FilterCtl* ctl;
-  ChunkRec* rec;        // one per filter
+  ChunkRec* rec;        // [2][rec_stride]: chunk records by Σ parity (chain → factors, next chain)
+  size_t rec_stride;
+  unsigned* sync;       // device epochs (ekf_device.hpp kSync*)
+  unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
+  unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
   const MsgDesc* desc;
   int n, ld, N, f0;
   double q, r, gate;

@@ -8,7 +8,14 @@
 #include <vector>
 
 using namespace ekfslam;
+static int g_look = 0;
 
+static unsigned* sync_buf(int nf) {  // device epochs (kSync*), zeroed
+  unsigned* p = nullptr;
+  const size_t bytes = sizeof(unsigned) * (kSyncChain + nf);
+  if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) abort();
+  return p;
+}
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 
 template <typename T>
@@ -42,7 +49,7 @@ void run(int N, int m, int reps) {
   CK(hipMalloc(&mc, kMaxKW * ldk * sizeof(T)));
   CK(hipMalloc(&ctl, sizeof(FilterCtl)));
   CK(hipMemset(ctl, 0, sizeof(FilterCtl)));
-  CK(hipMalloc(&rec, sizeof(ChunkRec)));
+  CK(hipMalloc(&rec, 2 * sizeof(ChunkRec)));
   MsgDesc d{};
   d.m = m;
   d.flags = kActive | kFirst | kLast;
@@ -54,15 +61,26 @@ void run(int N, int m, int reps) {
     d.z[c][1] = atan2(ly, lx) + 0.001;
   }
   CK(hipMalloc(&dd, sizeof(MsgDesc)));
+  // record at parity 1 first (no kLook), then the timed chains rebuild from it (kLook, parity 0)
+  d.parity = 1;
   CK(hipMemcpy(dd, &d, sizeof(MsgDesc), hipMemcpyHostToDevice));
   PassArgs<T> a{};
   a.sig[0] = dS[0]; a.sig[1] = dS[1]; a.sig_stride = 0;
   a.x[0] = dx[0]; a.x[1] = dx[1]; a.x_stride = 0;
   a.kcat = kc; a.mcat = mc; a.km_stride = 0; a.ldk = ldk;
-  a.ctl = ctl; a.rec = rec; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0;
+  a.ctl = ctl; a.sync = sync_buf(4096); a.rec = rec; a.rec_stride = 1; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0;
   a.q = 1e-2; a.r = 1e-2; a.gate = 2.0;
   hipStream_t s;
   CK(hipStreamCreate(&s));
+  CK(launch_chain<T>(a, 1, s));
+  CK(hipStreamSynchronize(s));
+  if (g_look) {
+    d.parity = 0;
+    d.flags |= kLook;
+    d.prev_m = m;
+    for (int c = 0; c < m; ++c) d.prev_ids[c] = d.ids[c];
+    CK(hipMemcpy(dd, &d, sizeof(MsgDesc), hipMemcpyHostToDevice));
+  }
   for (int i = 0; i < 5; ++i) CK(launch_chain<T>(a, 1, s));
   CK(hipStreamSynchronize(s));
   hipEvent_t e0, e1;
@@ -91,7 +109,8 @@ void run(int N, int m, int reps) {
     }
     printf(" %s %.0f", nm[p], acc / (m > 1 ? m - 1 : 1));
   }
-  printf("\n");
+  printf("\n    prologue stamps (cycles from 0): loads %llu transform %llu K'M' %llu P %llu\n",
+         st[3] - st[0], st[4] - st[0], st[5] - st[0], st[6] - st[0]);
   CK(hipEventRecord(e0, s));
   for (int i = 0; i < reps; ++i) CK(launch_factors<T>(a, 1, s));
   CK(hipEventRecord(e1, s));
@@ -100,7 +119,9 @@ void run(int N, int m, int reps) {
   printf("    factors %.2f us/launch\n", ms * 1e3 / reps);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) g_look = atoi(argv[1]);
+  printf("kLook %d\n", g_look);
   run<double>(50, 4, 200);
   run<double>(256, 16, 200);
   run<float>(1024, 16, 200);

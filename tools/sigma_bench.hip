@@ -10,6 +10,12 @@
 
 using namespace ekfslam;
 static int g_pingpong = 0;
+static unsigned* sync_buf(int nf) {  // device epochs (kSync*), zeroed
+  unsigned* p = nullptr;
+  const size_t bytes = sizeof(unsigned) * (kSyncChain + nf);
+  if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) abort();
+  return p;
+}
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 
 template <typename V>
@@ -45,7 +51,7 @@ void run(int N, int F, int reps) {
   PassArgs<T> a{};
   a.sig[0] = S0; a.sig[1] = S1; a.sig_stride = stride;
   a.kcat = kc; a.mcat = mc; a.km_stride = static_cast<size_t>(kMaxKW) * ldk; a.ldk = ldk;
-  a.ctl = ctl; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0; a.q = 1e-2;
+  a.ctl = ctl; a.sync = sync_buf(4096); a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0; a.q = 1e-2;
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
