@@ -600,46 +600,60 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
   }
   __syncthreads();
   if (wave == 0) {
+    // Lane ℓ carries row ℓ of the step's block columns (pk = Σ[ℓ, pA]) and column ℓ of its block
+    // rows (pm = Σ[pA, ℓ]) in registers from one step to the next: the cross update of step c
+    // produces exactly step c+1's pk (and pm for the later columns). S needs no block read:
+    // (Σ·Hᵀ)[ℓ] is the first half of K anyway, and S = H·(Σ·Hᵀ)[pA] takes five lanes' values by
+    // v_readlane. The pose / landmark x of a step come by v_readlane from the lane that updated
+    // them. Lanes ≥ |U| carry a clamped row and never store.
+    const int lr = lane < kMaxU ? lane : kMaxU - 1;
+    const int ul = sh.u[lr];
+    double pk[5], pm[5];
+    double xl = sh.xU[0][lr];
+#pragma unroll
+    for (int a = 0; a < 5; ++a) {
+      const int col = a < 3 ? a : 3 + a - 3;  // pA of step 0 = {0, 1, 2, 3, 4}
+      pk[a] = sh.P[0][lr][col];
+      pm[a] = sh.P[0][col][lr];
+    }
     for (int c = 0; c < m; ++c) {
-      const int pj = 3 + 2 * c;
+      const int pj = 3 + 2 * c, nx = pj + 2;
+      const bool more = c + 1 < m;
       EKF_STAMP(64 + 6 * c);
-      const double* xc = sh.xU[0];
       const double z0 = d.z[c][0], z1 = d.z[c][1];
+      bool sk = sh.skip[c] != 0;
+      const double* xc = sh.xU[0];  // written by this wave at the end of the previous step
       const double pose[3] = {xc[0], xc[1], xc[2]};
       double lx = xc[pj], ly = xc[pj + 1];
-      bool sk = sh.skip[c] != 0;
       bool init = false;
       if (!sk && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
         init = true;
         lx = pose[1] + z0 * cos(z1 + pose[0]);
         ly = pose[2] + z0 * sin(z1 + pose[0]);
       }
-      const int pA[5] = {0, 1, 2, pj, pj + 1};
       double H0[5], H1[5], Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
+      double zhat[2];
+      range_bearing(pose, lx, ly, zhat, H0, H1);
+      EKF_STAMP(65 + 6 * c);
+      // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]
+      double ka = 0.0, kb = 0.0, mm0 = 0.0, mm1 = 0.0;
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        ka += pk[a] * H0[a];
+        kb += pk[a] * H1[a];
+        mm0 += H0[a] * pm[a];
+        mm1 += H1[a] * pm[a];
+      }
       {
-        double zhat[2];
-        range_bearing(pose, lx, ly, zhat, H0, H1);
-        EKF_STAMP(65 + 6 * c);
-        double HP0[5], HP1[5];
-#pragma unroll
-        for (int bb = 0; bb < 5; ++bb) {
-          double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-          for (int a = 0; a < 5; ++a) {
-            const double v = sh.P[0][pA[a]][pA[bb]];
-            s0 += H0[a] * v;
-            s1 += H1[a] * v;
-          }
-          HP0[bb] = s0;
-          HP1[bb] = s1;
-        }
-        double Sm[4] = {0.0, 0.0, 0.0, 0.0};
+        double Sm[4] = {0.0, 0.0, 0.0, 0.0};  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:252)
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
-          Sm[0] += HP0[a] * H0[a];
-          Sm[1] += HP0[a] * H1[a];
-          Sm[2] += HP1[a] * H0[a];
-          Sm[3] += HP1[a] * H1[a];
+          const int l = a < 3 ? a : pj + a - 3;
+          const double ta = readlane_f64(ka, l), tb = readlane_f64(kb, l);
+          Sm[0] += H0[a] * ta;
+          Sm[1] += H0[a] * tb;
+          Sm[2] += H1[a] * ta;
+          Sm[3] += H1[a] * tb;
         }
         Sm[0] += A.r;
         Sm[3] += A.r;
@@ -656,42 +670,40 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
         for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
         Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
         nv0 = nv1 = 0.0;
+        ka = kb = mm0 = mm1 = 0.0;
+      }
+      // the next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}): wave 3 must have applied
+      // step c−1 outside this step's cross first
+      const int bx = more ? nx : pj;  // last step: any in-bounds columns, unused
+      double xr[5], xq[5];
+      if (more) lds_wait_ge(&sh.pdone, c);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int col = k < 3 ? k : bx + k - 3;
+        xr[k] = sh.P[0][lr][col];
+        xq[k] = sh.P[0][col][lr];
       }
       const int jx = sh.u[pj];
       EKF_STAMP(66 + 6 * c);
-      double K0 = 0.0, K1 = 0.0, mm0 = 0.0, mm1 = 0.0;  // row / column `lane` of this step
-      if (lane < nu) {  // K[U] = Σ[U, pA]·Hᵀ·S⁻¹, M[:, live] = H·Σ[pA, live], x[U]
-        double ka = 0.0, kb = 0.0;
-#pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          const double v = sh.P[0][lane][pA[a]];
-          ka += v * H0[a];
-          kb += v * H1[a];
-        }
-        K0 = ka * Si[0] + kb * Si[2];
-        K1 = ka * Si[1] + kb * Si[3];
-        if (lane < 3 || lane >= pj + 2) {
-#pragma unroll
-          for (int a = 0; a < 5; ++a) {
-            const double v = sh.P[0][pA[a]][lane];
-            mm0 += H0[a] * v;
-            mm1 += H1[a] * v;
-          }
-        }
-        double xt = xc[lane];
+      const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
+      const double K1 = ka * Si[1] + kb * Si[3];
+      {
+        double xt = xl;
         if (init) {
-          if (sh.u[lane] == jx) xt = lx;
-          else if (sh.u[lane] == jx + 1) xt = ly;
+          if (ul == jx) xt = lx;
+          else if (ul == jx + 1) xt = ly;
         }
         xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
         if (lane == 0) xt = normalize_angle(xt);     // slam.cpp:267
-        sh.xU[0][lane] = xt;
+        xl = xt;
+        if (lane < nu) sh.xU[0][lane] = xt;
       }
       if (lane < kMaxU) {
-        sh.KU[c][lane][0] = K0;
-        sh.KU[c][lane][1] = K1;
-        sh.MU[c][lane][0] = mm0;
-        sh.MU[c][lane][1] = mm1;
+        const bool in = lane < nu;
+        sh.KU[c][lane][0] = in ? K0 : 0.0;
+        sh.KU[c][lane][1] = in ? K1 : 0.0;
+        sh.MU[c][lane][0] = in ? mm0 : 0.0;
+        sh.MU[c][lane][1] = in ? mm1 : 0.0;
       }
       if (lane == 0) {
 #pragma unroll
@@ -704,34 +716,43 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
         sh.nu[c][0] = nv0;
         sh.nu[c][1] = nv1;
       }
-      lds_publish(&sh.pub, c + 1);
+      lds_publish(&sh.pub, c + 1);  // drains this wave's LDS writes first
       EKF_STAMP(67 + 6 * c);
-      if (c + 1 < m) {
-        const int nx = pj + 2;  // next marker's columns; Bx = {0, 1, 2, nx, nx+1}
-        // K and M of the five Bx rows / columns, broadcast from their lanes
+      if (more) {
+        // K and M of the five Bx rows / columns, from their lanes
         double kx0[5], kx1[5], mx0[5], mx1[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
           const int l = k < 3 ? k : nx + k - 3;
-          kx0[k] = readlane_f64(K0, l);
-          kx1[k] = readlane_f64(K1, l);
-          mx0[k] = readlane_f64(mm0, l);
-          mx1[k] = readlane_f64(mm1, l);
+          kx0[k] = sh.KU[c][l][0];
+          kx1[k] = sh.KU[c][l][1];
+          mx0[k] = sh.MU[c][l][0];
+          mx1[k] = sh.MU[c][l][1];
         }
-        lds_wait_ge(&sh.pdone, c);  // wave 3 has applied step c−1 outside this step's cross
         EKF_STAMP(68 + 6 * c);
-        if (lane < nu) {  // all rows × Bx columns
+        // all rows × Bx columns: next step's pk
 #pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            const int b = k < 3 ? k : nx + k - 3;
-            sh.P[0][lane][b] = rank2_sub(sh.P[0][lane][b], K0, K1, mx0[k], mx1[k]);
-          }
+        for (int k = 0; k < 5; ++k) {
+          const int col = k < 3 ? k : nx + k - 3;
+          pk[k] = rank2_sub(xr[k], K0, K1, mx0[k], mx1[k]);
+          if (lane < nu) sh.P[0][lane][col] = pk[k];
         }
-        if (lane >= nx + 2 && lane < nu) {  // Bx rows × columns of markers ≥ c+2
+        // Bx rows × columns of markers ≥ c+2: next step's pm there
+        const bool later = lane >= nx + 2 && lane < nu;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+          const int row = k < 3 ? k : nx + k - 3;
+          const double v = rank2_sub(xq[k], kx0[k], kx1[k], mm0, mm1);
+          pm[k] = v;
+          if (later) sh.P[0][row][lane] = v;
+        }
+        // pm of the Bx columns themselves (and pose): entries another lane just wrote
+        const bool own = lane < 3 || lane == nx || lane == nx + 1;
+        if (own) {  // LDS executes one wave's accesses in order: the reads see the writes above
 #pragma unroll
           for (int k = 0; k < 5; ++k) {
-            const int a = k < 3 ? k : nx + k - 3;
-            sh.P[0][a][lane] = rank2_sub(sh.P[0][a][lane], kx0[k], kx1[k], mm0, mm1);
+            const int row = k < 3 ? k : nx + k - 3;
+            pm[k] = sh.P[0][row][lane];
           }
         }
       }
@@ -748,13 +769,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
         const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
         double pv[16], k0[16], k1[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int a = 3 + hr + 2 * i;
-          if (a < nu) {
-            pv[i] = sh.P[0][a][b];
-            k0[i] = sh.KU[c][a][0];
-            k1[i] = sh.KU[c][a][1];
-          }
+        for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
+          const int a = min(3 + hr + 2 * i, kMaxU - 1);
+          pv[i] = sh.P[0][a][b];
+          k0[i] = sh.KU[c][a][0];
+          k1[i] = sh.KU[c][a][1];
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -795,12 +814,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
           double pv[18], z0[18], z1[18];
 #pragma unroll
           for (int i = 0; i < 18; ++i) {
-            const int a = hr + 2 * i;
-            if (a < nu) {
-              pv[i] = sh.Phi[0][a][b];
-              z0[i] = sh.Z[a][2 * c];
-              z1[i] = sh.Z[a][2 * c + 1];
-            }
+            const int a = min(hr + 2 * i, kMaxU - 1);
+            pv[i] = sh.Phi[0][a][b];
+            z0[i] = sh.Z[a][2 * c];
+            z1[i] = sh.Z[a][2 * c + 1];
           }
 #pragma unroll
           for (int i = 0; i < 18; ++i) {
@@ -837,12 +854,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
 #pragma unroll
           for (int i = 0; i < 17; ++i) {
             const int bi = hr + 2 * i;
-            const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
-            if (bi < live) {
-              pv[i] = sh.Psi[0][b][a];
-              k0[i] = sh.KU[c][b][0];
-              k1[i] = sh.KU[c][b][1];
-            }
+            const int b = min(bi < 3 ? bi : pj + 2 + (bi - 3), kMaxU - 1);
+            pv[i] = sh.Psi[0][b][a];
+            k0[i] = sh.KU[c][b][0];
+            k1[i] = sh.KU[c][b][1];
           }
 #pragma unroll
           for (int i = 0; i < 17; ++i) {

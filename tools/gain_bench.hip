@@ -97,7 +97,7 @@ void run(int N, int m, int reps) {
   printf("N=%d m=%d %s: chain %.2f us/launch | A0 %llu A1 %llu endA %llu | per step (avg cycles):",
          N, m, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, st[1] - st[0], st[2] - st[0],
          st[40] - st[0]);
-  const char* nm[6] = {"rb", "S+inv", "KMx+pub", "wait", "cross", "loop"};
+  const char* nm[6] = {"rb", "S+inv+xpre", "KMx+pub", "kx", "cross", "loop"};
   const int pts[7] = {64, 65, 66, 67, 68, 69, 70};
   for (int p = 0; p < 6; ++p) {
     double acc = 0;
