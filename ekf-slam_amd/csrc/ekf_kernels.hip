@@ -479,6 +479,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
           if (16 * tj + i16 < kMaxU) sh.pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[r];
       }
     }
+    EKF_STAMP(7);
     if (tid < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
       const int u = sh.u[tid];
       int pos = -1;

@@ -223,3 +223,69 @@ def test_n1024_fp32_warm_state_against_oracle():
     seen = np.abs(np.diag(S32)) < 1e6
     assert np.all(np.diag(S32)[seen][3:] > 0)
     assert np.all(np.isfinite(S32))
+
+
+def _pipelined_final(sc, monkeypatch, env, dtype=pyekf.EKF_F64, F=1):
+    """Replay every message in one call (one upload, chunks pipelined across the two streams)."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    odom = pyekf.odometry(sc)
+    e = pyekf.EKF(n_landmarks=sc.n_landmarks, n_filters=F, dtype=dtype)
+    rep = lambda a: np.repeat(a[:, None], F, 1)  # noqa: E731
+    e.replay(rep(sc.count), rep(sc.rel), rep(odom), ids=rep(sc.ids), actions=rep(sc.actions))
+    out = [e.state(f) for f in range(F)]
+    e.close()
+    return out
+
+
+@pytest.mark.parametrize("F", [1, 4], ids=["1filter", "4filters"])
+def test_pipelined_replay_sync_modes_bit_identical(monkeypatch, F):
+    """The device-epoch pipeline (chains on one stream, factors + Σ passes on the other, no host
+    events), the event-synchronised two-stream pipeline and the single-stream order compute the
+    same numbers: every kernel does the same arithmetic, only the synchronisation differs. Run
+    without per-message synchronisation so chunks really overlap, then against the oracle."""
+    sc = synth.synthetic(256, 30)
+    dev = _pipelined_final(sc, monkeypatch, {}, F=F)
+    evt = _pipelined_final(sc, monkeypatch, {"EKF_DEVSYNC": "0"}, F=F)
+    ser = _pipelined_final(sc, monkeypatch, {"EKF_SERIAL": "1"}, F=F)
+    for (xd, Sd, cd), (xe, Se, ce), (xs, Ss, cs) in zip(dev, evt, ser):
+        assert cd == ce == cs
+        np.testing.assert_array_equal(xd, xs)
+        np.testing.assert_array_equal(Sd, Ss)
+        np.testing.assert_array_equal(xe, xs)
+        np.testing.assert_array_equal(Se, Ss)
+    o = orc.run_scenario(sc, False)
+    x, S, _ = dev[0]
+    assert np.abs(x - o["state"]).max() < 1e-7
+    assert np.abs(S - o["sigma"]).max() < 1e-7
+
+
+def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
+    """Config 3 size, fp32 Σ, 24 messages pipelined: device-epoch vs single-stream bit-identical."""
+    N, warm, T = 1024, 40, 24
+    sc = synth.synthetic(N, warm + T)
+    odom = pyekf.odometry(sc)
+    e64 = pyekf.EKF(n_landmarks=N)
+    e64.replay(sc.count[:warm, None], sc.rel[:warm, None], odom[:warm, None],
+               ids=sc.ids[:warm, None], actions=sc.actions[:warm, None])
+    x0, S0, c0 = e64.state()
+    tmo0 = e64.map_odom()
+    e64.close()
+    res = []
+    for env in ({}, {"EKF_SERIAL": "1"}):
+        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        e = pyekf.EKF(n_landmarks=N, dtype=pyekf.EKF_F32)
+        e.set_state(x0, S0, tmo=tmo0, counter=c0)
+        sl = slice(warm, warm + T)
+        e.replay(sc.count[sl, None], sc.rel[sl, None], odom[sl, None], ids=sc.ids[sl, None],
+                 actions=sc.actions[sl, None])
+        res.append(e.state())
+        e.close()
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    assert np.all(np.isfinite(res[0][1]))

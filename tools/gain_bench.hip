@@ -109,8 +109,8 @@ void run(int N, int m, int reps) {
     }
     printf(" %s %.0f", nm[p], acc / (m > 1 ? m - 1 : 1));
   }
-  printf("\n    prologue stamps (cycles from 0): loads %llu transform %llu K'M' %llu P %llu\n",
-         st[3] - st[0], st[4] - st[0], st[5] - st[0], st[6] - st[0]);
+  printf("\n    prologue stamps (cycles from 0): A0 %llu loads+transform %llu K'M'-tiles %llu +x %llu P %llu\n",
+         st[1] - st[0], st[3] - st[0], st[7] - st[0], st[5] - st[0], st[6] - st[0]);
   CK(hipEventRecord(e0, s));
   for (int i = 0; i < reps; ++i) CK(launch_factors<T>(a, 1, s));
   CK(hipEventRecord(e1, s));
