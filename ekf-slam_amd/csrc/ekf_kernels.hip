@@ -1171,16 +1171,27 @@ __device__ __forceinline__ void sigma_tile(const float* Sin, float* Sout, const 
   }
 }
 
+// xcd_b = 0: grid (blocks per filter, filters). xcd_b = B > 0 (many filters): a 1-D grid whose
+// block L runs on XCD L % 8 (dispatch deals blocks round-robin over the XCDs); it is given filter
+// 8·⌊(L/8)/B⌋ + L % 8, tile block (L/8) % B, so all of a filter's blocks share one XCD and its
+// Kcat/Mcat are fetched into one L2 instead of eight. Placement only changes speed.
 template <typename T>
-__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles) {
+__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles, int xcd_b, int nf) {
   SIG_STAMP(0);
-  const MsgDesc& d = A.desc[blockIdx.y];
+  int fb = blockIdx.y, bx = blockIdx.x;
+  if (xcd_b > 0) {
+    const int L = blockIdx.x, j = L >> 3;
+    fb = (L & 7) + 8 * (j / xcd_b);
+    bx = j % xcd_b;
+    if (fb >= nf) return;
+  }
+  const MsgDesc& d = A.desc[fb];
   // One 32×32 tile per wave, tiles row-major over a tiles × tiles grid.
   const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int t = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if ((d.flags & kActive) && t < tiles * tiles) {
     SIG_STAMP(1);
-    const int f = A.f0 + blockIdx.y;
+    const int f = A.f0 + fb;
     const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
     const int tr = t / tiles, tc = t - tr * tiles;
     sigma_tile(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
@@ -1403,9 +1414,15 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s
                              hipEvent_t e1) {
   const int tiles = (a.n + 31) / 32;
   const int wpb = g_sigma_waves;
-  const dim3 grid((tiles * tiles + wpb - 1) / wpb, nf);
+  const int per_filter = (tiles * tiles + wpb - 1) / wpb;
   (void)kw;
-  launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles);
+  if (nf >= 16) {  // XCD-aware 1-D grid (see k_sigma_pass)
+    const dim3 grid(8 * ((nf + 7) / 8) * per_filter);
+    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles, per_filter, nf);
+  } else {
+    const dim3 grid(per_filter, nf);
+    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles, 0, nf);
+  }
   hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();
 }
