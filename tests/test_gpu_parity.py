@@ -289,3 +289,42 @@ def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
     np.testing.assert_array_equal(res[0][0], res[1][0])
     np.testing.assert_array_equal(res[0][1], res[1][1])
     assert np.all(np.isfinite(res[0][1]))
+
+
+@pytest.mark.parametrize("F", [24, 40], ids=["24filters_devsync", "40filters_events"])
+def test_many_filters_match_small_batch(F):
+    """≥16 filters take the XCD-aware Σ-pass grid, > 32 filters the event-synchronised streams;
+    filter f replays scenario f % 8, and must equal the same scenario in an 8-filter handle bit for
+    bit (the arithmetic per filter does not depend on the batch)."""
+    N, T = 64, 12
+    scs = [synth.synthetic(N, T, seed=100 + k) for k in range(8)]
+    odo = [pyekf.odometry(s) for s in scs]
+    M = max(s.ids.shape[1] for s in scs)
+
+    def run(nf):
+        cnt = np.zeros((T, nf), np.int32)
+        ids = np.full((T, nf, M), -1, np.int32)
+        act = np.zeros((T, nf, M), np.int32)
+        rel = np.zeros((T, nf, M, 2))
+        od = np.zeros((T, nf, 3))
+        for f in range(nf):
+            s = scs[f % 8]
+            k = s.ids.shape[1]
+            cnt[:, f] = s.count
+            ids[:, f, :k] = s.ids
+            act[:, f, :k] = s.actions
+            rel[:, f, :k] = s.rel
+            od[:, f] = odo[f % 8]
+        e = pyekf.EKF(n_landmarks=N, n_filters=nf)
+        e.replay(cnt, rel, od, ids=ids, actions=act)
+        out = [e.state(f) for f in range(nf)]
+        e.close()
+        return out
+
+    small, big = run(8), run(F)
+    for f in range(F):
+        xs, Ss, cs = small[f % 8]
+        xb, Sb, cb = big[f]
+        assert cs == cb
+        np.testing.assert_array_equal(xs, xb)
+        np.testing.assert_array_equal(Ss, Sb)
