@@ -87,6 +87,7 @@ struct ekf_ctx {
   ProfEvents pe[4];
   std::vector<hipEvent_t> pool;
   long long prof_launches[4] = {0, 0, 0, 0};
+  long long prof_chunks = 0;  // chunks the timed chain launches walked
   double prof_ms[4] = {0, 0, 0, 0};
 };
 
@@ -185,45 +186,54 @@ int join_bulk(ekf_ctx* h) {
 // epoch. A hipStreamWaitEvent hop between the queues costs 6–12 µs, a device poll ≈ 1–2 µs.
 // Without the CU split a spinning factor grid could hold every CU the chain needs, so events are
 // used instead (the kernels' polls are then satisfied on arrival).
+// `nchunks` consecutive chunks of filters [f0, f0+nf) (descriptors dptr[i·nf + k]): ONE chain
+// launch that walks them all (carrying its block from chunk to chunk), then per chunk the factor
+// kernel and the Σ pass on the bulk stream. More than one chunk only with devsync, where the bulk
+// kernels of chunk i wait on the device for the chain's epoch of chunk i.
 template <typename T>
-int launch_pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pipelined) {
+int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined) {
   PassArgs<T> a = args<T>(h, dptr, f0);
-  const unsigned s = static_cast<unsigned>(h->seq);
-  a.seq = s;
+  a.desc_stride = nf;
+  const unsigned s0 = static_cast<unsigned>(h->seq);
+  a.seq = s0;
   const bool two = pipelined && !h->serial;
   hipStream_t ms = h->stream, bs = two ? h->bulk : h->stream;
   if (pipelined) {
-    a.need_sigma = s >= 2 ? s - 1 : 0;  // epoch of the Σ pass two launches back
-    if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s & 1], 0));
+    if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s0 & 1], 0));
   } else {
-    a.need_sigma = 0;
     if (join_bulk(h)) return EKF_E_HIP;
   }
   int rc = timed(h, 1, ms, [&](hipEvent_t e0, hipEvent_t e1) {
-    return launch_chain<T>(a, nf, ms, e0, e1);
+    return launch_chain<T>(a, nf, nchunks, ms, e0, e1);
   });
   if (rc) return rc;
-  if (two && !h->devsync) {
+  if (h->prof) h->prof_chunks += nchunks;
+  if (two && !h->devsync) {  // nchunks == 1 here
     HIPCHK(hipEventRecord(h->ev_chain, ms));
     HIPCHK(hipStreamWaitEvent(bs, h->ev_chain, 0));
   }
-  // factors gather the materialised Σ_in (the previous Σ pass, same stream) and the chain's record
-  rc = timed(h, 3, bs, [&](hipEvent_t e0, hipEvent_t e1) {
-    return launch_factors<T>(a, nf, bs, e0, e1);
-  });
-  if (rc) return rc;
-  rc = timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
-    return launch_sigma_pass<T>(a, nf, kw, bs, e0, e1);
-  });
-  if (rc) return rc;
-  if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[s & 1], bs));
-  ++h->seq;
+  for (int i = 0; i < nchunks; ++i) {
+    PassArgs<T> ai = a;
+    ai.desc = dptr + static_cast<size_t>(i) * nf;
+    ai.seq = s0 + static_cast<unsigned>(i);
+    // factors gather the materialised Σ_in (the previous Σ pass, same stream) and the record
+    rc = timed(h, 3, bs, [&](hipEvent_t e0, hipEvent_t e1) {
+      return launch_factors<T>(ai, nf, bs, e0, e1);
+    });
+    if (rc) return rc;
+    rc = timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
+      return launch_sigma_pass<T>(ai, nf, 0, bs, e0, e1);
+    });
+    if (rc) return rc;
+    if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[(s0 + i) & 1], bs));
+  }
+  h->seq += nchunks;
   return EKF_OK;
 }
 
-int pair(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int kw, bool pipelined) {
-  return h->cfg.dtype == EKF_F32 ? launch_pair<float>(h, dptr, f0, nf, kw, pipelined)
-                                 : launch_pair<double>(h, dptr, f0, nf, kw, pipelined);
+int group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined) {
+  return h->cfg.dtype == EKF_F32 ? launch_group<float>(h, dptr, f0, nf, nchunks, pipelined)
+                                 : launch_group<double>(h, dptr, f0, nf, nchunks, pipelined);
 }
 
 // The chain → factors kernels of a message are a latency-bound critical path; the Σ pass of the
@@ -281,6 +291,28 @@ int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
   });
 }
 
+// kLook descriptors: where each index of this chunk's U sits in the previous chunk's U' (the
+// chain's mapping: pose 0..2, marker c → 3+2·id, 4+2·id, a bad id → slot 0's columns 3, 4).
+void index_map(MsgDesc* d, int N) {
+  auto col = [N](const int* ids, int a) {
+    if (a < 3) return a;
+    const int id = ids[(a - 3) >> 1];
+    return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
+  };
+  const int nu = 3 + 2 * d->m, np = 3 + 2 * d->prev_m;
+  d->nnew = 0;
+  for (int a = 0; a < kMaxU + 1; ++a) {
+    int pos = -1;
+    if (a < nu) {
+      const int u = col(d->ids, a);
+      for (int k = 0; k < np && pos < 0; ++k)
+        if (col(d->prev_ids, k) == u) pos = k;
+      if (pos < 0) ++d->nnew;
+    }
+    d->cpos[a] = static_cast<signed char>(pos);
+  }
+}
+
 // Known association, one message per filter in [f0, f0+nf): msgs[k] holds filter f0+k's markers.
 // Predict + chunks of ≤ kMaxChunk corrections + posterior (slam.cpp:180-316), appended to the plan.
 void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
@@ -309,13 +341,14 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
       fill_desc(d, m, flags, h->parity[f], h->odom[f]);
       d->prev_m = h->prev_m[f];
       for (int i = 0; i < kMaxChunk; ++i) d->prev_ids[i] = h->prev_ids[f][i];
-      h->prev_m[f] = m;
       for (int i = 0; i < m; ++i) {
         d->ids[i] = mk[b + i].id;
         d->z[i][0] = mk[b + i].zr;
         d->z[i][1] = mk[b + i].zb;
-        h->prev_ids[f][i] = mk[b + i].id;
       }
+      if (flags & kLook) index_map(d, h->cfg.n_landmarks);
+      h->prev_m[f] = m;
+      for (int i = 0; i < m; ++i) h->prev_ids[f][i] = mk[b + i].id;
       h->parity[f] ^= 1;
       kw = std::max(kw, ((2 + 2 * m + 3) / 4) * 4);
       if (chunk == 0) h->pending[f] = 0;
@@ -408,18 +441,30 @@ int flush(ekf_ctx* h) {
   HIPCHK(hipEventRecord(sl.ev, h->stream));
   sl.used = true;
   int rc = EKF_OK;
-  for (const Launch& L : h->plan_l) {
+  const size_t nl = h->plan_l.size();
+  for (size_t li = 0; li < nl && !rc;) {
+    const Launch& L = h->plan_l[li];
     const MsgDesc* dp = h->ddesc + L.off;
+    if (L.kind == 0) {  // a run of known-association chunks → one persistent chain launch
+      size_t lj = li + 1;
+      if (h->devsync && !h->serial)  // the bulk kernels must run beside the chain launch
+        while (lj < nl && h->plan_l[lj].kind == 0 && h->plan_l[lj].f0 == L.f0 &&
+               h->plan_l[lj].nf == L.nf && h->plan_l[lj].off == h->plan_l[lj - 1].off + L.nf)
+          ++lj;
+      rc = group(h, dp, L.f0, L.nf, static_cast<int>(lj - li), true);
+      li = lj;
+      continue;
+    }
     if (L.kind == 1) {
       if (join_bulk(h)) return EKF_E_HIP;
       rc = assoc(h, dp, L.f0, L.nf);
+      if (!rc) rc = group(h, dp, L.f0, L.nf, 1, false);
     }
-    if (!rc && L.kind <= 1) rc = pair(h, dp, L.f0, L.nf, L.kw, L.kind == 0);
     if (!rc && L.kind == 2) {
       if (join_bulk(h)) return EKF_E_HIP;
       rc = posterior_launch(h, dp, L.f0, L.nf);
     }
-    if (rc) break;
+    ++li;
   }
   h->plan_d.clear();
   h->plan_l.clear();
@@ -882,6 +927,10 @@ int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
   }
   pe.start.clear();
   pe.stop.clear();
+  if (kind == 1) {  // a chain launch walks several chunks: report per chunk
+    h->prof_launches[1] = h->prof_chunks;
+    h->prof_chunks = 0;
+  }
   if (launches) *launches = h->prof_launches[kind];
   if (total_ms) *total_ms = h->prof_ms[kind];
   h->prof_launches[kind] = 0;
@@ -890,6 +939,12 @@ int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
 }
 
 double ekf_normalize_angle(double rad) { return normalize_angle(rad); }
+
+#ifdef EKF_DIAG_STAMPS
+int ekfslam_diag_read_stamps(unsigned long long* out, int n);  // ekf_kernels.hip
+// dev only (libekfslam_diag.so): the chain kernel's s_memtime stamps of filter 0's last chunk
+int ekf_diag_stamps(unsigned long long* out, int n) { return ekfslam_diag_read_stamps(out, n); }
+#endif
 
 double ekf_sigma_pass_bytes(ekf_t h, int nf) {
   if (!h) return 0.0;

@@ -41,6 +41,9 @@ struct alignas(16) MsgDesc {
   int ids[kMaxChunk];        // landmark ids; < 0 ⇒ taken from FilterCtl::assoc_j[assoc_slot + c]
   double z[kMaxChunk][2];    // measured (range, bearing), computed on the host like slam.cpp:208-210
   int prev_ids[kMaxChunk];   // kLook: the previous chunk's ids (its index set U', known up front)
+  signed char cpos[kMaxU + 1];  // kLook: position of U[a] in U' (−1: new to this chunk)
+  int nnew;                     // kLook: count of cpos < 0
+  int pad2[2];
 };
 
 struct alignas(16) FilterCtl {
@@ -65,6 +68,8 @@ struct alignas(16) ChunkRec {
   double xU[kMaxU];
   double Z[kMaxU][kZC];
   double Y[kZC][kMaxU];
+  double Pend[kMaxU][kMaxU];         // the chain's final Σ[U, U] (fp64): written over the Σ pass's
+                                     // block so fp32 Σ keeps first sightings (1e7 − (1e7 − δ))
 };
 
 }  // namespace ekfslam

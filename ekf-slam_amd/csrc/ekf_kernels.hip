@@ -43,6 +43,14 @@ __device__ unsigned long long g_stamps[160];
   do {               \
   } while (0)
 #endif
+#ifdef EKF_DIAG_STAMPS
+}  // namespace ekfslam
+extern "C" int ekfslam_diag_read_stamps(unsigned long long* out, int n) {
+  using ekfslam::g_stamps;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < 160 ? n : 160)) == hipSuccess ? 0 : -5;
+}
+namespace ekfslam {
+#endif
 
 // Diagnostic build only (tools/sigma_bench.hip): s_memrealtime (100 MHz) per Σ-pass workgroup.
 #ifdef EKF_DIAG_STAMPS
@@ -191,7 +199,9 @@ struct ChainShared {
     double r0U[kMaxU], c0U[kMaxU], r0P[kMaxU], c0P[kMaxU];
     double xg[kMaxU];             // x_in'[u] for this chunk's U (rows the previous chunk missed)
   } pv;
+  double Pst[kMaxU][kMaxU + 1];  // carry: the previous chunk's final Σ[U', U'] (its U' order)
   double pose[3];
+  double npose[3], na1, na2;  // the next chunk's predicted pose and A entries (its prefetch)
   double xpose[3];  // x_in pose (posterior of the previous chunk)
   double tmo[3];    // t_map_odom
   double a1, a2, s00;
@@ -262,25 +272,65 @@ __device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
 
 constexpr int kChainThreads = 256;
 
-// One workgroup per filter: the chunk's m sequential corrections on the |U|×|U| block.
+// One workgroup per filter, persistent over the `nchunks` chunks of a launch (descriptors
+// A.desc[i·desc_stride + filter]): per chunk the m sequential corrections on the |U|×|U| block.
+// From the second chunk on, the block, x[U] and the factors of the chunk before stay in LDS
+// ("carry"): only indices new to U are gathered from HBM.
 template <typename T>
-__global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
+__global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchunks) {
   __shared__ ChainShared sh;
-  __shared__ MsgDesc sdesc;  // the descriptor is read every step: keep it in LDS, not global
+  // The descriptor is read every step: keep it in LDS. Two buffers: a chunk's epilogue prefetches
+  // the next one's (and computes its predicted pose from it).
+  __shared__ MsgDesc sdesc[2];
   static_assert(sizeof(MsgDesc) % 16 == 0, "MsgDesc copied as uint4");
-  const MsgDesc& gd = A.desc[blockIdx.y];
-  if (!(gd.flags & kActive)) return;
-  if (threadIdx.x < sizeof(MsgDesc) / 16)
-    reinterpret_cast<uint4*>(&sdesc)[threadIdx.x] =
-        reinterpret_cast<const uint4*>(&gd)[threadIdx.x];
-  const MsgDesc& d = sdesc;
   const int f = A.f0 + blockIdx.y;
   const int tid = threadIdx.x;
   const int ld = A.ld;
   FilterCtl* ctl = A.ctl + f;
-  // Σ_in / x / records this chain reads come from the Σ pass two launches back (bulk stream)
-  if (A.need_sigma && tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, A.need_sigma))
+  bool have_carry = false;
+  bool pre = false;        // sdesc[ci & 1] was prefetched by the previous chunk's epilogue
+  unsigned pending = 0;    // chain epoch of the previous chunk, not yet published (its record
+                           // stores are still in flight; see the epilogue)
+  for (int ci = 0; ci < nchunks; ++ci) {
+  if (!pre) {
+    const MsgDesc& gd = A.desc[static_cast<size_t>(ci) * A.desc_stride + blockIdx.y];
+    __syncthreads();
+    if (threadIdx.x < sizeof(MsgDesc) / 16)
+      reinterpret_cast<uint4*>(&sdesc[ci & 1])[threadIdx.x] =
+          reinterpret_cast<const uint4*>(&gd)[threadIdx.x];
+    __syncthreads();
+  }
+  const bool was_pre = pre;
+  pre = false;
+  const MsgDesc& d = sdesc[ci & 1];
+  const bool active = (d.flags & kActive) != 0;
+  const bool look = (d.flags & kLook) != 0;
+  const bool carry = look && have_carry;
+  // the previous epilogue computed this chunk's predicted pose iff it prefetched the descriptor
+  // and the chunk is an active kLook one (here: carried)
+  const bool pose_pre = was_pre && carry;
+  // Publish the previous chunk's record before this chunk waits on anything the bulk stream
+  // produces (its factor kernel needs that record). A carried chunk with no new index waits on
+  // nothing: it publishes just before its corrections, with the record stores long complete.
+  if (pending && !(active && carry && d.nnew == 0)) {
+    drain_stores();
+    __syncthreads();
+    if (tid == 0) epoch_store(A.sync + kSyncChain + f, pending);
+    pending = 0;
+  }
+  if (!active) continue;  // this filter sits the chunk out; its carry stays valid
+  const unsigned seq = A.seq + static_cast<unsigned>(ci);
+  // Σ_in / x / records a rebuilding chain reads come from the Σ pass two launches back (bulk
+  // stream); a chunk that gathers its own Σ_in needs the pass one back. Carry waits only when it
+  // has new indices to gather (below).
+  const unsigned need = look ? (seq >= 2 ? seq - 1 : 0u) : seq;
+  if (!carry && need && tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, need))
     atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+  if (carry && d.nnew > 0) {  // the previous chunk's Z', Y' rebuild the rows of new indices
+    for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.pv.Z[0][0])[e] = (&sh.Z[0][0])[e];
+    for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.pv.Y[0][0])[e] = (&sh.Y[0][0])[e];
+    if (tid < kZC) sh.pv.Z[kMaxU][tid] = 0.0;
+  }
   for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.Z[0][0])[e] = 0.0;
   for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.Y[0][0])[e] = 0.0;
   for (int e = tid; e < kMaxU * (kMaxU + 1); e += blockDim.x) {  // Φ = Ψ = I
@@ -289,7 +339,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
     (&sh.Psi[0][0][0])[e] = a == b ? 1.0 : 0.0;
   }
   if (tid == 0) sh.status = 0;
-  drain_stores();
   __syncthreads();
   EKF_STAMP(0);
   const T* S = A.sig[d.parity] + f * A.sig_stride;
@@ -299,7 +348,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
 
   // kLook: this chunk's Σ_in is still being written by the previous chunk's Σ pass. Rebuild what
   // the chain needs from the chunk before: Σ_in' (the other buffer, complete) and its record.
-  const bool look = (d.flags & kLook) != 0;
   const ChunkRec* rp = A.rec + static_cast<size_t>(d.parity ^ 1) * A.rec_stride + f;
 
   // ---- A0: index sets U (this chunk) and U' (kLook: the previous chunk, from the descriptor) ----
@@ -318,7 +366,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
     sh.u[tid] = u;
   }
   if (tid == 0) sh.nu_cnt = 3 + 2 * m;
-  if (look && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0's columns)
+  if (look && !carry && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0)
     const int pm = d.prev_m;
     int u = 0;
     if (tid < 3) {
@@ -344,7 +392,210 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
   constexpr int kW = kMaxU + 1;  // block entries are indexed e = a·36 + b (constant divisor)
   constexpr int kPer = (kW * kW + kChainThreads - 1) / kChainThreads;  // 6
   const int wv = tid >> 6, ln = tid & 63, i16 = ln & 15, k4 = ln >> 4;
-  if (look) {
+  if (carry) {
+    // The previous chunk of this launch left, in LDS: its final Σ[U', U'] (Pst), x[U'], Z', Y',
+    // K'_c (KU, every row of U') and M'_c (MU, every column of U'). Entries of Σ_in[U, U] with both
+    // indices in U' are Pst's; an entry with an index new to U is
+    //   Σ_pred'[u_a, u_b] − Σ_c K'_c[a]·M'_c[b],  K'_c[a] = Σ_pred'[u_a, U']·Z'_c for a new row,
+    //                                              M'_c[b] = Y'_c·Σ_pred'[U', u_b] for a new column,
+    // with Σ_pred' gathered from Σ_in' (the other buffer, complete two passes back).
+    // d.cpos is the host's index map (ekf_api.cpp index_map): position of u_a in U', −1 if new.
+    const int np = sh.pv.nu, zc = 2 * sh.pv.m;
+    const bool any_new = d.nnew > 0;
+    EKF_STAMP(8);
+    if (!any_new && pose_pre) {
+      // Σ_in[U, U] = Pst permuted, x[U] = x[U'] permuted, and this chunk's predict folded in
+      // directly (the A3 fold below, same expressions): one pass, no gather, no barrier.
+      // (indices clamped, reads unconditional: all of a thread's LDS reads in flight together)
+      const double qa1 = sh.na1, qa2 = sh.na2, p00 = sh.Pst[0][0];
+      int ua[kPer], ub[kPer];
+      double vp[kPer], vr[kPer], vc[kPer];
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + i * kChainThreads;
+        const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
+        const int pa = max(static_cast<int>(d.cpos[a]), 0), pb = max(static_cast<int>(d.cpos[b]), 0);
+        ua[i] = sh.u[a];
+        ub[i] = sh.u[b];
+        vp[i] = sh.Pst[pa][pb];
+        vr[i] = sh.Pst[0][pb];
+        vc[i] = sh.Pst[pa][0];
+      }
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + i * kChainThreads;
+        const int a = e / kW, b = e % kW;
+        double v = vp[i];
+        if (first) {
+          const double aa = alpha_of(ua[i], qa1, qa2), ab = alpha_of(ub[i], qa1, qa2);
+          v = v + aa * vr[i];
+          v = v + (vc[i] + aa * p00) * ab;
+          if (ua[i] == ub[i] && ua[i] < 3) v += A.q;
+        }
+        if (a < nu && b < nu) sh.P[0][a][b] = v;
+      }
+      if (tid < nu) {
+        const int pos = d.cpos[tid];
+        sh.xU[0][tid] = tid < 3 ? sh.npose[tid] : sh.pv.xU[pos];
+        sh.alphaU[tid] = first ? alpha_of(sh.u[tid], qa1, qa2) : 0.0;
+        sh.row0raw[tid] = sh.Pst[0][pos];
+        sh.col0raw[tid] = sh.Pst[pos][0];
+      }
+      if (tid == 0) {
+        sh.s00 = sh.Pst[0][0];
+        sh.a1 = qa1;
+        sh.a2 = qa2;
+      }
+    } else {
+    if (any_new) {
+      if (tid == 0 && need && !epoch_wait_acquire(A.sync + kSyncSigma, need))
+        atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+      drain_stores();
+      __syncthreads();
+      const T* Sp = A.sig[d.parity ^ 1] + f * A.sig_stride;
+      const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
+      double vd[kPer], vr[kPer], vc[kPer];
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + i * kChainThreads;
+        const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
+        const size_t ua = static_cast<size_t>(sh.u[a]) * ld, pa = static_cast<size_t>(sh.pv.u[b]);
+        vd[i] = static_cast<double>(Sp[ua + sh.u[b]]);
+        vr[i] = static_cast<double>(Sp[ua + pa]);
+        vc[i] = static_cast<double>(Sp[pa * ld + sh.u[a]]);
+      }
+      const int tc = tid < kMaxU ? tid : 0;
+      const int uu = sh.u[tc], pu = sh.pv.u[tc];
+      const double r0u = static_cast<double>(Sp[uu]);
+      const double c0u = static_cast<double>(Sp[static_cast<size_t>(uu) * ld]);
+      const double r0p = static_cast<double>(Sp[pu]);
+      const double c0p = static_cast<double>(Sp[static_cast<size_t>(pu) * ld]);
+      const double x2 = xp[uu];
+      if (tid < kMaxU) {
+        sh.pv.r0U[tid] = r0u;
+        sh.pv.c0U[tid] = c0u;
+        sh.pv.r0P[tid] = r0p;
+        sh.pv.c0P[tid] = c0p;
+        sh.pv.xg[tid] = x2;
+      }
+      __syncthreads();
+      const bool pf = sh.pv.first != 0;
+      const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + i * kChainThreads;
+        const int a = e / kW, b = e % kW;
+        if (a < nu && b < nu) {
+          double v = vd[i];
+          if (pf) {
+            const double ai = alpha_of(sh.u[a], qa1, qa2), aj = alpha_of(sh.u[b], qa1, qa2);
+            v = v + ai * sh.pv.r0U[b];
+            v = v + (sh.pv.c0U[a] + ai * s00) * aj;
+            if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
+          }
+          sh.P[0][a][b] = v;
+        }
+        if (a < nu && b < kW) {
+          double v = 0.0, w = 0.0;
+          if (b < np) {
+            v = vr[i];
+            w = vc[i];
+            if (pf) {
+              const double ai = alpha_of(sh.u[a], qa1, qa2), ak = alpha_of(sh.pv.u[b], qa1, qa2);
+              v = v + ai * sh.pv.r0P[b];
+              v = v + (sh.pv.c0U[a] + ai * s00) * ak;
+              w = w + ak * sh.pv.r0U[a];
+              w = w + (sh.pv.c0P[b] + ak * s00) * ai;
+              if (sh.u[a] == sh.pv.u[b] && sh.u[a] < 3) {
+                v += A.q;
+                w += A.q;
+              }
+            }
+          }
+          sh.pv.R[a][b] = v;
+          sh.pv.C[b][a] = w;
+        }
+      }
+      __syncthreads();
+      EKF_STAMP(9);
+      // K' rows and M' columns: the previous chain's K / M where U' has the index, else rebuilt
+      // (R, C, Z', Y' are zero beyond |U'| and 2m', so the sums run unguarded; columns ≥ 2m' of
+      // K' / rows of M' are written as zeros for the same reason below)
+      for (int e = tid; e < nu * kZC; e += blockDim.x) {
+        const int a = e >> 5, c = e & (kZC - 1);
+        const int pos = d.cpos[a];
+        double kk = 0.0, mm = 0.0;
+        if (c < zc) {
+          if (pos >= 0) {
+            kk = sh.KU[c >> 1][pos][c & 1];
+            mm = sh.MU[c >> 1][pos][c & 1];
+          } else {
+            double k2 = 0.0, m2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < kMaxU + 1; k += 2) {
+              kk = fma(sh.pv.R[a][k], sh.pv.Z[k][c], kk);
+              mm = fma(sh.pv.Y[c][k], sh.pv.C[k][a], mm);
+              if (k + 1 < kMaxU + 1) {
+                k2 = fma(sh.pv.R[a][k + 1], sh.pv.Z[k + 1][c], k2);
+                m2 = fma(sh.pv.Y[c][k + 1], sh.pv.C[k + 1][a], m2);
+              }
+            }
+            kk += k2;
+            mm += m2;
+          }
+        }
+        sh.pv.K[a][c] = kk;
+        sh.pv.M[c][a] = mm;
+      }
+      __syncthreads();
+    }
+    EKF_STAMP(10);
+    // Σ_in[U, U] and x[U]
+    for (int e = tid; e < kW * kW; e += blockDim.x) {
+      const int a = e / kW, b = e % kW;
+      if (a >= nu || b >= nu) continue;
+      const int pa = d.cpos[a], pb = d.cpos[b];
+      if (pa >= 0 && pb >= 0) {
+        sh.P[0][a][b] = sh.Pst[pa][pb];
+      } else {
+        double v = sh.P[0][a][b], w = 0.0;
+#pragma unroll
+        for (int c = 0; c < kZC; c += 2) {
+          v = fma(-sh.pv.K[a][c], sh.pv.M[c][b], v);
+          w = fma(-sh.pv.K[a][c + 1], sh.pv.M[c + 1][b], w);
+        }
+        sh.P[0][a][b] = v + w;
+      }
+    }
+    if (tid < nu) {
+      const int pos = d.cpos[tid];
+      double xv;
+      if (pos >= 0) {
+        xv = sh.pv.xU[pos];
+      } else {
+        double acc = 0.0;
+        for (int k = 0; k < np; ++k) acc = fma(sh.pv.R[tid][k], sh.pv.Zx[k], acc);
+        xv = sh.pv.xg[tid] + acc;
+      }
+      sh.xU[0][tid] = xv;
+    }
+    if (tid < 3) sh.xpose[tid] = sh.pv.xU[tid];  // pose ∈ U' always
+    __syncthreads();
+    EKF_STAMP(11);
+    if (tid == 192) {
+      if (pose_pre) {
+        for (int k = 0; k < 3; ++k) sh.pose[k] = sh.npose[k];
+        sh.a1 = sh.na1;
+        sh.a2 = sh.na2;
+      } else {
+        double a1, a2;
+        predicted_pose(sh.tmo, d, sh.xpose, sh.pose, &a1, &a2);
+        sh.a1 = a1;
+        sh.a2 = a2;
+      }
+    }
+    }
+  } else if (look) {
     // Σ_in[U,U] = Σ_pred'[U,U] − K'·M' with Σ_pred' = A'·Σ_in'·A'ᵀ + Q̄' (the previous chunk's
     // predict, if it had one), K'[a] = Σ_pred'[u_a, U']·Z', M'[:, b] = Y'·Σ_pred'[U', u_b]: the
     // factor kernel's formulas evaluated at U only.
@@ -561,6 +812,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
   }
   EKF_STAMP(6);
   // ---- A3: x[U] pose, α, this chunk's predict folded in: P ← A P Aᵀ + Q̄ (slam.cpp:198) --------
+  // (done in the carry pass above when the pose was ready)
+  if (!(carry && d.nnew == 0 && pose_pre)) {
   __syncthreads();
   if (tid < nu) {
     if (tid < 3) sh.xU[0][tid] = sh.pose[tid];
@@ -582,6 +835,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
     }
   }
   __syncthreads();
+  }
   EKF_STAMP(2);
 
   // ---- A2: the m corrections -----------------------------------------------------------------
@@ -599,7 +853,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
     sh.pub = 0;
     sh.pdone = 0;
   }
+  if (pending) drain_stores();
   __syncthreads();
+  if (pending) {
+    if (tid == 0) epoch_store(A.sync + kSyncChain + f, pending);
+    pending = 0;
+  }
   if (wave == 0) {
     // Lane ℓ carries row ℓ of the step's block columns (pk = Σ[ℓ, pA]) and column ℓ of its block
     // rows (pm = Σ[pA, ℓ]) in registers from one step to the next: the cross update of step c
@@ -738,8 +997,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
           pk[k] = rank2_sub(xr[k], K0, K1, mx0[k], mx1[k]);
           if (lane < nu) sh.P[0][lane][col] = pk[k];
         }
-        // Bx rows × columns of markers ≥ c+2: next step's pm there
-        const bool later = lane >= nx + 2 && lane < nu;
+        // Bx rows × every other column (the block is kept whole so that the chunk's final Σ[U,U]
+        // can seed the next chunk): next step's pm there
+        const bool later = lane >= 3 && lane < nu && lane != nx && lane != nx + 1;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
           const int row = k < 3 ? k : nx + k - 3;
@@ -759,23 +1019,24 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
       }
       EKF_STAMP(69 + 6 * c);
     }
-  } else if (wave == 3) {  // P outside the cross: rows ∉ next marker, columns of markers ≥ c+2
-    // lane → column nx+2+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
+  } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
+    // lane → column 3+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
     const int hb = lane & 31, hr = lane >> 5;
+    const int b = min(3 + hb, kMaxU - 1);
     for (int c = 0; c + 1 < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int nx = 5 + 2 * c;
-      const int b = nx + 2 + hb;
-      if (b < nu) {
-        const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
-        double pv[16], k0[16], k1[16];
+      const bool colok = 3 + hb < nu && b != nx && b != nx + 1;
+      const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
+      double pv[16], k0[16], k1[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
-          const int a = min(3 + hr + 2 * i, kMaxU - 1);
-          pv[i] = sh.P[0][a][b];
-          k0[i] = sh.KU[c][a][0];
-          k1[i] = sh.KU[c][a][1];
-        }
+      for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
+        const int a = min(3 + hr + 2 * i, kMaxU - 1);
+        pv[i] = sh.P[0][a][b];
+        k0[i] = sh.KU[c][a][0];
+        k1[i] = sh.KU[c][a][1];
+      }
+      if (colok) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int a = 3 + hr + 2 * i;
@@ -787,6 +1048,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
     }
   } else if (wave == 1) {  // Z_c and Φ (live columns)
     const int hb = lane & 31, hr = lane >> 5;
+    // The record parity this chunk writes was last written two chunks back: the bulk stream must
+    // be done with it (its factor kernel and block scatter finish before that chunk's Σ-pass
+    // epoch). A carried chunk without new indices has not polled; the others' polls covered this.
+    if (lane == 0 && carry && d.nnew == 0 && seq >= 2 &&
+        !epoch_wait_acquire(A.sync + kSyncSigma, seq - 1))
+      atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -871,54 +1138,113 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A) {
     }
   }
   __syncthreads();
-  const double* xfin = sh.xU[0];
-  if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
-    double zx = 0.0;
-    for (int c = 0; c < m; ++c) zx += sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];
-    sh.Zx[tid] = zx;
-  }
-  if (tid == 0) {
-    if (sh.status) atomicOr(&ctl->status, sh.status);
-    if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
-      const Pose2 tmo = compose(Pose2{xfin[0], xfin[1], xfin[2]},
-                                inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
-      ctl->tmo[0] = tmo.theta;
-      ctl->tmo[1] = tmo.x;
-      ctl->tmo[2] = tmo.y;
+  // The last step's rank-2 term on the whole block (earlier steps are applied), written to Pst:
+  // the final Σ[U, U] is what the next chunk of this launch carries.
+  {
+    const int c = max(m - 1, 0);
+    for (int e = tid; e < kMaxU * (kMaxU + 1); e += blockDim.x) {
+      const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
+      double v = sh.P[0][a][b];
+      if (m > 0 && a < nu && b < nu)
+        v = rank2_sub(v, sh.KU[c][a][0], sh.KU[c][a][1], sh.MU[c][b][0], sh.MU[c][b][1]);
+      sh.Pst[a][b] = v;
     }
   }
   __syncthreads();
-  // hand the chunk to the factor kernel (and the next chain): write-through record, then the epoch
-  ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
-  for (int e = tid; e < kMaxU * kZC; e += blockDim.x) {
-    const int b = e / kZC, k = e - b * kZC;
-    st_wt(&rec->Z[b][k], sh.Z[b][k]);
+  EKF_STAMP(12);
+  // ---- epilogue -----------------------------------------------------------------------------
+  // Wave 3 (one lane): the posterior t_map_odom, then the next chunk's predicted pose from its
+  // descriptor. Waves 0–2 meanwhile prefetch that descriptor, store the record write-through and
+  // keep the carry. The record's epoch is published at the next chunk's start (or the kernel's
+  // end): the stores drain behind the next prologue instead of stalling this one. The record
+  // parity's release (the bulk stream done with it) was awaited by wave 1 before its steps, or by
+  // the prologue's poll.
+  const double* xfin = sh.xU[0];
+  const bool pre_next = ci + 1 < nchunks;
+  if (wave == 3) {
+    if (lane == 0) {
+      if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
+        const Pose2 tmo = compose(Pose2{xfin[0], xfin[1], xfin[2]},
+                                  inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
+        ctl->tmo[0] = tmo.theta;
+        ctl->tmo[1] = tmo.x;
+        ctl->tmo[2] = tmo.y;
+        sh.tmo[0] = tmo.theta;
+        sh.tmo[1] = tmo.x;
+        sh.tmo[2] = tmo.y;
+      }
+      if (pre_next) {
+        const MsgDesc& gnd = A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y];
+        if ((gnd.flags & kActive) && (gnd.flags & kLook)) {
+          double a1, a2;
+          predicted_pose(sh.tmo, gnd, xfin, sh.npose, &a1, &a2);
+          sh.na1 = a1;
+          sh.na2 = a2;
+        }
+      }
+    }
+  } else {
+    constexpr int kT = 3 * 64;
+    if (pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
+      reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
+          &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
+    if (tid == 0 && sh.status) atomicOr(&ctl->status, sh.status);
+    // hand the chunk to the factor kernel (and the next chain): write-through record
+    ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+    if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
+      double zx = 0.0;
+      for (int c = 0; c < m; ++c) zx += sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];
+      const bool in = tid < nu;
+      st_wt(&rec->Zx[tid], zx);
+      st_wt(&rec->u[tid], sh.u[tid]);
+      st_wt(&rec->alphaU[tid], in ? sh.alphaU[tid] : 0.0);
+      st_wt(&rec->row0raw[tid], in ? sh.row0raw[tid] : 0.0);
+      st_wt(&rec->col0raw[tid], in ? sh.col0raw[tid] : 0.0);
+      st_wt(&rec->xU[tid], in ? xfin[tid] : 0.0);
+      sh.pv.u[tid] = sh.u[tid];
+      sh.pv.xU[tid] = xfin[tid];
+      sh.pv.Zx[tid] = zx;
+    }
+    if (tid == 0) {
+      st_wt(&rec->m, m);
+      st_wt(&rec->nu, nu);
+      st_wt(&rec->flags, d.flags);
+      st_wt(&rec->a1, sh.a1);
+      st_wt(&rec->a2, sh.a2);
+      st_wt(&rec->s00, sh.s00);
+      sh.pv.nu = nu;
+      sh.pv.m = m;
+      sh.pv.first = first ? 1 : 0;
+      sh.pv.a1 = sh.a1;
+      sh.pv.a2 = sh.a2;
+    }
+    for (int e = tid; e < kMaxU * kZC; e += kT) {
+      const int b = e / kZC, k = e - b * kZC;
+      st_wt(&rec->Z[b][k], sh.Z[b][k]);
+    }
+    for (int e = tid; e < kZC * kMaxU; e += kT) {
+      const int k = e / kMaxU, b = e - k * kMaxU;
+      st_wt(&rec->Y[k][b], sh.Y[k][b]);
+    }
+    if constexpr (sizeof(T) == 4) {  // fp32 Σ only: the block scatter's payload
+      for (int e = tid; e < kMaxU * kMaxU; e += kT) {
+        const int a = e / kMaxU, b = e - a * kMaxU;
+        st_wt(&rec->Pend[a][b], a < nu && b < nu ? sh.Pst[a][b] : 0.0);
+      }
+    }
+    EKF_STAMP(16);
   }
-  for (int e = tid; e < kZC * kMaxU; e += blockDim.x) {
-    const int k = e / kMaxU, b = e - k * kMaxU;
-    st_wt(&rec->Y[k][b], sh.Y[k][b]);
-  }
-  if (tid < kMaxU) {
-    const bool in = tid < nu;
-    st_wt(&rec->u[tid], sh.u[tid]);
-    st_wt(&rec->alphaU[tid], in ? sh.alphaU[tid] : 0.0);
-    st_wt(&rec->row0raw[tid], in ? sh.row0raw[tid] : 0.0);
-    st_wt(&rec->col0raw[tid], in ? sh.col0raw[tid] : 0.0);
-    st_wt(&rec->Zx[tid], sh.Zx[tid]);
-    st_wt(&rec->xU[tid], in ? xfin[tid] : 0.0);
-  }
-  if (tid == 0) {
-    st_wt(&rec->m, m);
-    st_wt(&rec->nu, nu);
-    st_wt(&rec->flags, d.flags);
-    st_wt(&rec->a1, sh.a1);
-    st_wt(&rec->a2, sh.a2);
-    st_wt(&rec->s00, sh.s00);
-  }
-  drain_stores();
+  pending = seq + 1u;
+  have_carry = true;
+  pre = pre_next;
   __syncthreads();
-  if (tid == 0) epoch_store(A.sync + kSyncChain + f, A.seq + 1u);
   EKF_STAMP(40);
+  }  // chunk loop
+  if (pending) {
+    drain_stores();
+    __syncthreads();
+    if (tid == 0) epoch_store(A.sync + kSyncChain + f, pending);
+  }
 }
 
 struct FactorShared {
@@ -1201,6 +1527,39 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles, in
   SIG_STAMP(3);
 }
 
+// After the Σ pass: its Σ_out[U, U] block replaced by the chain's fp64 values. With fp32 Σ the
+// pass's 1e7 − (1e7 − δ) at a first sighting (the reference's prior, slam.cpp:130) loses δ; the
+// chain computed it in fp64. Other entries carry no such cancellation (the prior has no cross
+// terms). fp32 only: with fp64 Σ the pass's block equals the chain's up to summation order.
+// nf_loop > 0: one workgroup walks the launch's nf_loop filters, stores write-through and then
+// publishes the Σ-pass epoch itself (small batches: one kernel instead of two behind the pass).
+template <typename T>
+__global__ __launch_bounds__(256) void k_block_scatter(PassArgs<T> A, int nf_loop) {
+  const int f_lo = nf_loop > 0 ? 0 : blockIdx.y, f_hi = nf_loop > 0 ? nf_loop : blockIdx.y + 1;
+  for (int fb = f_lo; fb < f_hi; ++fb) {
+    const MsgDesc& d = A.desc[fb];
+    if (!(d.flags & kActive)) continue;
+    const int f = A.f0 + fb;
+    const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+    const int nu = rec->nu;
+    T* Sout = A.sig[d.parity ^ 1] + f * A.sig_stride;
+    for (int e = threadIdx.x; e < nu * nu; e += blockDim.x) {
+      const int a = e / nu, b = e - a * nu;
+      const T v = static_cast<T>(rec->Pend[a][b]);
+      T* p = Sout + static_cast<size_t>(rec->u[a]) * A.ld + rec->u[b];
+      if (nf_loop > 0)
+        st_wt(p, v);
+      else
+        *p = v;
+    }
+  }
+  if (nf_loop > 0) {
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0) epoch_store(A.sync + kSyncSigma, A.seq + 1u);
+  }
+}
+
 // Σ-pass epoch for the chains on the other stream, launched right behind the Σ pass on its stream:
 // the kernel boundary's release has written the pass's Σ_out (and the factor kernel's x, Kcat,
 // Mcat) back before this store, so the pass itself keeps plain stores and no per-block release.
@@ -1393,8 +1752,9 @@ void launch(K kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t e0, hipEv
 }
 
 template <typename T>
-hipError_t launch_chain(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a);
+hipError_t launch_chain(const PassArgs<T>& a, int nf, int nchunks, hipStream_t s, hipEvent_t e0,
+                        hipEvent_t e1) {
+  launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a, nchunks);
   return hipGetLastError();
 }
 
@@ -1423,7 +1783,14 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s
     const dim3 grid(per_filter, nf);
     launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles, 0, nf);
   }
-  hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
+  if constexpr (sizeof(T) == 8) {  // fp64 Σ keeps first sightings: no block scatter
+    hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
+  } else if (nf <= 32) {  // scatter + epoch in one workgroup
+    hipLaunchKernelGGL(k_block_scatter<T>, dim3(1, 1), dim3(256), 0, s, a, nf);
+  } else {
+    hipLaunchKernelGGL(k_block_scatter<T>, dim3(1, nf), dim3(256), 0, s, a, 0);
+    hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
+  }
   return hipGetLastError();
 }
 
@@ -1447,7 +1814,8 @@ hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
 }
 
 #define EKF_INSTANTIATE(T)                                                              \
-  template hipError_t launch_chain<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t, hipEvent_t); \
+  template hipError_t launch_chain<T>(const PassArgs<T>&, int, int, hipStream_t, hipEvent_t,        \
+                                      hipEvent_t);                                                 \
   template hipError_t launch_factors<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t,          \
                                         hipEvent_t);                                               \
   template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, int, hipStream_t, hipEvent_t,  \

@@ -28,15 +28,17 @@ struct PassArgs {
   unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
   unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
   const MsgDesc* desc;
+  int desc_stride;      // descriptors between consecutive chunks of a chain launch
   int n, ld, N, f0;
   double q, r, gate;
 };
 
 // Chain kernel: the chunk's sequential corrections on the |U|×|U| block (predict folded in),
 // one workgroup per filter → ChunkRec.
+// nchunks consecutive chunks in one launch (descriptors a.desc[i·a.desc_stride + filter]).
 template <typename T>
-hipError_t launch_chain(const PassArgs<T>& a, int n_filters, hipStream_t s,
-                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t launch_chain(const PassArgs<T>& a, int n_filters, int nchunks, hipStream_t s,
+                        hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // Factor kernel: Kcat = R·Z, Mcat = Y·C on f64 MFMA and the new state. 16 rows / columns per wave.
 template <typename T>

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libekfslam.so")
+LIB_PATH = os.path.join(PKG_DIR, os.environ.get("EKF_LIB", "libekfslam.so"))
 
 EKF_OK, EKF_E_ARG, EKF_E_RANGE, EKF_E_EMPTY, EKF_E_NUMERIC, EKF_E_HIP, EKF_E_NOMEM = \
     0, -1, -2, -3, -4, -5, -6

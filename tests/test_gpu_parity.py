@@ -241,21 +241,25 @@ def _pipelined_final(sc, monkeypatch, env, dtype=pyekf.EKF_F64, F=1):
 
 
 @pytest.mark.parametrize("F", [1, 4], ids=["1filter", "4filters"])
-def test_pipelined_replay_sync_modes_bit_identical(monkeypatch, F):
-    """The device-epoch pipeline (chains on one stream, factors + Σ passes on the other, no host
-    events), the event-synchronised two-stream pipeline and the single-stream order compute the
-    same numbers: every kernel does the same arithmetic, only the synchronisation differs. Run
-    without per-message synchronisation so chunks really overlap, then against the oracle."""
+def test_pipelined_replay_sync_modes(monkeypatch, F):
+    """Three schedules of the same replay, run without per-message synchronisation so chunks
+    really overlap:
+      - event-synchronised two streams and the single-stream order launch the same kernels on
+        the same data: bit-identical;
+      - the device-epoch pipeline walks a run of chunks in ONE chain launch that carries its
+        |U|×|U| block in LDS from chunk to chunk (instead of rebuilding it from the chunk
+        record), a different summation order: equal to rounding (1e-9),
+    and all against the oracle."""
     sc = synth.synthetic(256, 30)
     dev = _pipelined_final(sc, monkeypatch, {}, F=F)
     evt = _pipelined_final(sc, monkeypatch, {"EKF_DEVSYNC": "0"}, F=F)
     ser = _pipelined_final(sc, monkeypatch, {"EKF_SERIAL": "1"}, F=F)
     for (xd, Sd, cd), (xe, Se, ce), (xs, Ss, cs) in zip(dev, evt, ser):
         assert cd == ce == cs
-        np.testing.assert_array_equal(xd, xs)
-        np.testing.assert_array_equal(Sd, Ss)
         np.testing.assert_array_equal(xe, xs)
         np.testing.assert_array_equal(Se, Ss)
+        assert np.abs(xd - xs).max() < 1e-9
+        assert np.abs(Sd - Ss).max() < 1e-9
     o = orc.run_scenario(sc, False)
     x, S, _ = dev[0]
     assert np.abs(x - o["state"]).max() < 1e-7
@@ -263,7 +267,8 @@ def test_pipelined_replay_sync_modes_bit_identical(monkeypatch, F):
 
 
 def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
-    """Config 3 size, fp32 Σ, 24 messages pipelined: device-epoch vs single-stream bit-identical."""
+    """Config 3 size, fp32 Σ, 24 messages pipelined: device-epoch (carried block) vs single
+    stream (rebuilt block) agree to fp32 rounding of the stored Σ."""
     N, warm, T = 1024, 40, 24
     sc = synth.synthetic(N, warm + T)
     odom = pyekf.odometry(sc)
@@ -286,16 +291,23 @@ def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
                  actions=sc.actions[sl, None])
         res.append(e.state())
         e.close()
-    np.testing.assert_array_equal(res[0][0], res[1][0])
-    np.testing.assert_array_equal(res[0][1], res[1][1])
-    assert np.all(np.isfinite(res[0][1]))
+    assert np.abs(res[0][0] - res[1][0]).max() < 1e-5
+    S0, S1 = res[0][1], res[1][1]
+    assert np.all(np.isfinite(S0))
+    seen = np.abs(np.diag(S1)) < 1e6  # landmarks seen (fp32 Σ entries ~1e-2 .. 1)
+    blk = np.ix_(seen, seen)
+    assert np.abs(S0[blk] - S1[blk]).max() < 1e-5
 
 
 @pytest.mark.parametrize("F", [24, 40], ids=["24filters_devsync", "40filters_events"])
-def test_many_filters_match_small_batch(F):
+def test_many_filters_match_small_batch(F, monkeypatch):
     """≥16 filters take the XCD-aware Σ-pass grid, > 32 filters the event-synchronised streams;
     filter f replays scenario f % 8, and must equal the same scenario in an 8-filter handle bit for
-    bit (the arithmetic per filter does not depend on the batch)."""
+    bit when both run the same schedule (the arithmetic per filter does not depend on the batch):
+    24 filters and 8 filters both on the device-epoch pipeline; 40 filters (events) against 8
+    filters with EKF_DEVSYNC=0."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+        monkeypatch.delenv(k, raising=False)
     N, T = 64, 12
     scs = [synth.synthetic(N, T, seed=100 + k) for k in range(8)]
     odo = [pyekf.odometry(s) for s in scs]
@@ -321,7 +333,10 @@ def test_many_filters_match_small_batch(F):
         e.close()
         return out
 
-    small, big = run(8), run(F)
+    big = run(F)
+    if F > 32:
+        monkeypatch.setenv("EKF_DEVSYNC", "0")
+    small = run(8)
     for f in range(F):
         xs, Ss, cs = small[f % 8]
         xb, Sb, cb = big[f]

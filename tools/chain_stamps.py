@@ -1,0 +1,40 @@
+"""Dev tool: phase stamps (s_memtime cycles) of the chain kernel's last chunk, filter 0, in the
+pipelined replay (libekfslam_diag.so; build: make -C ekf-slam_amd diag)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+os.environ["EKF_LIB"] = "libekfslam_diag.so"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ekf-slam_amd"))
+import pyekf  # noqa: E402
+from pyekf import synth  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+T = 40
+sc = synth.synthetic(N, T)
+odom = pyekf.odometry(sc)
+e = pyekf.EKF(n_landmarks=N)
+e.replay(sc.count[:, None], sc.rel[:, None], odom[:, None], ids=sc.ids[:, None],
+         actions=sc.actions[:, None])
+e.sync()
+L = pyekf.lib()
+st = (C.c_ulonglong * 160)()
+L.ekf_diag_stamps.argtypes = [C.c_void_p, C.c_int]
+assert L.ekf_diag_stamps(st, 160) == 0
+s = np.array(st[:], dtype=np.int64)
+t0 = s[0]
+names = {1: "A0", 8: "carry:pos", 9: "carry:gather", 10: "carry:K'M'", 11: "carry:P,x", 6: "A1 done",
+         2: "predict (steps start)", 12: "steps+final pass", 16: "epi: rec stores issued", 40: "carry copies"}
+for k in (1, 8, 9, 10, 11, 6, 2, 12, 16, 40):
+    print(f"{names[k]:24s} {s[k] - t0:8d}")
+m = int(sc.count[-1])
+steps = [s[64 + 6 * c] - t0 for c in range(m)]
+print("step starts:", steps)
+for c in (0, m // 2, m - 1):
+    b = 64 + 6 * c
+    print(f"step {c}: range_bearing {s[b+1]-s[b]}  S,inv {s[b+2]-s[b+1]}  K,M,x,publish {s[b+3]-s[b+2]}"
+          f"  Bx reads {s[b+4]-s[b+3]}  cross update {s[b+5]-s[b+4]}  -> next {s[b+6]-s[b+5] if c+1<m else 0}")
+e.close()

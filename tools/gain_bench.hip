@@ -68,11 +68,11 @@ void run(int N, int m, int reps) {
   a.sig[0] = dS[0]; a.sig[1] = dS[1]; a.sig_stride = 0;
   a.x[0] = dx[0]; a.x[1] = dx[1]; a.x_stride = 0;
   a.kcat = kc; a.mcat = mc; a.km_stride = 0; a.ldk = ldk;
-  a.ctl = ctl; a.sync = sync_buf(4096); a.rec = rec; a.rec_stride = 1; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0;
+  a.ctl = ctl; a.sync = sync_buf(4096); a.desc_stride = 1; a.rec = rec; a.rec_stride = 1; a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0;
   a.q = 1e-2; a.r = 1e-2; a.gate = 2.0;
   hipStream_t s;
   CK(hipStreamCreate(&s));
-  CK(launch_chain<T>(a, 1, s));
+  CK(launch_chain<T>(a, 1, 1, s));
   CK(hipStreamSynchronize(s));
   if (g_look) {
     d.parity = 0;
@@ -81,13 +81,13 @@ void run(int N, int m, int reps) {
     for (int c = 0; c < m; ++c) d.prev_ids[c] = d.ids[c];
     CK(hipMemcpy(dd, &d, sizeof(MsgDesc), hipMemcpyHostToDevice));
   }
-  for (int i = 0; i < 5; ++i) CK(launch_chain<T>(a, 1, s));
+  for (int i = 0; i < 5; ++i) CK(launch_chain<T>(a, 1, 1, s));
   CK(hipStreamSynchronize(s));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, s));
-  for (int i = 0; i < reps; ++i) CK(launch_chain<T>(a, 1, s));
+  for (int i = 0; i < reps; ++i) CK(launch_chain<T>(a, 1, 1, s));
   CK(hipEventRecord(e1, s));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -111,6 +111,30 @@ void run(int N, int m, int reps) {
   }
   printf("\n    prologue stamps (cycles from 0): A0 %llu loads+transform %llu K'M'-tiles %llu +x %llu P %llu\n",
          st[1] - st[0], st[3] - st[0], st[7] - st[0], st[5] - st[0], st[6] - st[0]);
+  if (g_look == 2) {  // one launch walking C chunks (carry path), same markers every chunk
+    const int C = 8;
+    std::vector<MsgDesc> dv(C, d);
+    for (int i = 0; i < C; ++i) {
+      dv[i].parity = i & 1;
+      dv[i].flags = (d.flags & ~kLook) | kLook;
+    }
+    MsgDesc* dm;
+    CK(hipMalloc(&dm, C * sizeof(MsgDesc)));
+    CK(hipMemcpy(dm, dv.data(), C * sizeof(MsgDesc), hipMemcpyHostToDevice));
+    unsigned big = 0x40000000u;  // every Σ-pass epoch poll passes at once
+    CK(hipMemcpy(a.sync + kSyncSigma, &big, sizeof(unsigned), hipMemcpyHostToDevice));
+    PassArgs<T> ac = a;
+    ac.desc = dm;
+    CK(launch_chain<T>(ac, 1, C, s));
+    CK(hipStreamSynchronize(s));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < reps / C; ++i) CK(launch_chain<T>(ac, 1, C, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("    carry: %.2f us/chunk (launches of %d chunks)\n", ms * 1e3 / (reps / C * C), C);
+    CK(hipFree(dm));
+  }
   CK(hipEventRecord(e0, s));
   for (int i = 0; i < reps; ++i) CK(launch_factors<T>(a, 1, s));
   CK(hipEventRecord(e1, s));
