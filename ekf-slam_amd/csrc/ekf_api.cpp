@@ -216,13 +216,18 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, b
     PassArgs<T> ai = a;
     ai.desc = dptr + static_cast<size_t>(i) * nf;
     ai.seq = s0 + static_cast<unsigned>(i);
+    // Inside a device-synchronised group the factor kernel of chunk i publishes the Σ-pass epoch
+    // of chunk i−1 (the kernel boundary has made that pass's output visible): one launch less per
+    // chunk on the bulk stream. The group's last pass gets its own epoch kernel.
+    const bool in_group = h->devsync && nchunks > 1;
+    ai.pub_sigma = in_group && i > 0 ? ai.seq : 0u;
     // factors gather the materialised Σ_in (the previous Σ pass, same stream) and the record
     rc = timed(h, 3, bs, [&](hipEvent_t e0, hipEvent_t e1) {
       return launch_factors<T>(ai, nf, bs, e0, e1);
     });
     if (rc) return rc;
     rc = timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
-      return launch_sigma_pass<T>(ai, nf, 0, bs, e0, e1);
+      return launch_sigma_pass<T>(ai, nf, !(in_group && i + 1 < nchunks), bs, e0, e1);
     });
     if (rc) return rc;
     if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[(s0 + i) & 1], bs));

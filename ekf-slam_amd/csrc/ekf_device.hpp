@@ -7,6 +7,7 @@
 //   Kcat,Mcat : KW × ldk low-rank factors of one chunk: Σ_out = Σ_in + Q − Kcatᵀ·Mcat.
 //   FilterCtl : t_map_odom, counter_obstacles, status, association results.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 
 namespace ekfslam {
@@ -71,5 +72,9 @@ struct alignas(16) ChunkRec {
   double Pend[kMaxU][kMaxU];         // the chain's final Σ[U, U] (fp64): written over the Σ pass's
                                      // block so fp32 Σ keeps first sightings (1e7 − (1e7 − δ))
 };
+// the chain stores Z, Y and Pend in 16-byte pairs
+static_assert(offsetof(ChunkRec, Z) % 16 == 0 && offsetof(ChunkRec, Y) % 16 == 0 &&
+                  offsetof(ChunkRec, Pend) % 16 == 0 && sizeof(ChunkRec) % 16 == 0,
+              "ChunkRec payload 16-byte aligned");
 
 }  // namespace ekfslam

@@ -32,13 +32,21 @@ namespace ekfslam {
 
 // Diagnostic build only (tools/gain_bench.hip): s_memtime stamps of block (0,0), thread 0.
 #ifdef EKF_DIAG_STAMPS
-__device__ unsigned long long g_stamps[160];
+__device__ unsigned long long g_stamps[256];
 #define EKF_STAMP(i)                                                              \
   do {                                                                            \
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                   \
       g_stamps[i] = __builtin_amdgcn_s_memtime();                                 \
   } while (0)
+#define EKF_STAMPT(i, t)                                                          \
+  do {                                                                            \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == (t))                 \
+      g_stamps[i] = __builtin_amdgcn_s_memtime();                                 \
+  } while (0)
 #else
+#define EKF_STAMPT(i, t) \
+  do {                   \
+  } while (0)
 #define EKF_STAMP(i) \
   do {               \
   } while (0)
@@ -47,7 +55,7 @@ __device__ unsigned long long g_stamps[160];
 }  // namespace ekfslam
 extern "C" int ekfslam_diag_read_stamps(unsigned long long* out, int n) {
   using ekfslam::g_stamps;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < 160 ? n : 160)) == hipSuccess ? 0 : -5;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < 256 ? n : 256)) == hipSuccess ? 0 : -5;
 }
 namespace ekfslam {
 #endif
@@ -120,13 +128,17 @@ __device__ __forceinline__ double rsq_refined(double x) {
 
 // Range-bearing model for landmark at (lx, ly) seen from pose: ẑ and the 2×5 H over
 // {θ, x, y, jx, jy} (slam.cpp:219-249).
+// bear_raw / bear_ok: the bearing before normalisation and whether the branch-free normalisation
+// applied (|θ| ≤ π keeps it so); when not, the caller sets zhat[1] = normalize_angle(bear_raw).
 __device__ __forceinline__ void range_bearing(const double* pose, double lx, double ly,
-                                              double* zhat, double* H0, double* H1) {
+                                              double* zhat, double* H0, double* H1,
+                                              double* bear_raw, bool* bear_ok) {
   const double ex = lx - pose[1], ey = ly - pose[2];
   const double d = ex * ex + ey * ey;
   const double isd = rsq_refined(d), id = isd * isd;
   zhat[0] = d * isd;
-  zhat[1] = normalize_angle(atan2_fast(ey, ex) - pose[0]);
+  *bear_raw = atan2_fast(ey, ex) - pose[0];
+  zhat[1] = normalize_angle_near(*bear_raw, bear_ok);
   H0[0] = 0.0;
   H0[1] = -ex * isd;
   H0[2] = -ey * isd;
@@ -200,6 +212,8 @@ struct ChainShared {
     double xg[kMaxU];             // x_in'[u] for this chunk's U (rows the previous chunk missed)
   } pv;
   double Pst[kMaxU][kMaxU + 1];  // carry: the previous chunk's final Σ[U', U'] (its U' order)
+  double junk[4][64];             // per-wave sink of masked-off LDS stores (no divergent branch)
+  double junk2[64][2];
   double pose[3];
   double npose[3], na1, na2;  // the next chunk's predicted pose and A entries (its prefetch)
   double xpose[3];  // x_in pose (posterior of the previous chunk)
@@ -255,14 +269,23 @@ __device__ __forceinline__ void st_wt(double* p, double v) {
 __device__ __forceinline__ void st_wt(float* p, float v) {
   __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16-byte write-through store (buffer store, cache policy sc1) at byte offset `off` of `r`
+__device__ __forceinline__ void st_wt2(__amdgpu_buffer_rsrc_t r, int off, double a, double b) {
+  typedef int i4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4, make_double2(a, b)), r, off, 0, 16);
+}
 __device__ __forceinline__ void st_wt(int* p, int v) {
   __hip_atomic_store((gu32*)p, static_cast<unsigned>(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Intra-workgroup hand-off through LDS (waves on different SIMDs; no s_barrier).
+// The LDS executes one wave's accesses in issue order, so a flag stored after the data is seen
+// after it by any wave: no s_waitcnt before the flag (a release would drain every LDS op of the
+// wave first), only a compiler fence that keeps the data stores ahead of it.
 __device__ __forceinline__ void lds_publish(int* flag, int v) {
-  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
   while (__builtin_amdgcn_readfirstlane(
@@ -421,6 +444,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         vr[i] = sh.Pst[0][pb];
         vc[i] = sh.Pst[pa][0];
       }
+      EKF_STAMP(17);
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
         const int e = tid + i * kChainThreads;
@@ -434,6 +458,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
         if (a < nu && b < nu) sh.P[0][a][b] = v;
       }
+      EKF_STAMP(18);
       if (tid < nu) {
         const int pos = d.cpos[tid];
         sh.xU[0][tid] = tid < 3 ? sh.npose[tid] : sh.pv.xU[pos];
@@ -876,25 +901,44 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       pk[a] = sh.P[0][lr][col];
       pm[a] = sh.P[0][col][lr];
     }
-    for (int c = 0; c < m; ++c) {
-      const int pj = 3 + 2 * c, nx = pj + 2;
-      const bool more = c + 1 < m;
-      EKF_STAMP(64 + 6 * c);
-      const double z0 = d.z[c][0], z1 = d.z[c][1];
-      bool sk = sh.skip[c] != 0;
-      const double* xc = sh.xU[0];  // written by this wave at the end of the previous step
-      const double pose[3] = {xc[0], xc[1], xc[2]};
-      double lx = xc[pj], ly = xc[pj + 1];
-      bool init = false;
-      if (!sk && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
+    // Look-ahead operands of the next marker's cross (see the step): rn = Σ[ℓ, nx..nx+1] and
+    // qn = Σ[nx..nx+1, ℓ] one step old, and the previous step's K (kp) and M (mp) of this lane.
+    double rn[2], qn[2], kp0 = 0.0, kp1 = 0.0, mp0 = 0.0, mp1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = min(5 + j, kMaxU - 1);
+      rn[j] = sh.P[0][lr][col];
+      qn[j] = sh.P[0][col][lr];
+    }
+    // A step's geometry (first sighting, ẑ, H) needs only x after the step before. It is computed
+    // right after that step's state update, ahead of the step's cross update, so the two
+    // independent chains (f64 ALU vs LDS round trips) interleave in one basic block.
+    double lx = 0.0, ly = 0.0, H0[5], H1[5], zhat[2], braw = 0.0;
+    bool init = false, bok = true;
+    auto geometry = [&](int c) {
+      const int pj = 3 + 2 * c;
+      const double pose[3] = {readlane_f64(xl, 0), readlane_f64(xl, 1), readlane_f64(xl, 2)};
+      lx = readlane_f64(xl, pj);
+      ly = readlane_f64(xl, pj + 1);
+      init = false;
+      if (!sh.skip[c] && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
         init = true;
+        const double z0 = d.z[c][0], z1 = d.z[c][1];
         lx = pose[1] + z0 * cos(z1 + pose[0]);
         ly = pose[2] + z0 * sin(z1 + pose[0]);
       }
-      double H0[5], H1[5], Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
-      double zhat[2];
-      range_bearing(pose, lx, ly, zhat, H0, H1);
-      EKF_STAMP(65 + 6 * c);
+      range_bearing(pose, lx, ly, zhat, H0, H1, &braw, &bok);
+    };
+    if (m > 0) geometry(0);
+    for (int c = 0; c < m; ++c) {
+      const int pj = 3 + 2 * c, nx = pj + 2;
+      const bool more = c + 1 < m;
+      EKF_STAMP(64 + 8 * c);
+      const double z0 = d.z[c][0], z1 = d.z[c][1];
+      bool sk = sh.skip[c] != 0;
+      double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
+      if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
+      EKF_STAMP(65 + 8 * c);
       // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]
       double ka = 0.0, kb = 0.0, mm0 = 0.0, mm1 = 0.0;
 #pragma unroll
@@ -919,7 +963,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         Sm[3] += A.r;
         if (!sk && inv2(Sm, Si)) {
           nv0 = z0 - zhat[0];
-          nv1 = normalize_angle(z1 - zhat[1]);
+          bool nok;
+          const double nn = normalize_angle_near(z1 - zhat[1], &nok);
+          nv1 = nok ? nn : normalize_angle(z1 - zhat[1]);
         } else {
           if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every lane
           sk = true;
@@ -932,19 +978,42 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         nv0 = nv1 = 0.0;
         ka = kb = mm0 = mm1 = 0.0;
       }
-      // the next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}): wave 3 must have applied
-      // step c−1 outside this step's cross first
-      const int bx = more ? nx : pj;  // last step: any in-bounds columns, unused
+      // The next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}) after step c−1. Pose columns /
+      // rows: pk / pm (pA ⊃ pose). The nx columns / rows were read one step back (rn / qn, after
+      // step c−2) and get step c−1's rank-2 term here from registers: K_{c−1} of this lane (kp)
+      // and of the nx rows (v_readlane), M_{c−1} of this column (mp) and of the nx columns
+      // (v_readlane) — the writers' expression, operands and order (wave 3's, or this wave's cross
+      // update), so the same bits. Step 0 has kp = mp = 0: rank2_sub(v, 0, 0, 0, 0) = v.
       double xr[5], xq[5];
-      if (more) lds_wait_ge(&sh.pdone, c);
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const int col = k < 3 ? k : bx + k - 3;
-        xr[k] = sh.P[0][lr][col];
-        xq[k] = sh.P[0][col][lr];
+      for (int k = 0; k < 3; ++k) {
+        xr[k] = pk[k];
+        xq[k] = pm[k];
+      }
+      {
+        const int l0 = more ? nx : 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const double mq0 = readlane_f64(mp0, l0 + j), mq1 = readlane_f64(mp1, l0 + j);
+          const double kq0 = readlane_f64(kp0, l0 + j), kq1 = readlane_f64(kp1, l0 + j);
+          xr[3 + j] = rank2_sub(rn[j], kp0, kp1, mq0, mq1);
+          xq[3 + j] = rank2_sub(qn[j], kq0, kq1, mp0, mp1);
+        }
+      }
+      EKF_STAMP(66 + 8 * c);
+      // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's
+      // cross, before this step's cross update writes its Bx rows (wave 3 writes these entries for
+      // step c only after the publish below, whose release waits for the reads)
+      if (c + 2 < m) {
+        lds_wait_ge(&sh.pdone, c);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          rn[j] = sh.P[0][lr][nx + 2 + j];
+          qn[j] = sh.P[0][nx + 2 + j][lr];
+        }
       }
       const int jx = sh.u[pj];
-      EKF_STAMP(66 + 6 * c);
+      EKF_STAMP(67 + 8 * c);
       const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
       const double K1 = ka * Si[1] + kb * Si[3];
       {
@@ -954,16 +1023,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           else if (ul == jx + 1) xt = ly;
         }
         xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
-        if (lane == 0) xt = normalize_angle(xt);     // slam.cpp:267
+        bool tok;                                     // slam.cpp:267 on lane 0, branch-free
+        const double tn = normalize_angle_near(xt, &tok);
+        if (lane == 0) xt = tok ? tn : normalize_angle(xt);
         xl = xt;
-        if (lane < nu) sh.xU[0][lane] = xt;
+        *(lane < nu ? &sh.xU[0][lane] : &sh.junk[0][lane]) = xt;
       }
-      if (lane < kMaxU) {
-        const bool in = lane < nu;
-        sh.KU[c][lane][0] = in ? K0 : 0.0;
-        sh.KU[c][lane][1] = in ? K1 : 0.0;
-        sh.MU[c][lane][0] = in ? mm0 : 0.0;
-        sh.MU[c][lane][1] = in ? mm1 : 0.0;
+      {
+        const bool in = lane < nu, st = lane < kMaxU;
+        double* kd = st ? &sh.KU[c][lane][0] : &sh.junk2[lane][0];
+        double* md = st ? &sh.MU[c][lane][0] : &sh.junk2[lane][0];
+        kd[0] = in ? K0 : 0.0;
+        kd[1] = in ? K1 : 0.0;
+        md[0] = in ? mm0 : 0.0;
+        md[1] = in ? mm1 : 0.0;
       }
       if (lane == 0) {
 #pragma unroll
@@ -976,26 +1049,29 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         sh.nu[c][0] = nv0;
         sh.nu[c][1] = nv1;
       }
-      lds_publish(&sh.pub, c + 1);  // drains this wave's LDS writes first
-      EKF_STAMP(67 + 6 * c);
+      lds_publish(&sh.pub, c + 1);
+      EKF_STAMP(68 + 8 * c);
       if (more) {
+        geometry(c + 1);
+        // wave 3's step c−1 writes outside this step's cross must land before this cross update
+        // overwrites the nx columns / rows (waited for above already when c + 2 < m)
+        if (c + 2 >= m) lds_wait_ge(&sh.pdone, c);
         // K and M of the five Bx rows / columns, from their lanes
         double kx0[5], kx1[5], mx0[5], mx1[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
           const int l = k < 3 ? k : nx + k - 3;
-          kx0[k] = sh.KU[c][l][0];
-          kx1[k] = sh.KU[c][l][1];
-          mx0[k] = sh.MU[c][l][0];
-          mx1[k] = sh.MU[c][l][1];
+          kx0[k] = readlane_f64(K0, l);
+          kx1[k] = readlane_f64(K1, l);
+          mx0[k] = readlane_f64(mm0, l);
+          mx1[k] = readlane_f64(mm1, l);
         }
-        EKF_STAMP(68 + 6 * c);
         // all rows × Bx columns: next step's pk
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
           const int col = k < 3 ? k : nx + k - 3;
           pk[k] = rank2_sub(xr[k], K0, K1, mx0[k], mx1[k]);
-          if (lane < nu) sh.P[0][lane][col] = pk[k];
+          *(lane < nu ? &sh.P[0][lane][col] : &sh.junk[0][lane]) = pk[k];
         }
         // Bx rows × every other column (the block is kept whole so that the chunk's final Σ[U,U]
         // can seed the next chunk): next step's pm there
@@ -1005,19 +1081,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           const int row = k < 3 ? k : nx + k - 3;
           const double v = rank2_sub(xq[k], kx0[k], kx1[k], mm0, mm1);
           pm[k] = v;
-          if (later) sh.P[0][row][lane] = v;
+          *(later ? &sh.P[0][row][lane] : &sh.junk[0][lane]) = v;
         }
-        // pm of the Bx columns themselves (and pose): entries another lane just wrote
-        const bool own = lane < 3 || lane == nx || lane == nx + 1;
-        if (own) {  // LDS executes one wave's accesses in order: the reads see the writes above
-#pragma unroll
-          for (int k = 0; k < 5; ++k) {
-            const int row = k < 3 ? k : nx + k - 3;
-            pm[k] = sh.P[0][row][lane];
-          }
-        }
+        // (the Bx × Bx entries: lane `row` stored the same value as its pk, same operands)
+        kp0 = K0;
+        kp1 = K1;
+        mp0 = mm0;
+        mp1 = mm1;
       }
-      EKF_STAMP(69 + 6 * c);
+      EKF_STAMP(70 + 8 * c);
     }
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
     // lane → column 3+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
@@ -1025,6 +1097,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const int b = min(3 + hb, kMaxU - 1);
     for (int c = 0; c + 1 < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
+      EKF_STAMPT(192 + 2 * c, 192);
       const int nx = 5 + 2 * c;
       const bool colok = 3 + hb < nu && b != nx && b != nx + 1;
       const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
@@ -1036,15 +1109,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         k0[i] = sh.KU[c][a][0];
         k1[i] = sh.KU[c][a][1];
       }
-      if (colok) {
+      // every lane stores every row (masked-off entries to its junk slot): no divergent branches,
+      // so the reads above are waited for once, not once per predicated store
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int a = 3 + hr + 2 * i;
-          if (a < nu && a != nx && a != nx + 1)
-            sh.P[0][a][b] = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
-        }
+      for (int i = 0; i < 16; ++i) {
+        const int a = 3 + hr + 2 * i;
+        const bool ok = colok && a < nu && a != nx && a != nx + 1;
+        *(ok ? &sh.P[0][a][b] : &sh.junk[3][lane]) = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
       }
       lds_publish(&sh.pdone, c + 1);
+      EKF_STAMPT(193 + 2 * c, 192);
     }
   } else if (wave == 1) {  // Z_c and Φ (live columns)
     const int hb = lane & 31, hr = lane >> 5;
@@ -1218,19 +1292,28 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       sh.pv.a1 = sh.a1;
       sh.pv.a2 = sh.a2;
     }
-    for (int e = tid; e < kMaxU * kZC; e += kT) {
-      const int b = e / kZC, k = e - b * kZC;
-      st_wt(&rec->Z[b][k], sh.Z[b][k]);
+    // Z, Y (and Pend) in 16-byte write-through stores: half the store instructions of 8-byte
+    // ones, and the issue of write-through stores is what this phase waits on
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
+    constexpr int oZ = static_cast<int>(offsetof(ChunkRec, Z)), oY = static_cast<int>(offsetof(ChunkRec, Y));
+    for (int e = tid; e < kMaxU * kZC / 2; e += kT) {
+      const int b = e / (kZC / 2), k = 2 * (e - b * (kZC / 2));
+      st_wt2(rr, oZ + 16 * e, sh.Z[b][k], sh.Z[b][k + 1]);
     }
-    for (int e = tid; e < kZC * kMaxU; e += kT) {
-      const int k = e / kMaxU, b = e - k * kMaxU;
-      st_wt(&rec->Y[k][b], sh.Y[k][b]);
+    for (int e = tid; e < kZC * kMaxU / 2; e += kT) {
+      const int e0 = 2 * e, e1 = e0 + 1;
+      const int k0 = e0 / kMaxU, b0 = e0 - k0 * kMaxU, k1 = e1 / kMaxU, b1 = e1 - k1 * kMaxU;
+      st_wt2(rr, oY + 16 * e, sh.Y[k0][b0], sh.Y[k1][b1]);
     }
-    if constexpr (sizeof(T) == 4) {  // fp32 Σ only: the block scatter's payload
-      for (int e = tid; e < kMaxU * kMaxU; e += kT) {
-        const int a = e / kMaxU, b = e - a * kMaxU;
-        st_wt(&rec->Pend[a][b], a < nu && b < nu ? sh.Pst[a][b] : 0.0);
+    if constexpr (sizeof(T) == 4) {  // fp32 Σ only: the Σ pass's payload for the U × U block
+      constexpr int oP = static_cast<int>(offsetof(ChunkRec, Pend));
+      for (int e = tid; e < kMaxU * kMaxU / 2; e += kT) {
+        const int e0 = 2 * e, e1 = e0 + 1;
+        const int a0 = e0 / kMaxU, b0 = e0 - a0 * kMaxU, a1 = e1 / kMaxU, b1 = e1 - a1 * kMaxU;
+        st_wt2(rr, oP + 16 * e, sh.Pst[a0][b0], sh.Pst[a1][b1]);
       }
+      if (tid == kT - 1) st_wt(&rec->Pend[kMaxU - 1][kMaxU - 1], sh.Pst[kMaxU - 1][kMaxU - 1]);
     }
     EKF_STAMP(16);
   }
@@ -1254,6 +1337,7 @@ struct FactorShared {
   double Y[kZC][kMaxU + 1];
   double a1, a2, s00;
   int nu;
+  int pos64[64];  // row waves: position in U of each of the workgroup's 64 rows (≥ nu: none)
 };
 
 // Kcat = R_pred·Z (rows) and Mcat = Y·C_pred (columns) on f64 MFMA, plus the new state.
@@ -1261,6 +1345,9 @@ struct FactorShared {
 template <typename T>
 __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
   __shared__ FactorShared sh;
+  // the previous chunk's Σ pass ended before this launch (same stream): its epoch, for the chains
+  if (A.pub_sigma && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    epoch_store(A.sync + kSyncSigma, A.pub_sigma);
   const MsgDesc& d = A.desc[blockIdx.y];
   if (!(d.flags & kActive)) return;
   const int f = A.f0 + blockIdx.y;
@@ -1274,20 +1361,35 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
   const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
   const bool first = (d.flags & kFirst) != 0;
   // the chain of this chunk runs on the other stream: wait for its record
+  if (tid < 64) sh.pos64[tid] = kMaxU;
   if (tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
     atomicOr(&A.ctl[f].status, EKF_FLAG_TIMEOUT_D);
   drain_stores();
   __syncthreads();
-  for (int e = tid; e < kMaxU * kZC; e += blockDim.x) {
-    const int b = e / kZC, k = e - b * kZC;
-    sh.Z[b][k] = rec->Z[b][k];
-  }
-  for (int e = tid; e < kZC * kMaxU; e += blockDim.x) {
-    const int k = e / kMaxU, b = e - k * kMaxU;
-    sh.Y[k][b] = rec->Y[k][b];
+  {  // the record into LDS: every load of a thread issued before its first LDS store
+    constexpr int kPer = (kMaxU * kZC + 255) / 256;  // 5
+    double vz[kPer], vy[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = min(tid + 256 * i, kMaxU * kZC - 1);
+      vz[i] = (&rec->Z[0][0])[e];
+      vy[i] = (&rec->Y[0][0])[e];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i;
+      if (e < kMaxU * kZC) {
+        const int b = e / kZC, k = e - b * kZC;
+        sh.Z[b][k] = vz[i];
+        const int k2 = e / kMaxU, b2 = e - k2 * kMaxU;
+        sh.Y[k2][b2] = vy[i];
+      }
+    }
   }
   if (tid < kMaxU) {
-    sh.u[tid] = rec->u[tid];
+    const int ub = rec->u[tid], rnu = rec->nu, rbase = blockIdx.x * 64;
+    sh.u[tid] = ub;
+    if (tid < rnu && ub >= rbase && ub < rbase + 64) atomicMin(&sh.pos64[ub - rbase], tid);
     sh.alphaU[tid] = rec->alphaU[tid];
     sh.row0raw[tid] = rec->row0raw[tid];
     sh.col0raw[tid] = rec->col0raw[tid];
@@ -1315,13 +1417,19 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
     const int i = R0 + l16;
     const bool vi = i < n;
     const T* rowp = S + static_cast<size_t>(vi ? i : 0) * ld;
-    const double r0raw = vi ? static_cast<double>(rowp[0]) : 0.0;
+    // every gather issued unconditionally (clamped index; padding u = 0 stays in bounds), then
+    // masked: a predicated load would be a branch with its own wait, one round trip per load
+    T raw[9];
+    const T r0t = rowp[0];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) raw[s] = rowp[sh.u[min(4 * s + ks, kMaxU - 1)]];
+    const double r0raw = vi ? static_cast<double>(r0t) : 0.0;
     const double ai = first ? alpha_of(i, sh.a1, sh.a2) : 0.0;
     double av[9];
 #pragma unroll
     for (int s = 0; s < 9; ++s) {
       const int k = 4 * s + ks;
-      double v = (vi && k < nu) ? static_cast<double>(rowp[sh.u[k]]) : 0.0;
+      double v = (vi && k < nu) ? static_cast<double>(raw[s]) : 0.0;
       if (first && vi && k < nu) {
         v = v + ai * sh.row0raw[k];
         v = v + (r0raw + ai * s00) * sh.alphaU[k];
@@ -1340,6 +1448,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
       acc1 = mfma_f64(av[s], z1, acc1);
       acc2 = mfma_f64(av[s], zx, acc2);
     }
+    const int rbase = blockIdx.x * 64;
     if (vi && ks == 0) {  // the predict's two rank-1 factors (slam.cpp:198)
       kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
       kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
@@ -1350,11 +1459,9 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
       if (row < n) {
         kc[(2 + l16) * ldk + row] = static_cast<T>(acc0[r]);
         kc[(18 + l16) * ldk + row] = static_cast<T>(acc1[r]);
-        if (l16 == 0) {
-          int pos = -1;
-          for (int b = nu - 1; b >= 0; --b)
-            if (sh.u[b] == row) pos = b;
-          xout[row] = pos >= 0 ? xfin[pos] : xin[row] + acc2[r];
+        if (l16 == 0) {  // rows of U take the chain's x (first position of the row in U)
+          const int pos = sh.pos64[row - rbase];
+          xout[row] = pos < nu ? xfin[pos] : xin[row] + acc2[r];
         }
       }
     }
@@ -1363,13 +1470,18 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
     const int j = C0 + l16;
     const bool vj = j < n;
     const int jj = vj ? j : 0;
-    const double c0raw = vj ? static_cast<double>(S[jj]) : 0.0;
+    T raw[9];
+    const T c0t = S[jj];
+#pragma unroll
+    for (int s = 0; s < 9; ++s)
+      raw[s] = S[static_cast<size_t>(sh.u[min(4 * s + ks, kMaxU - 1)]) * ld + jj];
+    const double c0raw = vj ? static_cast<double>(c0t) : 0.0;
     const double aj = first ? alpha_of(j, sh.a1, sh.a2) : 0.0;
     double bv[9];
 #pragma unroll
     for (int s = 0; s < 9; ++s) {
       const int k = 4 * s + ks;
-      double v = (vj && k < nu) ? static_cast<double>(S[static_cast<size_t>(sh.u[k]) * ld + jj]) : 0.0;
+      double v = (vj && k < nu) ? static_cast<double>(raw[s]) : 0.0;
       if (first && vj && k < nu) {
         v = v + sh.alphaU[k] * c0raw;
         v = v + (sh.col0raw[k] + sh.alphaU[k] * s00) * aj;
@@ -1418,7 +1530,8 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ void sigma_tile(const double* Sin, double* Sout, const double* kc,
                                            const double* mc, int n, int ld, int ldk, int kw,
-                                           bool first, double q, int R0, int C0, int lane) {
+                                           bool first, double q, int R0, int C0, int lane,
+                                           const ChunkRec*, int*) {
   const int kr = lane >> 4, kcol = lane & 15;
   double a[2][9], b[2][9];
 #pragma unroll
@@ -1465,11 +1578,17 @@ __device__ __forceinline__ void sigma_tile(const double* Sin, double* Sout, cons
       }
 }
 
+// fp32 also takes the chain's fp64 Σ[U, U] (rec->Pend) over the pass's own values there: the
+// pass's 1e7 − (1e7 − δ) at a first sighting (the reference's prior, slam.cpp:130) loses δ in
+// fp32; the chain computed it in fp64. Other entries carry no such cancellation (the prior has no
+// cross terms). spos: this wave's 64 LDS words (positions in U of its 32 rows and 32 columns).
 __device__ __forceinline__ void sigma_tile(const float* Sin, float* Sout, const float* kc,
                                            const float* mc, int n, int ld, int ldk, int kw,
-                                           bool first, double qd, int R0, int C0, int lane) {
+                                           bool first, double qd, int R0, int C0, int lane,
+                                           const ChunkRec* rec, int* spos) {
   const int kr = lane >> 5, kcol = lane & 31;
   const float q = static_cast<float>(qd);
+  const int ub = rec->u[min(lane, kMaxU - 1)], rnu = rec->nu;
   float a[18], b[18];
 #pragma unroll
   for (int s = 0; s < 18; ++s) {
@@ -1489,11 +1608,26 @@ __device__ __forceinline__ void sigma_tile(const float* Sin, float* Sout, const 
   for (int s = 0; s < 18; ++s)
     if (2 * s < kw) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
   SIG_STAMP(2);
+  // U positions (first one for a repeated index) of the tile's rows and columns; one wave's LDS
+  // accesses execute in order, the fences keep the compiler from reordering them
+  spos[lane] = kMaxU;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (lane < rnu) {
+    if (ub >= R0 && ub < R0 + 32) atomicMin(&spos[ub - R0], lane);
+    if (ub >= C0 && ub < C0 + 32) atomicMin(&spos[32 + ub - C0], lane);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const int bc = spos[32 + kcol];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
     const int col = C0 + kcol;
-    if (row < n && col < n) Sout[static_cast<size_t>(row) * ld + col] = acc[r];
+    float v = acc[r];
+    if (bc < kMaxU) {  // rare: a column of U
+      const int br = spos[row - R0];
+      if (br < kMaxU) v = static_cast<float>(rec->Pend[br][bc]);
+    }
+    if (row < n && col < n) Sout[static_cast<size_t>(row) * ld + col] = v;
   }
 }
 
@@ -1512,6 +1646,7 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles, in
     if (fb >= nf) return;
   }
   const MsgDesc& d = A.desc[fb];
+  __shared__ int spos[4][64];
   // One 32×32 tile per wave, tiles row-major over a tiles × tiles grid.
   const int lane = threadIdx.x & 63;
   const int t = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1522,42 +1657,10 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles, in
     const int tr = t / tiles, tc = t - tr * tiles;
     sigma_tile(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
                A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
-               (d.flags & kFirst) != 0, A.q, tr * 32, tc * 32, lane);
+               (d.flags & kFirst) != 0, A.q, tr * 32, tc * 32, lane,
+               A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f, spos[threadIdx.x >> 6]);
   }
   SIG_STAMP(3);
-}
-
-// After the Σ pass: its Σ_out[U, U] block replaced by the chain's fp64 values. With fp32 Σ the
-// pass's 1e7 − (1e7 − δ) at a first sighting (the reference's prior, slam.cpp:130) loses δ; the
-// chain computed it in fp64. Other entries carry no such cancellation (the prior has no cross
-// terms). fp32 only: with fp64 Σ the pass's block equals the chain's up to summation order.
-// nf_loop > 0: one workgroup walks the launch's nf_loop filters, stores write-through and then
-// publishes the Σ-pass epoch itself (small batches: one kernel instead of two behind the pass).
-template <typename T>
-__global__ __launch_bounds__(256) void k_block_scatter(PassArgs<T> A, int nf_loop) {
-  const int f_lo = nf_loop > 0 ? 0 : blockIdx.y, f_hi = nf_loop > 0 ? nf_loop : blockIdx.y + 1;
-  for (int fb = f_lo; fb < f_hi; ++fb) {
-    const MsgDesc& d = A.desc[fb];
-    if (!(d.flags & kActive)) continue;
-    const int f = A.f0 + fb;
-    const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
-    const int nu = rec->nu;
-    T* Sout = A.sig[d.parity ^ 1] + f * A.sig_stride;
-    for (int e = threadIdx.x; e < nu * nu; e += blockDim.x) {
-      const int a = e / nu, b = e - a * nu;
-      const T v = static_cast<T>(rec->Pend[a][b]);
-      T* p = Sout + static_cast<size_t>(rec->u[a]) * A.ld + rec->u[b];
-      if (nf_loop > 0)
-        st_wt(p, v);
-      else
-        *p = v;
-    }
-  }
-  if (nf_loop > 0) {
-    drain_stores();
-    __syncthreads();
-    if (threadIdx.x == 0) epoch_store(A.sync + kSyncSigma, A.seq + 1u);
-  }
 }
 
 // Σ-pass epoch for the chains on the other stream, launched right behind the Σ pass on its stream:
@@ -1641,7 +1744,10 @@ __global__ __launch_bounds__(256) void k_assoc(PassArgs<T> A) {
       P[3 + e][4] = static_cast<double>(row[j + 1]);
     }
     double zhat[2], H0[5], H1[5];
-    range_bearing(s_pose, x[j], x[j + 1], zhat, H0, H1);
+    double braw;
+    bool bok;
+    range_bearing(s_pose, x[j], x[j + 1], zhat, H0, H1, &braw, &bok);
+    if (!bok) zhat[1] = normalize_angle(braw);
     double HP0[5], HP1[5];
     for (int bb = 0; bb < 5; ++bb) {
       double s0 = 0.0, s1 = 0.0;
@@ -1770,12 +1876,11 @@ hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_
 int g_sigma_waves = 4;  // waves per Σ-pass workgroup
 
 template <typename T>
-hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s, hipEvent_t e0,
-                             hipEvent_t e1) {
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, hipStream_t s,
+                             hipEvent_t e0, hipEvent_t e1) {
   const int tiles = (a.n + 31) / 32;
   const int wpb = g_sigma_waves;
   const int per_filter = (tiles * tiles + wpb - 1) / wpb;
-  (void)kw;
   if (nf >= 16) {  // XCD-aware 1-D grid (see k_sigma_pass)
     const dim3 grid(8 * ((nf + 7) / 8) * per_filter);
     launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles, per_filter, nf);
@@ -1783,14 +1888,8 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, int kw, hipStream_t s
     const dim3 grid(per_filter, nf);
     launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles, 0, nf);
   }
-  if constexpr (sizeof(T) == 8) {  // fp64 Σ keeps first sightings: no block scatter
-    hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
-  } else if (nf <= 32) {  // scatter + epoch in one workgroup
-    hipLaunchKernelGGL(k_block_scatter<T>, dim3(1, 1), dim3(256), 0, s, a, nf);
-  } else {
-    hipLaunchKernelGGL(k_block_scatter<T>, dim3(1, nf), dim3(256), 0, s, a, 0);
-    hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
-  }
+  // the pass's epoch (otherwise published by the next chunk's factor kernel, PassArgs::pub_sigma)
+  if (publish) hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();
 }
 
@@ -1818,7 +1917,7 @@ hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
                                       hipEvent_t);                                                 \
   template hipError_t launch_factors<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t,          \
                                         hipEvent_t);                                               \
-  template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, int, hipStream_t, hipEvent_t,  \
+  template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, bool, hipStream_t, hipEvent_t, \
                                            hipEvent_t);                                            \
   template hipError_t launch_assoc<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t, hipEvent_t); \
   template hipError_t launch_posterior<T>(const PassArgs<T>&, int, hipStream_t);              \

@@ -27,6 +27,7 @@ struct PassArgs {
   unsigned* sync;       // device epochs (ekf_device.hpp kSync*)
   unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
   unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
+  unsigned pub_sigma;   // factors: publish this Σ-pass epoch first (the previous chunk's pass, 0 = none)
   const MsgDesc* desc;
   int desc_stride;      // descriptors between consecutive chunks of a chain launch
   int n, ld, N, f0;
@@ -45,9 +46,11 @@ template <typename T>
 hipError_t launch_factors(const PassArgs<T>& a, int n_filters, hipStream_t s,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
-// Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, 64×64 tiles. kw = padded rank for this launch.
+// Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, one 32×32 tile per wave (fp32: the chain's fp64
+// Σ[U,U] written over its block). publish: launch the Σ-pass epoch kernel behind it; otherwise
+// the next chunk's factor kernel publishes it (PassArgs::pub_sigma).
 template <typename T>
-hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, int kw, hipStream_t s,
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, bool publish, hipStream_t s,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // Mahalanobis nearest-neighbour association for one marker per filter (one workgroup each).

@@ -33,6 +33,16 @@ __host__ __device__ inline double normalize_angle(double rad) {
   return d <= 0.0 ? d + kPi : d - kPi;
 }
 
+// normalize_angle for |rad + π| < 5π, branch-free (selects): the same bits as normalize_angle
+// there; *ok is false outside, where the caller falls back to normalize_angle.
+__host__ __device__ inline double normalize_angle_near(double rad, bool* ok) {
+  const double y = 2.0 * kPi;
+  const double x = rad + kPi, ax = fabs(x);
+  *ok = ax < 2.5 * y;
+  const double d = ax < y ? x : copysign(ax < 2.0 * y ? ax - y : ax - 2.0 * y, x);
+  return d <= 0.0 ? d + kPi : d - kPi;
+}
+
 // atan2 in ~45 f64 operations (one division) for the bearing of every EKF step; max error
 // 0.59 ulp for the reduced atan (fitted at 60 digits by tools/fit_atan.py), ≤ 2 ulp overall.
 // ocml's atan2 costs ~190 f64 operations and sits on the correction chain's critical path.
@@ -44,13 +54,11 @@ __host__ __device__ inline double atan2_fast(double y, double x) {
   const double ax = fabs(x), ay = fabs(y);
   const bool swap = ay > ax;
   const double num = swap ? ax : ay, den = swap ? ay : ax;  // t = num/den ∈ [0, 1]
-  double t = 0.0, off = 0.0;
-  if (num > 0.41421356237309503 * den) {  // atan(t) = π/4 + atan((t−1)/(t+1))
-    t = (num - den) / (num + den);
-    off = 0.78539816339744831;
-  } else if (den > 0.0) {
-    t = num / den;
-  }
+  // atan(t) = π/4 + atan((t−1)/(t+1)) above tan(π/8); selects, one division, no branch
+  const bool hi = num > 0.41421356237309503 * den;
+  const double tq = (hi ? num - den : num) / (hi ? num + den : (den > 0.0 ? den : 1.0));
+  const double t = hi || den > 0.0 ? tq : 0.0;
+  const double off = hi ? 0.78539816339744831 : 0.0;
   const double z = t * t;
   double r = kC[10];
   for (int k = 9; k >= 0; --k) r = fma(r, z, kC[k]);

@@ -21,20 +21,23 @@ e.replay(sc.count[:, None], sc.rel[:, None], odom[:, None], ids=sc.ids[:, None],
          actions=sc.actions[:, None])
 e.sync()
 L = pyekf.lib()
-st = (C.c_ulonglong * 160)()
+st = (C.c_ulonglong * 256)()
 L.ekf_diag_stamps.argtypes = [C.c_void_p, C.c_int]
-assert L.ekf_diag_stamps(st, 160) == 0
+assert L.ekf_diag_stamps(st, 256) == 0
 s = np.array(st[:], dtype=np.int64)
 t0 = s[0]
-names = {1: "A0", 8: "carry:pos", 9: "carry:gather", 10: "carry:K'M'", 11: "carry:P,x", 6: "A1 done",
+names = {1: "A0", 8: "carry:pos", 9: "carry:gather", 10: "carry:K'M'", 11: "carry:P,x", 17: "fused: reads", 18: "fused: compute", 6: "A1 done",
          2: "predict (steps start)", 12: "steps+final pass", 16: "epi: rec stores issued", 40: "carry copies"}
-for k in (1, 8, 9, 10, 11, 6, 2, 12, 16, 40):
+for k in (1, 8, 9, 10, 11, 17, 18, 6, 2, 12, 16, 40):
     print(f"{names[k]:24s} {s[k] - t0:8d}")
 m = int(sc.count[-1])
-steps = [s[64 + 6 * c] - t0 for c in range(m)]
+steps = [s[64 + 8 * c] - t0 for c in range(m)]
 print("step starts:", steps)
-for c in (0, m // 2, m - 1):
-    b = 64 + 6 * c
-    print(f"step {c}: range_bearing {s[b+1]-s[b]}  S,inv {s[b+2]-s[b+1]}  K,M,x,publish {s[b+3]-s[b+2]}"
-          f"  Bx reads {s[b+4]-s[b+3]}  cross update {s[b+5]-s[b+4]}  -> next {s[b+6]-s[b+5] if c+1<m else 0}")
+for c in (0, 1, m // 2, m - 2):
+    b = 64 + 8 * c
+    d = [s[b + k + 1] - s[b + k] for k in range(6)]
+    print(f"step {c}: start {d[0]}  S,inv,nu {d[1]}  pdone wait+Bx reads {d[2]}  K,M,x,publish {d[3]}"
+          f"  geometry(c+1)+cross update {s[b + 6] - s[b + 4]}  -> next {s[b + 8] - s[b + 6]}")
+    print(f"   wave3: pub seen at {s[192 + 2 * c] - s[b]}, pdone at {s[193 + 2 * c] - s[b]} "
+          f"(wave0 publish at {s[b + 4] - s[b]}, next-step pdone wait at {s[b + 8 + 2] - s[b]})")
 e.close()
