@@ -354,13 +354,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.pv.Y[0][0])[e] = (&sh.Y[0][0])[e];
     if (tid < kZC) sh.pv.Z[kMaxU][tid] = 0.0;
   }
-  for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.Z[0][0])[e] = 0.0;
-  for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.Y[0][0])[e] = 0.0;
-  for (int e = tid; e < kMaxU * (kMaxU + 1); e += blockDim.x) {  // Φ = Ψ = I
-    const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
-    (&sh.Phi[0][0][0])[e] = a == b ? 1.0 : 0.0;
-    (&sh.Psi[0][0][0])[e] = a == b ? 1.0 : 0.0;
-  }
+  // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
   if (tid == 0) sh.status = 0;
   __syncthreads();
   EKF_STAMP(0);
@@ -1125,9 +1119,26 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // The record parity this chunk writes was last written two chunks back: the bulk stream must
     // be done with it (its factor kernel and block scatter finish before that chunk's Σ-pass
     // epoch). A carried chunk without new indices has not polled; the others' polls covered this.
+    // Z_c goes to the record as soon as it is computed (write-through, off the chain's path).
     if (lane == 0 && carry && d.nnew == 0 && seq >= 2 &&
         !epoch_wait_acquire(A.sync + kSyncSigma, seq - 1))
       atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+    for (int e = lane; e < kMaxU * (kMaxU + 1); e += 64) {  // Φ = I
+      const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
+      (&sh.Phi[0][0][0])[e] = a == b ? 1.0 : 0.0;
+    }
+    ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
+    constexpr int oZ = static_cast<int>(offsetof(ChunkRec, Z));
+    __syncwarp();  // the lane-0 wait above orders every lane's record stores below
+    {  // columns ≥ 2m of the record's Z are zero (the factor kernel and a rebuilding chain read them)
+      const int zw = kZC - 2 * m;
+      for (int e = lane; e < kMaxU * zw; e += 64) {
+        const int b = e / zw, k = 2 * m + (e - b * zw);
+        st_wt(&rec->Z[b][k], 0.0);
+      }
+    }
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1147,6 +1158,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
         sh.Z[lane][2 * c] = Z0;
         sh.Z[lane][2 * c + 1] = Z1;
+        st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
       }
       if (c + 1 < m) {
         const int live = 3 + (nu - pj - 2);
@@ -1169,8 +1181,19 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
       }
     }
-  } else {  // wave 2: Y_c and Ψ (live rows)
+  } else {  // wave 2: Y_c and Ψ (live rows); Y_c to the record as soon as it is computed
     const int ha = lane & 31, hr = lane >> 5;
+    if (lane == 0 && carry && d.nnew == 0 && seq >= 2 &&
+        !epoch_wait_acquire(A.sync + kSyncSigma, seq - 1))
+      atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+    for (int e = lane; e < kMaxU * (kMaxU + 1); e += 64) {  // Ψ = I
+      const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
+      (&sh.Psi[0][0][0])[e] = a == b ? 1.0 : 0.0;
+    }
+    ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+    __syncwarp();
+    for (int e = lane; e < (kZC - 2 * m) * kMaxU; e += 64)  // rows ≥ 2m of the record's Y are zero
+      st_wt(&(&rec->Y[2 * m][0])[e], 0.0);
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1187,6 +1210,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
         sh.Y[2 * c][lane] = y0;
         sh.Y[2 * c + 1][lane] = y1;
+        st_wt(&rec->Y[2 * c][lane], y0);
+        st_wt(&rec->Y[2 * c + 1][lane], y1);
       }
       if (c + 1 < m) {
         const int live = 3 + (nu - pj - 2);
@@ -1214,14 +1239,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   __syncthreads();
   // The last step's rank-2 term on the whole block (earlier steps are applied), written to Pst:
   // the final Σ[U, U] is what the next chunk of this launch carries.
+  // fp32 Σ: the block also goes to the record (write-through) for the Σ pass's U × U entries.
   {
     const int c = max(m - 1, 0);
+    ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     for (int e = tid; e < kMaxU * (kMaxU + 1); e += blockDim.x) {
       const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
       double v = sh.P[0][a][b];
-      if (m > 0 && a < nu && b < nu)
+      const bool in = a < nu && b < nu;
+      if (m > 0 && in)
         v = rank2_sub(v, sh.KU[c][a][0], sh.KU[c][a][1], sh.MU[c][b][0], sh.MU[c][b][1]);
       sh.Pst[a][b] = v;
+      if constexpr (sizeof(T) == 4) {
+        if (in) st_wt(&rec->Pend[a][b], v);
+      }
     }
   }
   __syncthreads();
@@ -1258,7 +1289,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
   } else {
-    constexpr int kT = 3 * 64;
     if (pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
       reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
           &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
@@ -1266,8 +1296,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // hand the chunk to the factor kernel (and the next chain): write-through record
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
-      double zx = 0.0;
-      for (int c = 0; c < m; ++c) zx += sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];
+      double zx = 0.0;  // (reads unconditional, terms past m selected away: one LDS round trip)
+#pragma unroll
+      for (int c = 0; c < kMaxChunk; ++c) {
+        const double t = sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];
+        zx += c < m ? t : 0.0;
+      }
       const bool in = tid < nu;
       st_wt(&rec->Zx[tid], zx);
       st_wt(&rec->u[tid], sh.u[tid]);
@@ -1291,29 +1325,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       sh.pv.first = first ? 1 : 0;
       sh.pv.a1 = sh.a1;
       sh.pv.a2 = sh.a2;
-    }
-    // Z, Y (and Pend) in 16-byte write-through stores: half the store instructions of 8-byte
-    // ones, and the issue of write-through stores is what this phase waits on
-    const __amdgpu_buffer_rsrc_t rr =
-        __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
-    constexpr int oZ = static_cast<int>(offsetof(ChunkRec, Z)), oY = static_cast<int>(offsetof(ChunkRec, Y));
-    for (int e = tid; e < kMaxU * kZC / 2; e += kT) {
-      const int b = e / (kZC / 2), k = 2 * (e - b * (kZC / 2));
-      st_wt2(rr, oZ + 16 * e, sh.Z[b][k], sh.Z[b][k + 1]);
-    }
-    for (int e = tid; e < kZC * kMaxU / 2; e += kT) {
-      const int e0 = 2 * e, e1 = e0 + 1;
-      const int k0 = e0 / kMaxU, b0 = e0 - k0 * kMaxU, k1 = e1 / kMaxU, b1 = e1 - k1 * kMaxU;
-      st_wt2(rr, oY + 16 * e, sh.Y[k0][b0], sh.Y[k1][b1]);
-    }
-    if constexpr (sizeof(T) == 4) {  // fp32 Σ only: the Σ pass's payload for the U × U block
-      constexpr int oP = static_cast<int>(offsetof(ChunkRec, Pend));
-      for (int e = tid; e < kMaxU * kMaxU / 2; e += kT) {
-        const int e0 = 2 * e, e1 = e0 + 1;
-        const int a0 = e0 / kMaxU, b0 = e0 - a0 * kMaxU, a1 = e1 / kMaxU, b1 = e1 - a1 * kMaxU;
-        st_wt2(rr, oP + 16 * e, sh.Pst[a0][b0], sh.Pst[a1][b1]);
-      }
-      if (tid == kT - 1) st_wt(&rec->Pend[kMaxU - 1][kMaxU - 1], sh.Pst[kMaxU - 1][kMaxU - 1]);
     }
     EKF_STAMP(16);
   }
@@ -1604,12 +1615,9 @@ __device__ __forceinline__ void sigma_tile(const float* Sin, float* Sout, const 
     if (first && row == col && row < 3) v += q;
     acc[r] = v;
   }
-#pragma unroll
-  for (int s = 0; s < 18; ++s)
-    if (2 * s < kw) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
-  SIG_STAMP(2);
-  // U positions (first one for a repeated index) of the tile's rows and columns; one wave's LDS
-  // accesses execute in order, the fences keep the compiler from reordering them
+  // U positions (first one for a repeated index) of the tile's rows and columns, while the
+  // operand loads are in flight; one wave's LDS accesses execute in order, the fences keep the
+  // compiler from reordering them
   spos[lane] = kMaxU;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   if (lane < rnu) {
@@ -1618,6 +1626,10 @@ __device__ __forceinline__ void sigma_tile(const float* Sin, float* Sout, const 
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const int bc = spos[32 + kcol];
+#pragma unroll
+  for (int s = 0; s < 18; ++s)
+    if (2 * s < kw) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+  SIG_STAMP(2);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
