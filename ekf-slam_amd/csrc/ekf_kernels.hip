@@ -1526,129 +1526,156 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
 
 
 // ---- Σ pass on MFMA -------------------------------------------------------------------------
-// Σ_out = Σ_in + Q̄ − Σ_k Kcat[k]ᵀ ⊗ Mcat[k]. Block tile 64×64, four waves of 32×32. Every operand
-// of a wave is loaded before the first MFMA (one wait), and the accumulator layout makes each load
-// / store instruction cover whole 128-B rows:
-//   fp64  v_mfma_f64_16x16x4_f64 (2×2 tiles): D[row = (lane>>4) + 4r][col = lane&15] → 4 rows × 128 B
-//   fp32  v_mfma_f32_32x32x2_f32 (1 tile):    D[row = (r&3) + 8(r>>2) + 4(lane>>5)][col = lane&31]
-//         → 2 rows × 128 B
-// Loads are unconditional — Kcat/Mcat hold kMaxKW rows × ldk columns, Σ indices are clamped — since
-// a predicated load becomes a branch with its own wait. Clamped lanes only feed D elements that
-// are never stored (an MFMA's D[i][j] reads only C[i][j], A[i][:], B[:][j]); rows ≥ kw are skipped
-// a whole k-step at a time.
+// Σ_out = Σ_in + Q̄ − Σ_k Kcat[k]ᵀ ⊗ Mcat[k], one tile per wave, four waves per workgroup.
+//   fp32  32×32 tile, v_mfma_f32_32x32x2_f32: D[row = (r&3) + 8(r>>2) + 4(lane>>5)][col = lane&31]
+//         → each load / store instruction covers 2 rows × 128 B
+//   fp64  32×16 tile, two v_mfma_f64_16x16x4_f64 blocks: D[row = 16ti + (lane>>4) + 4r][col = lane&15]
+//         → 4 rows × 128 B per instruction
 // A/B lane maps: 16x16x4 A[i = lane&15][k = lane>>4]; 32x32x2 A[i = lane&31][k = lane>>5].
+// Memory goes through buffer descriptors with 32-bit offsets (no 64-bit address per load):
+//   - Σ: the filter's n·ld elements; a row ≥ n lies past the end, a column ≥ n gets the offset
+//     kOOB, so the range check returns 0 for its loads and drops its stores (no masks, no waits);
+//   - Kcat / Mcat: the factor rows are uniform (SGPR soffset), the lane's column in voffset.
+// Order: operands (L2-hot) first, then Σ_in. The MFMAs start from zero as soon as the operands
+// land and run while Σ_in is still in flight; Σ_in (+ Q̄) is added once, before the store.
 typedef float f16v __attribute__((ext_vector_type(16)));
+constexpr unsigned kOOB = 0x80000000u;  // voffset past any Σ descriptor (n·ld·w < 2 GiB)
 
-__device__ __forceinline__ void sigma_tile(const double* Sin, double* Sout, const double* kc,
-                                           const double* mc, int n, int ld, int ldk, int kw,
-                                           bool first, double q, int R0, int C0, int lane,
-                                           const ChunkRec*, int*) {
-  const int kr = lane >> 4, kcol = lane & 15;
-  double a[2][9], b[2][9];
-#pragma unroll
-  for (int s = 0; s < 9; ++s) {
-    const double* krow = kc + static_cast<size_t>(4 * s + kr) * ldk;
-    const double* mrow = mc + static_cast<size_t>(4 * s + kr) * ldk;
-    a[0][s] = -krow[R0 + kcol];
-    a[1][s] = -krow[R0 + 16 + kcol];
-    b[0][s] = mrow[C0 + kcol];
-    b[1][s] = mrow[C0 + 16 + kcol];
-  }
-  d4 acc[2][2];
-#pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = R0 + 16 * ti + kr + 4 * r;
-        const int col = C0 + 16 * tj + kcol;
-        double v = Sin[static_cast<size_t>(min(row, n - 1)) * ld + min(col, n - 1)];
-        if (first && row == col && row < 3) v += q;
-        acc[ti][tj][r] = v;
-      }
-#pragma unroll
-  for (int s = 0; s < 9; ++s) {
-    if (4 * s < kw) {
-      acc[0][0] = mfma_f64(a[0][s], b[0][s], acc[0][0]);
-      acc[0][1] = mfma_f64(a[0][s], b[1][s], acc[0][1]);
-      acc[1][0] = mfma_f64(a[1][s], b[0][s], acc[1][0]);
-      acc[1][1] = mfma_f64(a[1][s], b[1][s], acc[1][1]);
-    }
-  }
-  SIG_STAMP(2);
-#pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = R0 + 16 * ti + kr + 4 * r;
-        const int col = C0 + 16 * tj + kcol;
-        if (row < n && col < n) Sout[static_cast<size_t>(row) * ld + col] = acc[ti][tj][r];
-      }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double ld_f64(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
 }
 
-// fp32 also takes the chain's fp64 Σ[U, U] (rec->Pend) over the pass's own values there: the
-// pass's 1e7 − (1e7 − δ) at a first sighting (the reference's prior, slam.cpp:130) loses δ in
-// fp32; the chain computed it in fp64. Other entries carry no such cancellation (the prior has no
-// cross terms). spos: this wave's 64 LDS words (positions in U of its 32 rows and 32 columns).
-__device__ __forceinline__ void sigma_tile(const float* Sin, float* Sout, const float* kc,
-                                           const float* mc, int n, int ld, int ldk, int kw,
-                                           bool first, double qd, int R0, int C0, int lane,
-                                           const ChunkRec* rec, int* spos) {
-  const int kr = lane >> 5, kcol = lane & 31;
-  const float q = static_cast<float>(qd);
-  const int ub = rec->u[min(lane, kMaxU - 1)], rnu = rec->nu;
-  float a[18], b[18];
+#ifndef EKF_SIGMA64_TJ
+#define EKF_SIGMA64_TJ 2  // fp64 tile = 32 × 16·TJ
+#endif
+template <typename T>
+struct SigmaTile;
+
+template <>
+struct SigmaTile<float> {
+  static constexpr int kRows = 32, kCols = 32;
+  static __device__ __forceinline__ void run(const float* Sin, float* Sout, const float* kc,
+                                             const float* mc, int n, int ld, int ldk, int kw,
+                                             bool first, double qd, int R0, int C0, int lane) {
+    const int kr = lane >> 5, kcol = lane & 31;
+    const unsigned sbytes = static_cast<unsigned>(n) * ld * 4u;
+    const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 4u;
+    const auto rin = buf_rsrc(Sin, sbytes), rout = buf_rsrc(Sout, sbytes);
+    const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
+    float a[18], b[18], sv[16];
+    const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 4u;
+    const unsigned mo = static_cast<unsigned>(kr * ldk + min(C0 + kcol, n - 1)) * 4u;
+    const unsigned kstep = 2u * ldk * 4u;
 #pragma unroll
-  for (int s = 0; s < 18; ++s) {
-    a[s] = -kc[static_cast<size_t>(2 * s + kr) * ldk + R0 + kcol];
-    b[s] = mc[static_cast<size_t>(2 * s + kr) * ldk + C0 + kcol];
-  }
-  f16v acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
-    const int col = C0 + kcol;
-    float v = Sin[static_cast<size_t>(min(row, n - 1)) * ld + min(col, n - 1)];
-    if (first && row == col && row < 3) v += q;
-    acc[r] = v;
-  }
-  // U positions (first one for a repeated index) of the tile's rows and columns, while the
-  // operand loads are in flight; one wave's LDS accesses execute in order, the fences keep the
-  // compiler from reordering them
-  spos[lane] = kMaxU;
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  if (lane < rnu) {
-    if (ub >= R0 && ub < R0 + 32) atomicMin(&spos[ub - R0], lane);
-    if (ub >= C0 && ub < C0 + 32) atomicMin(&spos[32 + ub - C0], lane);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const int bc = spos[32 + kcol];
-#pragma unroll
-  for (int s = 0; s < 18; ++s)
-    if (2 * s < kw) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
-  SIG_STAMP(2);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
-    const int col = C0 + kcol;
-    float v = acc[r];
-    if (bc < kMaxU) {  // rare: a column of U
-      const int br = spos[row - R0];
-      if (br < kMaxU) v = static_cast<float>(rec->Pend[br][bc]);
+    for (int s = 0; s < 18; ++s) {
+      a[s] = ld_f32(rk, ko, s * kstep);
+      b[s] = ld_f32(rm, mo, s * kstep);
     }
-    if (row < n && col < n) Sout[static_cast<size_t>(row) * ld + col] = v;
+    const int col = C0 + kcol;
+    const unsigned so = col < n ? static_cast<unsigned>((R0 + 4 * kr) * ld + col) * 4u : kOOB;
+    const unsigned rstride = static_cast<unsigned>(ld) * 4u;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[r] = ld_f32(rin, so + ((r & 3) + 8 * (r >> 2)) * rstride, 0);
+    f16v acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 18; ++s)
+      if (2 * s < kw) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    SIG_STAMP(2);
+    const float q = static_cast<float>(qd);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
+      float v = sv[r] - acc[r];
+      if (first && row == col && row < 3) v += q;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout,
+                                            so + ((r & 3) + 8 * (r >> 2)) * rstride, 0, 0);
+    }
   }
-}
+};
+
+template <>
+struct SigmaTile<double> {
+  static constexpr int kRows = 32, kCols = 16 * EKF_SIGMA64_TJ;
+  static constexpr int TJ = EKF_SIGMA64_TJ;
+  static __device__ __forceinline__ void run(const double* Sin, double* Sout, const double* kc,
+                                             const double* mc, int n, int ld, int ldk, int kw,
+                                             bool first, double q, int R0, int C0, int lane) {
+    const int kr = lane >> 4, kcol = lane & 15;
+    const unsigned sbytes = static_cast<unsigned>(n) * ld * 8u;
+    const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 8u;
+    const auto rin = buf_rsrc(Sin, sbytes), rout = buf_rsrc(Sout, sbytes);
+    const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
+    double a[2][9], b[TJ][9], sv[2][TJ][4];
+    const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 8u;
+    unsigned mo[TJ], so[TJ];
+    const unsigned rstride = static_cast<unsigned>(ld) * 8u;
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) {
+      const int col = C0 + 16 * tj + kcol;
+      mo[tj] = static_cast<unsigned>(kr * ldk + min(col, n - 1)) * 8u;
+      so[tj] = col < n ? static_cast<unsigned>((R0 + kr) * ld + col) * 8u : kOOB;
+    }
+    const unsigned kstep = 4u * ldk * 8u;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      a[0][s] = ld_f64(rk, ko, s * kstep);
+      a[1][s] = ld_f64(rk, ko + 16 * 8, s * kstep);
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) b[tj][s] = ld_f64(rm, mo[tj], s * kstep);
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sv[ti][tj][r] = ld_f64(rin, so[tj] + (16 * ti + 4 * r) * rstride, 0);
+    d4 acc[2][TJ];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = d4{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      if (4 * s < kw) {
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = mfma_f64(a[ti][s], b[tj][s], acc[ti][tj]);
+      }
+    }
+    SIG_STAMP(2);
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = R0 + 16 * ti + kr + 4 * r, col = C0 + 16 * tj + kcol;
+          double v = sv[ti][tj][r] - acc[ti][tj][r];
+          if (first && row == col && row < 3) v += q;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rout,
+                                                so[tj] + (16 * ti + 4 * r) * rstride, 0, 0);
+        }
+  }
+};
 
 // xcd_b = 0: grid (blocks per filter, filters). xcd_b = B > 0 (many filters): a 1-D grid whose
 // block L runs on XCD L % 8 (dispatch deals blocks round-robin over the XCDs); it is given filter
 // 8·⌊(L/8)/B⌋ + L % 8, tile block (L/8) % B, so all of a filter's blocks share one XCD and its
 // Kcat/Mcat are fetched into one L2 instead of eight. Placement only changes speed.
+// Waves take tiles row-major over a trows × tcols grid.
 template <typename T>
-__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles, int xcd_b, int nf) {
+__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, int xcd_b, int nf) {
   SIG_STAMP(0);
   int fb = blockIdx.y, bx = blockIdx.x;
   if (xcd_b > 0) {
@@ -1658,21 +1685,49 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tiles, in
     if (fb >= nf) return;
   }
   const MsgDesc& d = A.desc[fb];
-  __shared__ int spos[4][64];
-  // One 32×32 tile per wave, tiles row-major over a tiles × tiles grid.
   const int lane = threadIdx.x & 63;
+  const int trows = (A.n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows;
   const int t = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if ((d.flags & kActive) && t < tiles * tiles) {
+  if ((d.flags & kActive) && t < trows * tcols) {
     SIG_STAMP(1);
     const int f = A.f0 + fb;
     const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
-    const int tr = t / tiles, tc = t - tr * tiles;
-    sigma_tile(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
-               A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
-               (d.flags & kFirst) != 0, A.q, tr * 32, tc * 32, lane,
-               A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f, spos[threadIdx.x >> 6]);
+    const int tr = t / tcols, tc = t - tr * tcols;
+    SigmaTile<T>::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
+                      A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
+                      (d.flags & kFirst) != 0, A.q, tr * SigmaTile<T>::kRows,
+                      tc * SigmaTile<T>::kCols, lane);
   }
   SIG_STAMP(3);
+}
+
+// fp32 only, right behind the Σ pass on its stream: the chain's fp64 Σ[U, U] (rec->Pend, rounded
+// once) over the pass's values there. The pass's 1e7 − (1e7 − δ) at a first sighting (the
+// reference's prior, slam.cpp:130) loses δ in fp32; the chain computed it in fp64. Other entries
+// carry no such cancellation (the prior has no cross terms). A repeated index takes the entry of
+// its first position in U. One workgroup per filter, ≤ 35 × 35 stores.
+__global__ __launch_bounds__(256) void k_pend_scatter(PassArgs<float> A) {
+  const MsgDesc& d = A.desc[blockIdx.x];
+  if (!(d.flags & kActive)) return;
+  const int f = A.f0 + blockIdx.x;
+  const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+  __shared__ int su[kMaxU];
+  __shared__ bool firstpos[kMaxU];
+  const int nu = rec->nu;
+  if (threadIdx.x < kMaxU) su[threadIdx.x] = rec->u[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x < nu) {
+    bool fp = true;
+    for (int k = 0; k < static_cast<int>(threadIdx.x); ++k) fp = fp && su[k] != su[threadIdx.x];
+    firstpos[threadIdx.x] = fp;
+  }
+  __syncthreads();
+  float* S = A.sig[d.parity ^ 1] + f * A.sig_stride;
+  for (int e = threadIdx.x; e < nu * nu; e += blockDim.x) {
+    const int a = e / nu, b = e - a * nu;
+    if (firstpos[a] && firstpos[b])
+      S[static_cast<size_t>(su[a]) * A.ld + su[b]] = static_cast<float>(rec->Pend[a][b]);
+  }
 }
 
 // Σ-pass epoch for the chains on the other stream, launched right behind the Σ pass on its stream:
@@ -1885,21 +1940,22 @@ hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_
   return hipGetLastError();
 }
 
-int g_sigma_waves = 4;  // waves per Σ-pass workgroup
-
 template <typename T>
 hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, hipStream_t s,
                              hipEvent_t e0, hipEvent_t e1) {
-  const int tiles = (a.n + 31) / 32;
-  const int wpb = g_sigma_waves;
-  const int per_filter = (tiles * tiles + wpb - 1) / wpb;
+  constexpr int wpb = 4;  // waves per workgroup
+  const int trows = (a.n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows;
+  const int tcols = (a.n + SigmaTile<T>::kCols - 1) / SigmaTile<T>::kCols;
+  const int per_filter = (trows * tcols + wpb - 1) / wpb;
   if (nf >= 16) {  // XCD-aware 1-D grid (see k_sigma_pass)
     const dim3 grid(8 * ((nf + 7) / 8) * per_filter);
-    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles, per_filter, nf);
+    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, per_filter, nf);
   } else {
     const dim3 grid(per_filter, nf);
-    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tiles, 0, nf);
+    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
   }
+  if constexpr (sizeof(T) == 4)
+    hipLaunchKernelGGL(k_pend_scatter, dim3(nf), dim3(256), 0, s, a);
   // the pass's epoch (otherwise published by the next chunk's factor kernel, PassArgs::pub_sigma)
   if (publish) hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();

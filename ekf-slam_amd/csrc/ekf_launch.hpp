@@ -46,8 +46,8 @@ template <typename T>
 hipError_t launch_factors(const PassArgs<T>& a, int n_filters, hipStream_t s,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
-// Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, one 32×32 tile per wave (fp32: the chain's fp64
-// Σ[U,U] written over its block). publish: launch the Σ-pass epoch kernel behind it; otherwise
+// Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, one tile per wave (fp32: then the chain's fp64
+// Σ[U,U] scattered over its block by k_pend_scatter). publish: launch the Σ-pass epoch kernel behind it; otherwise
 // the next chunk's factor kernel publishes it (PassArgs::pub_sigma).
 template <typename T>
 hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, bool publish, hipStream_t s,

@@ -48,7 +48,11 @@ void run(int N, int F, int reps) {
   CK(hipMemcpy(dd + F, d.data(), F * sizeof(MsgDesc), hipMemcpyHostToDevice));
   FilterCtl* ctl;
   CK(hipMalloc(&ctl, F * sizeof(FilterCtl)));
+  ChunkRec* rec;  // [2][F], nu = 0: no U block to write back (the fp32 pass reads rec->u / nu)
+  CK(hipMalloc(&rec, 2 * F * sizeof(ChunkRec)));
+  CK(hipMemset(rec, 0, 2 * F * sizeof(ChunkRec)));
   PassArgs<T> a{};
+  a.rec = rec; a.rec_stride = F;
   a.sig[0] = S0; a.sig[1] = S1; a.sig_stride = stride;
   a.kcat = kc; a.mcat = mc; a.km_stride = static_cast<size_t>(kMaxKW) * ldk; a.ldk = ldk;
   a.ctl = ctl; a.sync = sync_buf(4096); a.desc = dd; a.n = n; a.ld = ld; a.N = N; a.f0 = 0; a.q = 1e-2;
@@ -83,7 +87,7 @@ void run(int N, int F, int reps) {
   printf(" | sigma pass %.2f us (%.0f GB/s algorithmic)\n", ms * 1e3 / reps, bytes / (ms / reps * 1e-3) / 1e9);
 #ifdef EKF_DIAG_STAMPS
   {
-    const int t32 = (n + 31) / 32, tiles = (t32 * t32 + g_sigma_waves - 1) / g_sigma_waves, nb = std::min(tiles, 4096);
+    const int tiles = ((n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows * ((n + SigmaTile<T>::kCols - 1) / SigmaTile<T>::kCols) + 3) / 4, nb = std::min(tiles, 4096);
     CK(launch_sigma_pass<T>(a, F, 36, s));
     CK(launch_sigma_pass<T>(a, F, 36, s));
     CK(hipStreamSynchronize(s));
@@ -111,13 +115,11 @@ void run(int N, int F, int reps) {
       }
   }
 #endif
-  CK(hipFree(S0)); CK(hipFree(S1)); CK(hipFree(kc)); CK(hipFree(mc)); CK(hipFree(dd)); CK(hipFree(ctl));
+  CK(hipFree(S0)); CK(hipFree(S1)); CK(hipFree(kc)); CK(hipFree(mc)); CK(hipFree(dd)); CK(hipFree(ctl)); CK(hipFree(rec));
 }
 
 int main(int argc, char** argv) {
-  if (argc > 1) g_sigma_waves = atoi(argv[1]);
-  if (argc > 2) g_pingpong = atoi(argv[2]);
-  printf("waves/WG %d\n", g_sigma_waves);
+  if (argc > 1) g_pingpong = atoi(argv[1]);
   run<float>(1024, 1, 200);
   run<double>(1024, 1, 200);
   run<double>(256, 1, 200);
