@@ -1,4 +1,4 @@
-"""ctypes binding of libekfslam.so (include/ekf.h, include/slam_core.h).
+"""ctypes binding of libekfslam.so (include/ekf.h, include/slam_core.h, include/landmarks.h).
 
 The binding is plumbing for tests and bench.py; the product is the C-ABI library. Loading fails
 loudly when the HIP library has not been built — there is no CPU fallback anywhere in this package.
@@ -29,6 +29,8 @@ EXPORTS = [
     "ekf_profile_enable", "ekf_profile_read", "ekf_sigma_pass_bytes", "ekf_normalize_angle",
     "slam_create", "slam_destroy", "slam_joint_states", "slam_markers", "slam_initial_pose",
     "slam_odom", "slam_map_odom", "slam_filter", "slam_replay", "slam_integrate_odometry",
+    "lm_create", "lm_destroy", "lm_detect", "lm_fit_circles", "lm_check_circles",
+    "lm_last_kernel_us",
 ]
 
 
@@ -90,6 +92,12 @@ def lib():
             "slam_filter": (_vp, [_vp]),
             "slam_replay": (_i, [_vp, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
             "slam_integrate_odometry": (_i, [_d, _d, _i, _i, _vp, _vp]),
+            "lm_create": (_i, [C.POINTER(_vp), _i, _i, _i]),
+            "lm_destroy": (_i, [_vp]),
+            "lm_detect": (_i, [_vp, _i, _i, _vp, _vp, _vp, _d, _vp, _i, _vp]),
+            "lm_fit_circles": (_i, [_vp, _i, _vp, _vp, _vp]),
+            "lm_check_circles": (_i, [_vp, _i, _vp, _vp, _vp]),
+            "lm_last_kernel_us": (_i, [_vp, _dp]),
         }
         for name, (res, argt) in sig.items():
             fn = getattr(L, name)

@@ -9,10 +9,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     names = set()
-    for h in ("ekf.h", "slam_core.h"):
+    for h in ("ekf.h", "slam_core.h", "landmarks.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b((?:ekf|slam)_\w+)\s*\(",
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b((?:ekf|slam|lm)_\w+)\s*\(",
                              src, flags=re.M):
             names.add(m.group(1))
     return names
@@ -48,5 +48,5 @@ def test_no_cpu_fallback_in_product():
             if fn.endswith((".py", ".cpp", ".hip", ".hpp")):
                 text = open(os.path.join(dirpath, fn)).read()
                 for banned in ("import orc", "ekf_numpy", "ekf_oracle", "libekf_oracle",
-                               "orc_ekf"):
+                               "orc_ekf", "landmarks_numpy"):
                     assert banned not in text, (fn, banned)
