@@ -309,10 +309,13 @@ __global__ __launch_bounds__(64) void k_detect(const float* __restrict__ ranges,
                                               const double* __restrict__ ainc, double thr,
                                               lm_marker* __restrict__ out, int max_markers,
                                               int* __restrict__ counts) {
-  __shared__ double px[LM_MAX_BEAMS], py[LM_MAX_BEAMS];
-  __shared__ int bpos[LM_MAX_BEAMS];
+  // dynamic LDS sized to the scan (B·20 bytes: 7.2 KB at 360 beams), so a CU holds many scans
+  extern __shared__ double lds[];
   const int s = blockIdx.x, lane = threadIdx.x;
   const int B = nb_beams;
+  double* px = lds;
+  double* py = lds + B;
+  int* bpos = reinterpret_cast<int*>(lds + 2 * B);
   const float* rs = ranges + static_cast<size_t>(s) * B;
   const double a0 = amin[s], inc = ainc[s];
   for (int i = lane; i < B; i += 64) {  // landmarks.cpp:66-70
@@ -405,7 +408,8 @@ __global__ __launch_bounds__(64) void k_check(int nc, const int* __restrict__ of
 hipError_t launch_detect(const float* ranges, int S, int B, const double* amin,
                          const double* ainc, double thr, lm_marker* out, int max_markers,
                          int* counts, hipStream_t st) {
-  hipLaunchKernelGGL(k_detect, dim3(S), dim3(64), 0, st, ranges, B, amin, ainc, thr, out,
+  const size_t lds = static_cast<size_t>(B) * (2 * sizeof(double) + sizeof(int));
+  hipLaunchKernelGGL(k_detect, dim3(S), dim3(64), lds, st, ranges, B, amin, ainc, thr, out,
                      max_markers, counts);
   return hipGetLastError();
 }

@@ -167,3 +167,35 @@ def synthetic(n_landmarks: int, n_messages: int, seed: int = 20240317, max_marke
     """SURVEY.md §8d synthetic map: N landmarks, unit circle at ω = 0.5, m nearest markers."""
     lm = random_landmarks(n_landmarks, seed)
     return make_scenario(n_landmarks, lm, n_messages, seed=seed, max_markers=max_markers, **kw)
+
+
+def lidar_scans(poses, circles, arena=(10.0, 5.0), n_beams=360, sigma=0.0, seed=20240317,
+                range_min=0.11, range_max=10.0):
+    """Synthetic LaserScan ranges (float32 [P, n_beams]) for body poses [P, 3] = (θ, x, y): a lidar
+    mounted −0.032 m along the body x axis (nusim.cpp:577), beam i at θ + i·2π/n_beams, exact ray
+    casting against cylinders ``circles`` [(x, y, r)] and the walls of an axis-aligned arena centred
+    on the origin, clamped to [range_min, range_max], plus N(0, σ²) noise (nusim.cpp:700-707).
+    Scan inputs for the landmark front-end (include/landmarks.h); angle_min = 0,
+    angle_increment = float32(2π / n_beams)."""
+    poses = np.atleast_2d(np.asarray(poses, dtype=np.float64))
+    th = poses[:, 0:1] + np.arange(n_beams)[None, :] * (2.0 * math.pi / n_beams)
+    lx = (poses[:, 1] - 0.032 * np.cos(poses[:, 0]))[:, None]
+    ly = (poses[:, 2] - 0.032 * np.sin(poses[:, 0]))[:, None]
+    dx, dy = np.cos(th), np.sin(th)
+    best = np.full(th.shape, np.inf)
+    for (cx, cy, r) in circles:
+        fx, fy = lx - cx, ly - cy
+        bq = fx * dx + fy * dy
+        disc = bq * bq - (fx * fx + fy * fy - r * r)
+        with np.errstate(invalid="ignore"):
+            t = -bq - np.sqrt(disc)
+        hit = (disc >= 0.0) & (t > 0.0)
+        best = np.where(hit, np.minimum(best, t), best)
+    hx, hy = arena[0] / 2.0, arena[1] / 2.0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for den, lim, org in ((dx, hx, lx), (-dx, hx, -lx), (dy, hy, ly), (-dy, hy, -ly)):
+            best = np.where(den > 1e-12, np.minimum(best, (lim - org) / den), best)
+    best = np.clip(best, range_min, range_max)
+    if sigma > 0.0:
+        best = best + np.random.default_rng(seed).normal(0.0, sigma, best.shape)
+    return best.astype(np.float32)
