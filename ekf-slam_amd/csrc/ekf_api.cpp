@@ -748,6 +748,8 @@ int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, cons
   return flush(h);
 }
 
+constexpr size_t kFlushDesc = 2048;
+
 int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, const int* ids,
                const int* actions, const double* rel_xy, const double* odom, double* out_pose) {
   if (!h || T < 0 || !counts || !odom || m_max < 0 || (m_max > 0 && !rel_xy) ||
@@ -769,6 +771,13 @@ int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, con
       plan_assoc(h, 0, h->F, true, true, 0, mm);
     } else {
       plan_known(h, 0, h->F, true);
+    }
+    // Many filters: upload and launch every ~kFlushDesc descriptors, so planning the next
+    // messages on the host overlaps the GPU's work on these (one filter keeps the whole replay in
+    // one upload and one persistent chain launch).
+    if (!out_pose && h->plan_d.size() >= kFlushDesc) {
+      rc = flush(h);
+      if (rc) return rc;
     }
     if (out_pose) {
       rc = flush(h);

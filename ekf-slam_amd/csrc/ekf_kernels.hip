@@ -1712,21 +1712,31 @@ __global__ __launch_bounds__(256) void k_pend_scatter(PassArgs<float> A) {
   const int f = A.f0 + blockIdx.x;
   const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
   __shared__ int su[kMaxU];
-  __shared__ bool firstpos[kMaxU];
+  __shared__ int firstpos[kMaxU];
+  // every global load issued up front: entry e ↔ (e / kMaxU, e % kMaxU) of the padded block
+  constexpr int kPer = (kMaxU * kMaxU + 255) / 256;
+  const int tid = threadIdx.x;
+  double pv[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = min(tid + 256 * i, kMaxU * kMaxU - 1);
+    pv[i] = rec->Pend[e / kMaxU][e % kMaxU];
+  }
   const int nu = rec->nu;
-  if (threadIdx.x < kMaxU) su[threadIdx.x] = rec->u[threadIdx.x];
+  if (tid < kMaxU) su[tid] = rec->u[tid];
   __syncthreads();
-  if (threadIdx.x < nu) {
-    bool fp = true;
-    for (int k = 0; k < static_cast<int>(threadIdx.x); ++k) fp = fp && su[k] != su[threadIdx.x];
-    firstpos[threadIdx.x] = fp;
+  if (tid < kMaxU) {
+    int fp = tid < nu;
+    for (int k = 0; k < tid; ++k) fp = fp && su[k] != su[tid];
+    firstpos[tid] = fp;
   }
   __syncthreads();
   float* S = A.sig[d.parity ^ 1] + f * A.sig_stride;
-  for (int e = threadIdx.x; e < nu * nu; e += blockDim.x) {
-    const int a = e / nu, b = e - a * nu;
-    if (firstpos[a] && firstpos[b])
-      S[static_cast<size_t>(su[a]) * A.ld + su[b]] = static_cast<float>(rec->Pend[a][b]);
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = tid + 256 * i, a = e / kMaxU, b = e % kMaxU;
+    if (e < kMaxU * kMaxU && firstpos[a] && firstpos[b])
+      S[static_cast<size_t>(su[a]) * A.ld + su[b]] = static_cast<float>(pv[i]);
   }
 }
 
