@@ -65,6 +65,7 @@ struct ekf_ctx {
   void* mcat = nullptr;
   FilterCtl* ctl = nullptr;
   ChunkRec* rec = nullptr;
+  void* rows = nullptr;  // fp64: Σ_in[i, U] from a Σ pass to the next chunk's factor kernel
   MsgDesc* ddesc = nullptr;
   size_t sig_stride = 0, x_stride = 0, km_stride = 0;
   // host mirror
@@ -73,6 +74,8 @@ struct ekf_ctx {
   std::vector<char> pending;
   std::vector<int> prev_m;       // ≥ 0: last chunk was a pipelined pair (its record is valid)
   std::vector<std::array<int, kMaxChunk>> prev_ids;  // that chunk's landmark ids
+  std::vector<long> last_desc;   // plan_d index of the filter's last known-association chunk in
+                                 // the current (not yet uploaded) plan, −1: none
   // launch plan: descriptors for a whole call (or a whole replay) uploaded with ONE copy
   std::vector<MsgDesc> plan_d;
   std::vector<Launch> plan_l;
@@ -114,6 +117,8 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.ctl = h->ctl;
   a.rec = h->rec;
   a.rec_stride = static_cast<size_t>(h->F);
+  a.rows = static_cast<T*>(h->rows);
+  a.rows_stride = static_cast<size_t>(h->ldk) * kRowW;
   a.sync = h->sync;
   a.desc = desc;
   a.n = h->n;
@@ -298,12 +303,14 @@ int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
 
 // kLook descriptors: where each index of this chunk's U sits in the previous chunk's U' (the
 // chain's mapping: pose 0..2, marker c → 3+2·id, 4+2·id, a bad id → slot 0's columns 3, 4).
+int ucol(const int* ids, int a, int N) {
+  if (a < 3) return a;
+  const int id = ids[(a - 3) >> 1];
+  return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
+}
+
 void index_map(MsgDesc* d, int N) {
-  auto col = [N](const int* ids, int a) {
-    if (a < 3) return a;
-    const int id = ids[(a - 3) >> 1];
-    return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
-  };
+  auto col = [N](const int* ids, int a) { return ucol(ids, a, N); };
   const int nu = 3 + 2 * d->m, np = 3 + 2 * d->prev_m;
   d->nnew = 0;
   for (int a = 0; a < kMaxU + 1; ++a) {
@@ -352,6 +359,16 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
         d->z[i][1] = mk[b + i].zb;
       }
       if (flags & kLook) index_map(d, h->cfg.n_landmarks);
+      // fp64: the previous chunk's Σ pass (same plan, not uploaded yet) hands this chunk's factor
+      // kernel Σ_in[i, U] as contiguous rows instead of a gather strided by ld
+      if (h->rows && h->last_desc[f] >= 0 && m > 0) {
+        MsgDesc* pd = &h->plan_d[h->last_desc[f]];
+        pd->flags |= kRowsOut;
+        pd->nxt_nu = 3 + 2 * m;
+        for (int a = 0; a < kMaxU + 1; ++a) pd->nxt_u[a] = a < pd->nxt_nu ? ucol(d->ids, a, h->cfg.n_landmarks) : 0;
+        d->flags |= kRowsIn;
+      }
+      h->last_desc[f] = m > 0 ? static_cast<long>(off + k) : -1;
       h->prev_m[f] = m;
       for (int i = 0; i < m; ++i) h->prev_ids[f][i] = mk[b + i].id;
       h->parity[f] ^= 1;
@@ -380,6 +397,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
       }
       int flags = kActive | kNoInit;
       h->prev_m[f] = -1;  // association chunks run unpipelined
+      h->last_desc[f] = -1;
       if (i == 0 && (predict || h->pending[f])) flags |= kFirst;
       if (i == std::max(mf, 1) - 1 && posterior) flags |= kLast;
       const int m = mf > 0 ? 1 : 0;
@@ -399,6 +417,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
 
 void plan_posterior(ekf_ctx* h, int f) {
   h->prev_m[f] = -1;
+  h->last_desc[f] = -1;
   const size_t off = h->plan_d.size();
   h->plan_d.resize(off + 1);
   fill_desc(&h->plan_d[off], 0, kActive, h->parity[f], h->odom[f]);
@@ -473,6 +492,7 @@ int flush(ekf_ctx* h) {
   }
   h->plan_d.clear();
   h->plan_l.clear();
+  std::fill(h->last_desc.begin(), h->last_desc.end(), -1L);
   return rc;
 }
 
@@ -584,6 +604,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   h->parity.assign(h->F, 0);
   h->pending.assign(h->F, 0);
   h->prev_m.assign(h->F, -1);
+  h->last_desc.assign(h->F, -1L);
   h->prev_ids.assign(h->F, std::array<int, kMaxChunk>{});
   h->msgs.resize(h->F);
   auto fail = [&](int rc) {
@@ -609,6 +630,11 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipMalloc(&h->mcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->ctl, sizeof(FilterCtl) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->rec, 2 * sizeof(ChunkRec) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
+  const char* rows_env = std::getenv("EKF_ROWS");  // EKF_ROWS=0: always gather (tests)
+  if (cfg.dtype == EKF_F64 && !(rows_env && std::atoi(rows_env) == 0) &&
+      // fp32's U block is rewritten after its pass (k_pend_scatter): gathered there
+      hipMalloc(&h->rows, sizeof(double) * kRowW * h->ldk * h->F) != hipSuccess)
+    return fail(EKF_E_NOMEM);
   const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + h->F);
   if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
@@ -650,6 +676,7 @@ int ekf_destroy(ekf_t h) {
   if (h->mcat) hipFree(h->mcat);
   if (h->ctl) hipFree(h->ctl);
   if (h->rec) hipFree(h->rec);
+  if (h->rows) hipFree(h->rows);
   if (h->ddesc) hipFree(h->ddesc);
   for (int i = 0; i < kRing; ++i) {
     if (h->ring[i].p) hipHostFree(h->ring[i].p);
@@ -748,7 +775,7 @@ int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, cons
   return flush(h);
 }
 
-constexpr size_t kFlushDesc = 2048;
+constexpr size_t kFlushDesc = 8192;
 
 int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, const int* ids,
                const int* actions, const double* rel_xy, const double* odom, double* out_pose) {
@@ -889,6 +916,7 @@ int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, cons
   if (!valid(h, f)) return EKF_E_ARG;
   if (drain(h)) return EKF_E_HIP;
   h->prev_m[f] = -1;
+  h->last_desc[f] = -1;
   const int p = h->parity[f];
   if (state)
     HIPCHK(hipMemcpy(h->x[p] + f * h->x_stride, state, h->n * sizeof(double),

@@ -29,6 +29,11 @@ constexpr int kNoInit = 4;   // association path: no first-sighting init in the 
 constexpr int kActive = 8;   // filter takes part in this launch
 constexpr int kLook = 16;    // Σ_in not materialised yet: rebuild the chain's block from the
                              // previous chunk's Σ_in (other buffer) and ChunkRec
+constexpr int kRowsOut = 32; // Σ pass (fp64): also write Σ_out[i, U_next] to the rows buffer
+                             // (U_next = MsgDesc::nxt_u, the filter's next chunk's index set)
+constexpr int kRowsIn = 64;  // factor kernel: r(i) = Σ_in[i, U] from the rows buffer (written
+                             // by the previous chunk's Σ pass) instead of a strided gather
+constexpr int kRowW = kMaxU + 1;  // rows buffer: kRowW × ldk per filter (position-major)
 
 // One chunk of one message for one filter (uploaded by the host, read by every kernel of the pair).
 struct alignas(16) MsgDesc {
@@ -44,7 +49,9 @@ struct alignas(16) MsgDesc {
   int prev_ids[kMaxChunk];   // kLook: the previous chunk's ids (its index set U', known up front)
   signed char cpos[kMaxU + 1];  // kLook: position of U[a] in U' (−1: new to this chunk)
   int nnew;                     // kLook: count of cpos < 0
-  int pad2[2];
+  int nxt_nu;                   // kRowsOut: |U_next|
+  int pad2;
+  int nxt_u[kMaxU + 1];         // kRowsOut: U_next in the next chain's order (ekf_api index_map)
 };
 
 struct alignas(16) FilterCtl {

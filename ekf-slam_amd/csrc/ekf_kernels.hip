@@ -1431,9 +1431,17 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
     // every gather issued unconditionally (clamped index; padding u = 0 stays in bounds), then
     // masked: a predicated load would be a branch with its own wait, one round trip per load
     T raw[9];
-    const T r0t = rowp[0];
+    T r0t;
+    if (d.flags & kRowsIn) {  // Σ_in[i, U] written contiguously by the previous chunk's Σ pass
+      const T* rr = A.rows + f * A.rows_stride + (vi ? i : 0);  // [kRowW][ldk]: 16 rows = 128 B
+      r0t = rr[0];  // u_0 = 0
 #pragma unroll
-    for (int s = 0; s < 9; ++s) raw[s] = rowp[sh.u[min(4 * s + ks, kMaxU - 1)]];
+      for (int s = 0; s < 9; ++s) raw[s] = rr[static_cast<size_t>(4 * s + ks) * A.ldk];
+    } else {
+      r0t = rowp[0];
+#pragma unroll
+      for (int s = 0; s < 9; ++s) raw[s] = rowp[sh.u[min(4 * s + ks, kMaxU - 1)]];
+    }
     const double r0raw = vi ? static_cast<double>(r0t) : 0.0;
     const double ai = first ? alpha_of(i, sh.a1, sh.a2) : 0.0;
     double av[9];
@@ -1563,7 +1571,8 @@ struct SigmaTile<float> {
   static constexpr int kRows = 32, kCols = 32;
   static __device__ __forceinline__ void run(const float* Sin, float* Sout, const float* kc,
                                              const float* mc, int n, int ld, int ldk, int kw,
-                                             bool first, double qd, int R0, int C0, int lane) {
+                                             bool first, double qd, int R0, int C0, int lane,
+                                             float*, const int*, int, int*) {
     const int kr = lane >> 5, kcol = lane & 31;
     const unsigned sbytes = static_cast<unsigned>(n) * ld * 4u;
     const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 4u;
@@ -1606,15 +1615,19 @@ template <>
 struct SigmaTile<double> {
   static constexpr int kRows = 32, kCols = 16 * EKF_SIGMA64_TJ;
   static constexpr int TJ = EKF_SIGMA64_TJ;
+  // rows ≠ null (kRowsOut): also Σ_out[i, U_next] → rows[b·ldk + i] for the next chunk's factor
+  // kernel, b = the first position of the column in U_next (nxt[0..nnu))
   static __device__ __forceinline__ void run(const double* Sin, double* Sout, const double* kc,
                                              const double* mc, int n, int ld, int ldk, int kw,
-                                             bool first, double q, int R0, int C0, int lane) {
+                                             bool first, double q, int R0, int C0, int lane,
+                                             double* rows, const int* nxt, int nnu, int* map) {
     const int kr = lane >> 4, kcol = lane & 15;
     const unsigned sbytes = static_cast<unsigned>(n) * ld * 8u;
     const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 8u;
     const auto rin = buf_rsrc(Sin, sbytes), rout = buf_rsrc(Sout, sbytes);
     const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
     double a[2][9], b[TJ][9], sv[2][TJ][4];
+    const int uk = rows ? nxt[min(lane, kMaxU)] : 0;  // issued with the operand loads
     const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 8u;
     unsigned mo[TJ], so[TJ];
     const unsigned rstride = static_cast<unsigned>(ld) * 8u;
@@ -1654,6 +1667,20 @@ struct SigmaTile<double> {
       }
     }
     SIG_STAMP(2);
+    int bpos[TJ];
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) bpos[tj] = -1;
+    if (rows) {  // wave-uniform: positions of the tile's columns in U_next through this wave's LDS
+      map[lane] = kMaxU + 1;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (lane < nnu && uk >= C0 && uk < C0 + kCols) atomicMin(&map[uk - C0], lane);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) {
+        const int b = map[16 * tj + kcol];
+        bpos[tj] = b <= kMaxU ? b : -1;
+      }
+    }
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -1665,6 +1692,7 @@ struct SigmaTile<double> {
           if (first && row == col && row < 3) v += q;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rout,
                                                 so[tj] + (16 * ti + 4 * r) * rstride, 0, 0);
+          if (bpos[tj] >= 0 && row < n) rows[static_cast<size_t>(bpos[tj]) * ldk + row] = v;
         }
   }
 };
@@ -1685,6 +1713,7 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
     if (fb >= nf) return;
   }
   const MsgDesc& d = A.desc[fb];
+  __shared__ int cmap[4][64];  // per wave: kRowsOut column → position in U_next
   const int lane = threadIdx.x & 63;
   const int trows = (A.n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows;
   const int t = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1693,10 +1722,12 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
     const int f = A.f0 + fb;
     const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
     const int tr = t / tcols, tc = t - tr * tcols;
+    T* rows = (d.flags & kRowsOut) ? A.rows + f * A.rows_stride : nullptr;
     SigmaTile<T>::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
                       A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
                       (d.flags & kFirst) != 0, A.q, tr * SigmaTile<T>::kRows,
-                      tc * SigmaTile<T>::kCols, lane);
+                      tc * SigmaTile<T>::kCols, lane, rows, d.nxt_u, d.nxt_nu,
+                      cmap[threadIdx.x >> 6]);
   }
   SIG_STAMP(3);
 }

@@ -21,6 +21,8 @@ struct PassArgs {
   T* mcat;              // [KW][ldk] per filter (row k = one rank-1 factor over cols c)
   size_t km_stride;
   int ldk;
+  T* rows;              // fp64: [kRowW][ldk] per filter, Σ_in[i, U] handed from a Σ pass to the
+  size_t rows_stride;   // next chunk's factor kernel (kRowsOut / kRowsIn)
   FilterCtl* ctl;
   ChunkRec* rec;        // [2][rec_stride]: chunk records by Σ parity (chain → factors, next chain)
   size_t rec_stride;

@@ -343,3 +343,21 @@ def test_many_filters_match_small_batch(F, monkeypatch):
         assert cs == cb
         np.testing.assert_array_equal(xs, xb)
         np.testing.assert_array_equal(Ss, Sb)
+
+
+@pytest.mark.parametrize("F,env", [(1, {}), (4, {}), (40, {"EKF_DEVSYNC": "0"})],
+                         ids=["1filter", "4filters", "40filters_events"])
+def test_rows_handoff_is_bit_identical(monkeypatch, F, env):
+    """fp64: a Σ pass hands the next chunk's factor kernel Σ_in[i, U] as contiguous rows
+    (kRowsOut / kRowsIn) — the very values it stores into Σ_out, so the replay equals the strided
+    gather (EKF_ROWS=0) bit for bit, including messages longer than one chunk."""
+    sc = synth.synthetic(96, 14, max_markers=24)
+    assert sc.count.max() > 16  # some messages span two chunks
+    monkeypatch.delenv("EKF_ROWS", raising=False)
+    on = _pipelined_final(sc, monkeypatch, env, F=F)
+    monkeypatch.setenv("EKF_ROWS", "0")
+    off = _pipelined_final(sc, monkeypatch, env, F=F)
+    for (x1, S1, c1), (x0, S0, c0) in zip(on, off):
+        assert c1 == c0
+        np.testing.assert_array_equal(x1, x0)
+        np.testing.assert_array_equal(S1, S0)
