@@ -10,6 +10,7 @@
 
 using namespace ekfslam;
 static int g_pingpong = 0;
+static int g_m = 16;
 static unsigned* sync_buf(int nf) {  // device epochs (kSync*), zeroed
   unsigned* p = nullptr;
   const size_t bytes = sizeof(unsigned) * (kSyncChain + nf);
@@ -40,7 +41,7 @@ void run(int N, int F, int reps) {
   CK(hipMemcpy(kc, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
   CK(hipMemcpy(mc, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
   std::vector<MsgDesc> d(F);
-  for (int f = 0; f < F; ++f) { std::memset(&d[f], 0, sizeof(MsgDesc)); d[f].m = 16; d[f].flags = kActive | kFirst; }
+  for (int f = 0; f < F; ++f) { std::memset(&d[f], 0, sizeof(MsgDesc)); d[f].m = g_m; d[f].flags = kActive | kFirst; }
   MsgDesc* dd;  // [2][F]: parity 0 and parity 1 descriptors (ping-pong like the product)
   CK(hipMalloc(&dd, 2 * F * sizeof(MsgDesc)));
   CK(hipMemcpy(dd, d.data(), F * sizeof(MsgDesc), hipMemcpyHostToDevice));
@@ -120,6 +121,7 @@ void run(int N, int F, int reps) {
 
 int main(int argc, char** argv) {
   if (argc > 1) g_pingpong = atoi(argv[1]);
+  if (argc > 2) g_m = atoi(argv[2]);
   run<float>(1024, 1, 200);
   run<double>(1024, 1, 200);
   run<double>(256, 1, 200);
