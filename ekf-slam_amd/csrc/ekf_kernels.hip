@@ -1541,13 +1541,14 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
 //         → 4 rows × 128 B per instruction
 // A/B lane maps: 16x16x4 A[i = lane&15][k = lane>>4]; 32x32x2 A[i = lane&31][k = lane>>5].
 // Memory goes through buffer descriptors with 32-bit offsets (no 64-bit address per load):
-//   - Σ: the filter's n·ld elements; a row ≥ n lies past the end, a column ≥ n gets the offset
-//     kOOB, so the range check returns 0 for its loads and drops its stores (no masks, no waits);
+//   - Σ: the wave's 32-row panel (up to row n); a row ≥ n lies past the end, a column ≥ n gets
+//     the offset kOOB, so the range check returns 0 for its loads and drops its stores (no masks,
+//     no waits);
 //   - Kcat / Mcat: the factor rows are uniform (SGPR soffset), the lane's column in voffset.
 // Order: operands (L2-hot) first, then Σ_in. The MFMAs start from zero as soon as the operands
 // land and run while Σ_in is still in flight; Σ_in (+ Q̄) is added once, before the store.
 typedef float f16v __attribute__((ext_vector_type(16)));
-constexpr unsigned kOOB = 0x80000000u;  // voffset past any Σ descriptor (n·ld·w < 2 GiB)
+constexpr unsigned kOOB = 0x80000000u;  // voffset past any Σ panel descriptor (32·ld·w < 2 GiB)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
@@ -1574,9 +1575,12 @@ struct SigmaTile<float> {
                                              bool first, double qd, int R0, int C0, int lane,
                                              float*, const int*, int, int*) {
     const int kr = lane >> 5, kcol = lane & 31;
-    const unsigned sbytes = static_cast<unsigned>(n) * ld * 4u;
+    // descriptors based at the wave's row panel: offsets stay 32-bit for any n (a filter's Σ
+    // may exceed 4 GiB), and the records end at row n
+    const size_t pbase = static_cast<size_t>(R0) * ld;
+    const unsigned sbytes = static_cast<unsigned>(min(n - R0, kRows)) * ld * 4u;
     const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 4u;
-    const auto rin = buf_rsrc(Sin, sbytes), rout = buf_rsrc(Sout, sbytes);
+    const auto rin = buf_rsrc(Sin + pbase, sbytes), rout = buf_rsrc(Sout + pbase, sbytes);
     const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
     float a[18], b[18], sv[16];
     const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 4u;
@@ -1588,7 +1592,7 @@ struct SigmaTile<float> {
       b[s] = ld_f32(rm, mo, s * kstep);
     }
     const int col = C0 + kcol;
-    const unsigned so = col < n ? static_cast<unsigned>((R0 + 4 * kr) * ld + col) * 4u : kOOB;
+    const unsigned so = col < n ? static_cast<unsigned>(4 * kr * ld + col) * 4u : kOOB;
     const unsigned rstride = static_cast<unsigned>(ld) * 4u;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sv[r] = ld_f32(rin, so + ((r & 3) + 8 * (r >> 2)) * rstride, 0);
@@ -1622,9 +1626,12 @@ struct SigmaTile<double> {
                                              bool first, double q, int R0, int C0, int lane,
                                              double* rows, const int* nxt, int nnu, int* map) {
     const int kr = lane >> 4, kcol = lane & 15;
-    const unsigned sbytes = static_cast<unsigned>(n) * ld * 8u;
+    // descriptors based at the wave's row panel: offsets stay 32-bit for any n (a filter's Σ
+    // may exceed 4 GiB), and the records end at row n
+    const size_t pbase = static_cast<size_t>(R0) * ld;
+    const unsigned sbytes = static_cast<unsigned>(min(n - R0, kRows)) * ld * 8u;
     const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 8u;
-    const auto rin = buf_rsrc(Sin, sbytes), rout = buf_rsrc(Sout, sbytes);
+    const auto rin = buf_rsrc(Sin + pbase, sbytes), rout = buf_rsrc(Sout + pbase, sbytes);
     const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
     double a[2][9], b[TJ][9], sv[2][TJ][4];
     const int uk = rows ? nxt[min(lane, kMaxU)] : 0;  // issued with the operand loads
@@ -1635,7 +1642,7 @@ struct SigmaTile<double> {
     for (int tj = 0; tj < TJ; ++tj) {
       const int col = C0 + 16 * tj + kcol;
       mo[tj] = static_cast<unsigned>(kr * ldk + min(col, n - 1)) * 8u;
-      so[tj] = col < n ? static_cast<unsigned>((R0 + kr) * ld + col) * 8u : kOOB;
+      so[tj] = col < n ? static_cast<unsigned>(kr * ld + col) * 8u : kOOB;
     }
     const unsigned kstep = 4u * ldk * 8u;
 #pragma unroll

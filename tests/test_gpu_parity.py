@@ -361,3 +361,27 @@ def test_rows_handoff_is_bit_identical(monkeypatch, F, env):
         assert c1 == c0
         np.testing.assert_array_equal(x1, x0)
         np.testing.assert_array_equal(S1, S0)
+
+
+@pytest.mark.parametrize("name,dtype,N", [("basic_world_known", pyekf.EKF_F64, 12000),
+                                          ("basic_world_assoc", pyekf.EKF_F64, 12000)],
+                         ids=["known_n12000_fp64", "assoc_n12000_fp64"])
+def test_maximum_size_prefix_equals_golden(name, dtype, N):
+    """Size-independent property at a size whose Σ (n = 24 003, 4.6 GB per copy) is beyond 32-bit
+    byte offsets: unused landmark slots never touch the used part of the state (their cross
+    covariances stay exactly 0), so the N=50 golden fixture is a prefix of the N=12000 run. Same
+    tolerances as at N=50; the slots past the fixture's stay exactly 0."""
+    import dataclasses
+    sc, g = load_golden(name)
+    s = pyekf.Slam(n_landmarks=N, source=pyekf.SOURCE_ASSOC if bool(g["assoc"]) else
+                   pyekf.SOURCE_SIM, dtype=dtype, track=sc.track, radius=sc.radius)
+    rc, poses, tmo = s.replay(dataclasses.replace(sc, n_landmarks=N))
+    x, _, cnt = s.filter_state(sigma=False)
+    s.close()
+    assert rc == pyekf.EKF_OK
+    assert np.abs(poses - g["poses"]).max() < POSE_TOL
+    assert np.abs(tmo - g["tmo"]).max() < POSE_TOL
+    n0 = g["state"].shape[0]
+    assert np.abs(x[:n0] - g["state"]).max() < POSE_TOL
+    assert not np.any(x[n0:])
+    assert cnt == int(g["counter"])
