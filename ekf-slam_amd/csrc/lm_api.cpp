@@ -18,6 +18,7 @@ struct lm_ctx {
   int* d_counts = nullptr;
   lm_marker* d_markers = nullptr;
   int marker_cap = 0;  // markers per scan the device buffer holds
+  lmk::DetectWork work{};
   // lm_fit_circles / lm_check_circles staging (grown on demand)
   int* d_offs = nullptr;
   double* d_xy = nullptr;
@@ -80,7 +81,14 @@ int lm_create(lm_t* out, int max_scans, int max_beams, int device) {
   if (hipMalloc(&h->d_ranges, sizeof(float) * S * max_beams) != hipSuccess ||
       hipMalloc(&h->d_amin, sizeof(double) * S) != hipSuccess ||
       hipMalloc(&h->d_ainc, sizeof(double) * S) != hipSuccess ||
-      hipMalloc(&h->d_counts, sizeof(int) * S) != hipSuccess) {
+      hipMalloc(&h->d_counts, sizeof(int) * S) != hipSuccess ||
+      hipMalloc(&h->work.px, sizeof(double) * S * max_beams) != hipSuccess ||
+      hipMalloc(&h->work.py, sizeof(double) * S * max_beams) != hipSuccess ||
+      hipMalloc(&h->work.cand, sizeof(lmk::Cand) * lmk::candidate_capacity(max_scans, max_beams)) !=
+          hipSuccess ||
+      hipMalloc(&h->work.gcount, sizeof(int) * lmk::kRegions) != hipSuccess ||
+      hipMalloc(&h->work.sbase, sizeof(int) * S) != hipSuccess ||
+      hipMalloc(&h->work.sncand, sizeof(int) * S) != hipSuccess) {
     lm_destroy(h);
     return EKF_E_NOMEM;
   }
@@ -95,7 +103,10 @@ int lm_destroy(lm_t h) {
   for (void* p : {static_cast<void*>(h->d_ranges), static_cast<void*>(h->d_amin),
                   static_cast<void*>(h->d_ainc), static_cast<void*>(h->d_counts),
                   static_cast<void*>(h->d_markers), static_cast<void*>(h->d_offs),
-                  static_cast<void*>(h->d_xy), static_cast<void*>(h->d_out)})
+                  static_cast<void*>(h->d_xy), static_cast<void*>(h->d_out),
+                  static_cast<void*>(h->work.px), static_cast<void*>(h->work.py),
+                  static_cast<void*>(h->work.cand), static_cast<void*>(h->work.gcount),
+                  static_cast<void*>(h->work.sbase), static_cast<void*>(h->work.sncand)})
     if (p) hipFree(p);
   if (h->e0) hipEventDestroy(h->e0);
   if (h->e1) hipEventDestroy(h->e1);
@@ -127,7 +138,7 @@ int lm_detect(lm_t h, int S, int B, const float* ranges, const double* amin, con
     return EKF_E_HIP;
   if (hipEventRecord(h->e0, h->stream) != hipSuccess) return EKF_E_HIP;
   if (lmk::launch_detect(h->d_ranges, S, B, h->d_amin, h->d_ainc, thr, h->d_markers, cap,
-                         h->d_counts, h->stream) != hipSuccess)
+                         h->d_counts, h->work, h->stream) != hipSuccess)
     return EKF_E_HIP;
   if (hipEventRecord(h->e1, h->stream) != hipSuccess) return EKF_E_HIP;
   h->timed = true;

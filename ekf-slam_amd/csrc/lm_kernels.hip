@@ -2,13 +2,16 @@
 // nuslam/src/landmarks.cpp (getClusters :58-106, laserCallback :109-156) and
 // turtlelib/src/landmark_detection.cpp (checkCircle :5-48, fitCircle :50-135).
 //
-// k_detect: one wavefront per scan.
-//   1. beams → points in LDS (64 lanes stride the scan);
-//   2. break flags by ballot, break positions compacted in order (prefix popcount): cluster c is
-//      the run between breaks c−1 and c, the breaking point itself dropped (landmarks.cpp:81-86),
-//      the last run appended to cluster 0 when the scan closes on itself (:94-103);
-//   3. one lane per cluster: checkCircle, then the Hyper fit, numbered and compacted by ballot in
-//      cluster order (the marker id of :147 and the publish filter of :145).
+// lm_detect is three launches:
+//   k_clusters    one wavefront per scan: beams → points (LDS + global); break flags by ballot,
+//                 break positions compacted in order (prefix popcount): cluster c is the run
+//                 between breaks c−1 and c, the breaking point itself dropped (landmarks.cpp:81-86),
+//                 the last run appended to cluster 0 when the scan closes on itself (:94-103);
+//                 clusters of 4..39 points go to a dense batch-wide candidate list;
+//   k_candidates  one lane per candidate of the whole batch: checkCircle, then the Hyper fit (a
+//                 scan has ≈ 20 candidates, so per-scan lanes would leave two thirds of a wave idle);
+//   k_markers     one wavefront per scan: ids (index among circle clusters, :147) and the publish
+//                 filter (:145), compacted by ballot in cluster order.
 // The fit never forms ZᵀZ: Z (n × 4) is reduced row by row to its 4 × 4 R factor with Givens
 // rotations (orthogonal, registers only), the SVD of R comes from one-sided Jacobi (same singular
 // values and V as Z's), and the 4 × 4 eigenproblem of Q = Y·H⁻¹·Y from cyclic Jacobi. Y⁻¹ = V·S⁻¹·Vᵀ
@@ -30,6 +33,17 @@ constexpr double kMaxR = 0.2;       // landmarks.cpp:145
 constexpr double kMaxDist = 2.0;    // landmarks.cpp:145
 
 __device__ __forceinline__ double sq(double v) { return v * v; }  // std::pow(v, 2): exact square
+
+// 1/√x: hardware estimate + two Newton steps (≤ 1 ulp); replaces sqrt + two divisions in the
+// rotations of the fit, whose latency chain bounds the front-end (one lane per cluster)
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double e = fma(-h * y, y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-h * y, y, 0.5);
+  return fma(y, e, y);
+}
 
 // arma accumulate / mean: two interleaved accumulators (even, odd), then (acc1 + acc2) / n
 struct PairSum {
@@ -54,20 +68,19 @@ __device__ bool check_circle(int n, const P& pt) {
     return acos((c * c - a * a - b * b) / (-2.0 * a * b));
   };
   const int m = n - 2;
-  PairSum s;
-  for (int j = 1; j <= m; ++j) s.add(angle(j));
-  const double mean = s.sum() / m;  // arma::mean
-  double var = 0.0;                 // arma::stddev (N − 1), op_var::direct_var
-  if (m > 1) {
-    PairSum a2, a3;
-    for (int j = 1; j <= m; ++j) {
-      const double t = mean - angle(j);
-      a2.add(t * t);
-      a3.add(t);
-    }
-    // the pair sums of direct_var add tmpi² + tmpj² per pair; same terms, rounding-level order
-    var = (a2.sum() - a3.sum() * a3.sum() / m) / (m - 1);
+  // one pass (each acos once): sums of the angles shifted by the first one, then the mean and
+  // the N − 1 variance from them; the same quantities as arma::mean / op_var::direct_var (whose
+  // acc2, acc3 are these sums shifted by the mean), equal up to rounding of a 1e-16 relative size
+  const double k0 = angle(1);
+  PairSum s1, s2;
+  for (int j = 2; j <= m; ++j) {
+    const double t = angle(j) - k0;
+    s1.add(t);
+    s2.add(t * t);
   }
+  const double mean = k0 + s1.sum() / m;  // arma::mean
+  double var = 0.0;                       // arma::stddev (N − 1)
+  if (m > 1) var = (s2.sum() - s1.sum() * s1.sum() / m) / (m - 1);
   const double sd = sqrt(var);
   return sd < 0.2 && 1.3 < mean && mean < 2.6;
 }
@@ -77,9 +90,10 @@ __device__ __forceinline__ void givens_row(double (&R)[4][4], double (&w)[4]) {
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     if (w[c] != 0.0) {
-      const double r = sqrt(fma(R[c][c], R[c][c], w[c] * w[c]));
-      const double cs = R[c][c] / r, sn = w[c] / r;
-      R[c][c] = r;
+      const double r2 = fma(R[c][c], R[c][c], w[c] * w[c]);
+      const double ir = rsq_nr(r2);
+      const double cs = R[c][c] * ir, sn = w[c] * ir;
+      R[c][c] = r2 * ir;
 #pragma unroll
       for (int j = c + 1; j < 4; ++j) {
         const double t = R[c][j];
@@ -129,7 +143,7 @@ __device__ double3 fit_circle(int n, const P& pt) {
           rotated = true;
           const double zeta = (be - al) / (2.0 * ga);
           const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(fma(zeta, zeta, 1.0)));
-          const double cs = 1.0 / sqrt(fma(t, t, 1.0)), sn = cs * t;
+          const double cs = rsq_nr(fma(t, t, 1.0)), sn = cs * t;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const double bp = B[i][p], bq = B[i][q];
@@ -211,7 +225,7 @@ __device__ double3 fit_circle(int n, const P& pt) {
             rotated = true;
             const double th = (Q[q][q] - Q[p][p]) / (2.0 * apq);
             const double t = copysign(1.0, th) / (fabs(th) + sqrt(fma(th, th, 1.0)));
-            const double cs = 1.0 / sqrt(fma(t, t, 1.0)), sn = t * cs;
+            const double cs = rsq_nr(fma(t, t, 1.0)), sn = t * cs;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const double kp = Q[k][p], kq = Q[k][q];
@@ -289,6 +303,7 @@ __device__ double3 fit_circle(int n, const P& pt) {
 }
 
 // A cluster of the scan: up to two index runs (cluster 0 may wrap around the scan's end).
+// A cluster of the scan: up to two index runs (cluster 0 may wrap around the scan's end).
 struct Run2 {
   const double* px;
   const double* py;
@@ -304,25 +319,36 @@ __device__ __forceinline__ unsigned long long lanes_below() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-__global__ __launch_bounds__(64) void k_detect(const float* __restrict__ ranges, int nb_beams,
-                                              const double* __restrict__ amin,
-                                              const double* __restrict__ ainc, double thr,
-                                              lm_marker* __restrict__ out, int max_markers,
-                                              int* __restrict__ counts) {
+// Stage 1, one wavefront per scan: points (LDS and global), breaks, clusters; clusters of 4..39
+// points are appended, in cluster order, to the candidate list of region s mod kRegions (one
+// atomic per scan; a single counter for 4096 scans serialised ≈ 40 µs of same-address atomics).
+__global__ __launch_bounds__(64) void k_clusters(const float* __restrict__ ranges, int B,
+                                                const double* __restrict__ amin,
+                                                const double* __restrict__ ainc, double thr,
+                                                double* __restrict__ gpx, double* __restrict__ gpy,
+                                                Cand* __restrict__ cand, int* __restrict__ gcount,
+                                                int regcap, int* __restrict__ sbase,
+                                                int* __restrict__ sncand) {
   // dynamic LDS sized to the scan (B·20 bytes: 7.2 KB at 360 beams), so a CU holds many scans
   extern __shared__ double lds[];
   const int s = blockIdx.x, lane = threadIdx.x;
-  const int B = nb_beams;
   double* px = lds;
   double* py = lds + B;
   int* bpos = reinterpret_cast<int*>(lds + 2 * B);
   const float* rs = ranges + static_cast<size_t>(s) * B;
+  double* gx = gpx + static_cast<size_t>(s) * B;
+  double* gy = gpy + static_cast<size_t>(s) * B;
   const double a0 = amin[s], inc = ainc[s];
   for (int i = lane; i < B; i += 64) {  // landmarks.cpp:66-70
     const double r = static_cast<double>(rs[i]);
     const double a = normalize_angle(static_cast<double>(i) * inc) + a0;
-    px[i] = r * cos(a) - kLidarX;
-    py[i] = r * sin(a);
+    double sa, ca;
+    sincos(a, &sa, &ca);
+    const double x = r * ca - kLidarX, y = r * sa;
+    px[i] = x;
+    py[i] = y;
+    gx[i] = x;
+    gy[i] = y;
   }
   __syncthreads();
   int nb = 0;  // breaks, compacted in scan order (:78-86)
@@ -336,37 +362,109 @@ __global__ __launch_bounds__(64) void k_detect(const float* __restrict__ ranges,
   }
   __syncthreads();
   if (nb == 0) {  // clusters.at(0) on an empty list throws in the reference (:94)
-    if (lane == 0) counts[s] = LM_NO_BREAK;
+    if (lane == 0) sncand[s] = LM_NO_BREAK;
     return;
   }
   const bool merged = sqrt(sq(px[0] - px[B - 1]) + sq(py[0] - py[B - 1])) <= thr;  // :96
   const int ncl = merged ? nb : nb + 1;
-  int id_base = 0, pub_base = 0;
-  lm_marker* o = out + static_cast<size_t>(s) * max_markers;
+  auto cluster = [&](int c, int* s0, int* n0, int* s1) {  // cluster c's runs; returns its size
+    *s0 = c == 0 ? 0 : bpos[c - 1] + 1;
+    *n0 = (c == nb ? B : bpos[c]) - *s0;
+    *s1 = bpos[nb - 1] + 1;
+    const int n1 = (c == 0 && merged) ? B - *s1 : 0;
+    return *n0 + n1;
+  };
+  int total = 0;  // pass 1: how many candidates (:122, the size test)
   for (int cb = 0; cb < ncl; cb += 64) {
-    const int c = cb + lane;
-    Run2 g{px, py, 0, 0, 0};
-    int n = 0;
-    if (c < ncl) {
-      g.s0 = c == 0 ? 0 : bpos[c - 1] + 1;
-      g.n0 = (c == nb ? B : bpos[c]) - g.s0;
-      const int n1 = (c == 0 && merged) ? B - (bpos[nb - 1] + 1) : 0;
-      g.s1 = bpos[nb - 1] + 1;
-      n = g.n0 + n1;
+    int s0, n0, s1, n = 0;
+    if (cb + lane < ncl) n = cluster(cb + lane, &s0, &n0, &s1);
+    total += __popcll(__ballot(n > 3 && n < 40));
+  }
+  int base = 0;
+  const int reg = s % kRegions;
+  if (lane == 0) base = reg * regcap + atomicAdd(gcount + reg, total);
+  base = __shfl(base, 0);
+  if (lane == 0) {
+    sbase[s] = base;
+    sncand[s] = total;
+  }
+  int k = base;  // pass 2: the candidates, in cluster order
+  for (int cb = 0; cb < ncl; cb += 64) {
+    int s0 = 0, n0 = 0, s1 = 0, n = 0;
+    if (cb + lane < ncl) n = cluster(cb + lane, &s0, &n0, &s1);
+    const bool cd = n > 3 && n < 40;
+    const unsigned long long bal = __ballot(cd);
+    if (cd) {
+      Cand e;
+      e.scan = s;
+      e.s0 = s0;
+      e.n0 = n0;
+      e.s1 = s1;
+      e.n = n;
+      e.pass = 0;
+      e.cx = e.cy = e.r = 0.0;
+      cand[k + __popcll(bal & lanes_below())] = e;
     }
-    const bool cand = n > 3 && n < 40 && check_circle(n, g);  // :122-123
-    const unsigned long long bc = __ballot(cand);
+    k += __popcll(bal);
+  }
+}
+
+// Stage 2, one lane per candidate over the whole batch (dense per region): checkCircle, then the
+// Hyper fit.
+__global__ __launch_bounds__(64) void k_candidates(int B, const double* __restrict__ gpx,
+                                                  const double* __restrict__ gpy,
+                                                  Cand* __restrict__ cand,
+                                                  const int* __restrict__ gcount, int regcap) {
+  // lanes interleave the regions (lane → region idx mod kRegions, entry idx / kRegions), so the
+  // occupied entries of every region come first in the grid and the empty tail retires at once
+  const int idx = blockIdx.x * 64 + threadIdx.x;
+  const int reg = idx % kRegions, k = idx / kRegions;
+  if (k >= regcap || k >= gcount[reg]) return;
+  const int slot = reg * regcap + k;
+  Cand e = cand[slot];
+  const size_t o = static_cast<size_t>(e.scan) * B;
+  const Run2 g{gpx + o, gpy + o, e.s0, e.n0, e.s1};
+  e.pass = check_circle(e.n, g) ? 1 : 0;  // :123
+  if (e.pass) {
+    const double3 f = fit_circle(e.n, g);  // :144
+    e.cx = f.x;
+    e.cy = f.y;
+    e.r = f.z;
+  }
+  cand[slot] = e;
+}
+
+// Stage 3, one wavefront per scan: marker ids (index among circle clusters, :147) and the publish
+// filter (R < 0.2, centre within 2 m, :145), compacted by ballot in cluster order.
+__global__ __launch_bounds__(64) void k_markers(const Cand* __restrict__ cand,
+                                               const int* __restrict__ sbase,
+                                               const int* __restrict__ sncand,
+                                               lm_marker* __restrict__ out, int max_markers,
+                                               int* __restrict__ counts) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  const int nc = sncand[s];
+  if (nc < 0) {
+    if (lane == 0) counts[s] = LM_NO_BREAK;
+    return;
+  }
+  const Cand* cs = cand + sbase[s];
+  lm_marker* o = out + static_cast<size_t>(s) * max_markers;
+  int id_base = 0, pub_base = 0;
+  for (int cb = 0; cb < nc; cb += 64) {
+    Cand e;
+    e.pass = 0;
+    if (cb + lane < nc) e = cs[cb + lane];
+    const bool cand_ok = e.pass != 0;
+    const unsigned long long bc = __ballot(cand_ok);
     const int id = id_base + __popcll(bc & lanes_below());
-    double3 f = make_double3(0.0, 0.0, 0.0);
-    if (cand) f = fit_circle(n, g);
-    const bool pub = cand && f.z < kMaxR && sqrt(sq(f.x) + sq(f.y)) < kMaxDist;  // :145
+    const bool pub = cand_ok && e.r < kMaxR && sqrt(sq(e.cx) + sq(e.cy)) < kMaxDist;
     const unsigned long long bp = __ballot(pub);
     const int slot = pub_base + __popcll(bp & lanes_below());
     if (pub && slot < max_markers) {
       lm_marker m;
-      m.x = f.x;
-      m.y = f.y;
-      m.r = f.z;
+      m.x = e.cx;
+      m.y = e.cy;
+      m.r = e.r;
       m.id = id;
       m.pad = 0;
       o[slot] = m;
@@ -407,9 +505,17 @@ __global__ __launch_bounds__(64) void k_check(int nc, const int* __restrict__ of
 
 hipError_t launch_detect(const float* ranges, int S, int B, const double* amin,
                          const double* ainc, double thr, lm_marker* out, int max_markers,
-                         int* counts, hipStream_t st) {
+                         int* counts, const DetectWork& w, hipStream_t st) {
+  if (hipMemsetAsync(w.gcount, 0, sizeof(int) * kRegions, st) != hipSuccess)
+    return hipErrorUnknown;
+  const int regcap = (S + kRegions - 1) / kRegions * max_candidates(B);
   const size_t lds = static_cast<size_t>(B) * (2 * sizeof(double) + sizeof(int));
-  hipLaunchKernelGGL(k_detect, dim3(S), dim3(64), lds, st, ranges, B, amin, ainc, thr, out,
+  hipLaunchKernelGGL(k_clusters, dim3(S), dim3(64), lds, st, ranges, B, amin, ainc, thr, w.px,
+                     w.py, w.cand, w.gcount, regcap, w.sbase, w.sncand);
+  const size_t cap = static_cast<size_t>(kRegions) * regcap;  // bound of the regions' lists
+  hipLaunchKernelGGL(k_candidates, dim3((cap + 63) / 64), dim3(64), 0, st, B, w.px, w.py, w.cand,
+                     w.gcount, regcap);
+  hipLaunchKernelGGL(k_markers, dim3(S), dim3(64), 0, st, w.cand, w.sbase, w.sncand, out,
                      max_markers, counts);
   return hipGetLastError();
 }
