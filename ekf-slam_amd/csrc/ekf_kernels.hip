@@ -1594,14 +1594,21 @@ struct SigmaTile<float> {
     const int col = C0 + kcol;
     const unsigned so = col < n ? static_cast<unsigned>(4 * kr * ld + col) * 4u : kOOB;
     const unsigned rstride = static_cast<unsigned>(ld) * 4u;
+    // keep the operand loads ahead of Σ_in's: the MFMAs then wait for vmcnt(16), not vmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < 16; ++r) sv[r] = ld_f32(rin, so + ((r & 3) + 8 * (r >> 2)) * rstride, 0);
     f16v acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    // every MFMA issued, factor rows ≥ kw (stale) zeroed by a select: a branch per k-step let
+    // the compiler sink each operand load into its branch behind a vmcnt(0)
 #pragma unroll
-    for (int s = 0; s < 18; ++s)
-      if (2 * s < kw) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+    for (int s = 0; s < 18; ++s) {
+      const bool live = 2 * s < kw;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(live ? a[s] : 0.0f, live ? b[s] : 0.0f, acc, 0,
+                                                 0, 0);
+    }
     SIG_STAMP(2);
     const float q = static_cast<float>(qd);
 #pragma unroll
@@ -1665,13 +1672,13 @@ struct SigmaTile<double> {
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = d4{0, 0, 0, 0};
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      if (4 * s < kw) {
+    for (int s = 0; s < 9; ++s) {  // unconditional, stale rows ≥ kw zeroed (see the fp32 tile)
+      const bool live = 4 * s < kw;
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti)
+      for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-          for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = mfma_f64(a[ti][s], b[tj][s], acc[ti][tj]);
-      }
+        for (int tj = 0; tj < TJ; ++tj)
+          acc[ti][tj] = mfma_f64(live ? a[ti][s] : 0.0, live ? b[tj][s] : 0.0, acc[ti][tj]);
     }
     SIG_STAMP(2);
     int bpos[TJ];
@@ -1723,7 +1730,9 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
   __shared__ int cmap[4][64];  // per wave: kRowsOut column → position in U_next
   const int lane = threadIdx.x & 63;
   const int trows = (A.n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows;
-  const int t = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // the wave's tile index, provably wave-uniform (readfirstlane): the buffer descriptors built
+  // from it stay in SGPRs instead of a waterfall loop around every buffer access
+  const int t = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if ((d.flags & kActive) && t < trows * tcols) {
     SIG_STAMP(1);
     const int f = A.f0 + fb;
