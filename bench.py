@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ekf-slam_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# dense MFMA peaks: fp32 157.3 TF (MI355X_MICROARCH.md); fp64 78.6 TF (AMD MI355X spec sheet)
+MFMA_PEAK_TF = {"f32": 157.3, "f64": 78.6}
 WORKLOADS = {
     # name: (N landmarks, dtype, filters per GPU, markers per message, BASELINE config)
     "n1024_fp32": (1024, "f32", 1, 16, "configs[2]: N=1024 synthetic landmarks, 1 filter, fp32"),
@@ -53,11 +55,10 @@ def parse():
     return p.parse_args()
 
 
-def pmc_traffic(args):
-    """HBM-side bytes per k_sigma_pass launch from PMC counters (MI355X_MICROARCH.md, HBM):
-    FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes (they do not fit one pass), FETCH_SIZE
-    doubled on gfx950. Runs short child benches before this process touches the GPU; any failure
-    gives None with the reason (a measurement gap, never a different compute path)."""
+def _pmc_pass(args, counters):
+    """One rocprofv3 --pmc pass (its own child bench run, every kernel on one stream so each
+    dispatch's counters are its own) → {counter: mean over k_sigma_pass dispatches}, or an error
+    string. Child runs happen before this process touches the GPU."""
     import csv
     import glob
     import shutil
@@ -66,39 +67,66 @@ def pmc_traffic(args):
     exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(exe):
         return None, "rocprofv3 not found"
-    vals = {}
     # the workload's own instantiation (the fp32 workload's fp64 warm-up lap is excluded)
     kname = "k_sigma_pass<float>" if WORKLOADS[args.workload][1] == "f32" else "k_sigma_pass<double>"
+    d = tempfile.mkdtemp(prefix="ekf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [exe, "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--workload", args.workload,
+           "--steps", "8", "--warmup", "2", "--no-cpu", "--traffic", "off"]
+    env = dict(os.environ, EKF_SERIAL="1")
+    name = " ".join(counters)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    except subprocess.TimeoutExpired:
+        return None, f"rocprofv3 --pmc {name} timed out"
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if r.returncode != 0 or not files:
+        return None, f"rocprofv3 --pmc {name} failed (rc {r.returncode})"
+    per = {c: {} for c in counters}
+    with open(files[0]) as fh:
+        for row in csv.DictReader(fh):
+            c = row.get("Counter_Name")
+            if kname in row.get("Kernel_Name", "") and c in per:
+                key = row.get("Dispatch_Id", row.get("Correlation_Id", len(per[c])))
+                per[c][key] = per[c].get(key, 0.0) + float(row["Counter_Value"])
+    shutil.rmtree(d, ignore_errors=True)
+    if not all(per[c] for c in counters):
+        return None, f"no k_sigma_pass dispatches with {name}"
+    return {c: float(np.mean(list(per[c].values()))) for c in counters}, None
+
+
+def pmc_traffic(args):
+    """HBM-side bytes per k_sigma_pass launch from PMC counters (MI355X_MICROARCH.md, HBM):
+    FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes (they do not fit one pass), FETCH_SIZE
+    doubled on gfx950; then MFMA-busy cycles beside GRBM_GUI_ACTIVE in a third pass. Any failure
+    gives None with the reason (a measurement gap, never a different compute path)."""
+    vals = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = tempfile.mkdtemp(prefix="ekf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [exe, "--pmc", counter, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
-               sys.executable, os.path.abspath(__file__), "--workload", args.workload,
-               "--steps", "8", "--warmup", "2", "--no-cpu", "--traffic", "off"]
-        env = dict(os.environ, EKF_SERIAL="1")  # one stream: counters belong to one dispatch
-        try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
-        except subprocess.TimeoutExpired:
-            return None, f"rocprofv3 --pmc {counter} timed out"
-        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-        if r.returncode != 0 or not files:
-            return None, f"rocprofv3 --pmc {counter} failed (rc {r.returncode})"
-        per = []
-        with open(files[0]) as fh:
-            for row in csv.DictReader(fh):
-                if kname in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
-                    per.append(float(row["Counter_Value"]))
-        shutil.rmtree(d, ignore_errors=True)
-        if not per:
-            return None, f"no k_sigma_pass dispatches with {counter}"
-        vals[counter] = float(np.mean(per))
+        v, err = _pmc_pass(args, [counter])
+        if v is None:
+            return None, err
+        vals.update(v)
     # counters are in KB (rocprofv3 derived FETCH_SIZE / WRITE_SIZE)
     fetch = 2.0 * vals["FETCH_SIZE"] * 1024.0
     write = vals["WRITE_SIZE"] * 1024.0
-    return {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
-            "note": "FETCH_SIZE x2 (gfx950 correction, calibrated for this kernel's loads in "
-                    "profiles/r1/pmc_calibration.md) + WRITE_SIZE; separate --pmc passes over a "
-                    "short child run with every kernel on one stream (EKF_SERIAL=1); mean over "
-                    "k_sigma_pass dispatches"}, None
+    out = {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+           "note": "FETCH_SIZE x2 (gfx950 correction, calibrated for this kernel's loads in "
+                   "profiles/r1/pmc_calibration.md) + WRITE_SIZE; separate --pmc passes over a "
+                   "short child run with every kernel on one stream (EKF_SERIAL=1); mean over "
+                   "k_sigma_pass dispatches"}
+    v, err = _pmc_pass(args, ["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"])
+    if v is None:
+        out["mfma_busy"] = err
+    else:
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md); the MFMA-busy cycles
+        # over every SIMD: busy ÷ (kernel cycles × 256 CUs × 4 SIMDs)
+        # (GRBM_GUI_ACTIVE spans the whole counter-collection window of a dispatch, several times
+        # the kernel; main() divides the busy cycles by the event-timed duration instead)
+        out["mfma_busy"] = {"SQ_VALU_MFMA_BUSY_CYCLES": v["SQ_VALU_MFMA_BUSY_CYCLES"],
+                            "GRBM_GUI_ACTIVE": v["GRBM_GUI_ACTIVE"],
+                            "note": "SQ_VALU_MFMA_BUSY_CYCLES summed over the SIMDs, per "
+                                    "k_sigma_pass dispatch; one --pmc pass, same child run shape"}
+    return out, None
 
 
 def build_inputs(N, F, msgs, seed, m):
@@ -267,11 +295,17 @@ def main():
     avg_sig_s = ms_sig / max(n_sig, 1) / 1e3
     achieved = bytes_per_launch / avg_sig_s / 1e9 if n_sig else 0.0
 
+    if traffic and isinstance(traffic.get("mfma_busy"), dict) and n_sig:
+        # busy SIMD-cycles over what 1024 SIMDs offer in the event-timed launch at the 2.4 GHz
+        # maximum clock (the chip runs slower under load, so this is a lower bound)
+        mb = traffic["mfma_busy"]
+        mb["busy_frac_at_max_clock"] = mb["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg_sig_s * 2.4e9 * 1024)
     result = None
     if rank == 0:
         value = total_corr / elapsed
         wsz = 4 if dt == "f32" else 8
         n = 3 + 2 * N
+        mfma_flops = 2.0 * (2 + 2 * m) * n * n * F  # the rank-(2+2m) update's useful flops
         result = {
             "metric": "EKF correction steps/sec at N landmarks; pose RMSE vs reference",
             "value": value,
@@ -297,6 +331,12 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "bytes_formula": f"2*n^2*w*F = 2*{n}^2*{wsz}*{F}",
                 "avg_launch_us": avg_sig_s * 1e6, "launches": n_sig,
+                "mfma": {"flops_per_launch": mfma_flops,
+                         "achieved_tflops": mfma_flops / avg_sig_s / 1e12 if n_sig else 0.0,
+                         "peak_tflops": MFMA_PEAK_TF[dt],
+                         "frac": mfma_flops / avg_sig_s / 1e12 / MFMA_PEAK_TF[dt] if n_sig else 0.0,
+                         "formula": f"2*(2+2m)*n^2*F = 2*{2 + 2 * m}*{n}^2*{F}",
+                         "pmc": traffic.get("mfma_busy") if traffic else traffic_err},
                 "chain_kernel_avg_us": ms_gain / max(n_gain, 1) * 1e3,
                 "factor_kernel_avg_us": ms_fac / max(n_fac, 1) * 1e3,
             },
