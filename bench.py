@@ -44,8 +44,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--workload", default="n1024_fp32", choices=sorted(WORKLOADS) + ["frontend"],
-                   help="frontend: the landmark front-end (include/landmarks.h), scans/s")
+    p.add_argument("--workload", default="n1024_fp32",
+                   choices=sorted(WORKLOADS) + ["frontend", "rosbag_surrogate"],
+                   help="frontend: the landmark front-end (include/landmarks.h), scans/s; "
+                        "rosbag_surrogate: configs[4]'s shape, scans → detect → slam node")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--cpu-messages", type=int, default=3,
                    help="messages in the CPU baseline sample (literal dense)")
@@ -215,10 +217,81 @@ def frontend_main(args):
     det.close()
 
 
+def rosbag_main(args):
+    """BASELINE configs[4] surrogate (the bag's .mcap payload is missing from the reference
+    snapshot; synth.lidar_world has its shape: 426 scans at 5 Hz, 20 odometry ticks per scan,
+    20 obstacles): one step = the whole 87 s drive — lm_detect over the 426 scans (one batch) and
+    the slam node's loop (joint states, unknown-association MarkerArrays) natively (slam_replay),
+    fp64, N = 50 slots. value = corrections/s; parity = pose trace vs the CPU pipeline
+    (landmarks_numpy.laser_callback → the C oracle's node loop); the CPU pipeline's time is the
+    cpu_baseline."""
+    import math as _m
+    import pyekf
+    from pyekf import synth
+    from pyekf.landmarks import Detector
+    sc, obs, scans = synth.lidar_world()
+    T = len(scans)
+    inc = float(np.float32(2 * _m.pi / 360))
+    det = Detector(max_scans=T, max_beams=360)
+
+    def gpu_run(trace):
+        cnt, mk = det.detect(scans, np.zeros(T), np.full(T, inc))
+        scg = synth.with_markers(sc, [[(m["x"], m["y"]) for m in mk[t, :cnt[t]]]
+                                      for t in range(T)])
+        s = pyekf.Slam(n_landmarks=50, source=pyekf.SOURCE_ASSOC)
+        _, poses, _ = s.replay(scg, poses=trace)  # trace: read every posterior back (syncs)
+        s.filter_state(sigma=False)               # the drive's end: synchronises
+        s.close()
+        return scg, poses
+    for _ in range(max(args.warmup, 1)):
+        gpu_run(False)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        scg, _ = gpu_run(False)
+    dt = (time.perf_counter() - t0) / args.steps
+    scg, poses = gpu_run(True)  # the pose trace for parity, untimed
+    det.close()
+    corr = int(scg.count.sum())
+    tr = sc.truth.copy()
+    tr[:, 1] -= 1.0  # the map frame starts at the drive's start pose (θ0 = 0, x0 = 1)
+    result = {
+        "metric": "EKF correction steps/sec at N landmarks; pose RMSE vs reference",
+        "value": corr / dt, "unit": "corrections/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic surrogate of rosbag2_2024_03_17-18_35_57 (payload missing)",
+        "config": {"workload": "rosbag_surrogate", "baseline_config": "configs[4] (surrogate)",
+                   "scans": T, "obstacles": len(obs), "n_landmarks": 50,
+                   "markers": corr, "association": "unknown (sensor_cb)",
+                   "step": "lm_detect batch + 426 slam_markers messages with wheel ticks"},
+        "pose_rmse_vs_truth_m": float(np.sqrt(np.mean(np.sum((poses[:, 1:] - tr[:, 1:]) ** 2,
+                                                               1)))),
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import landmarks_numpy as L  # noqa: E402  (cpu_baseline / parity legs only)
+        orc = _oracle()
+        t0 = time.perf_counter()
+        cpu_mk = [[(w[1], w[2]) for w in L.laser_callback(scans[t], 0.0, inc)] for t in range(T)]
+        o = orc.run_scenario(synth.with_markers(sc, cpu_mk), True)
+        cdt = time.perf_counter() - t0
+        d = poses - o["poses"]
+        result["parity"] = {"pose_rmse_m": float(np.sqrt(np.mean(d[:, 1] ** 2 + d[:, 2] ** 2))),
+                            "heading_rmse_rad": float(np.sqrt(np.mean(np.arctan2(
+                                np.sin(d[:, 0]), np.cos(d[:, 0])) ** 2))),
+                            "messages": T, "vs": "laser_callback (numpy) → C oracle node loop"}
+        result["cpu_baseline"] = {"value": corr / cdt, "unit": "corrections/s", "cores": 1,
+                                  "kind": "port", "sample": f"the whole drive: numpy front-end + "
+                                  f"C oracle (O(n^2)), {corr} corrections in {cdt:.2f} s"}
+    print(json.dumps(result))
+
+
 def main():
     args = parse()
     if args.workload == "frontend":
         return frontend_main(args)
+    if args.workload == "rosbag_surrogate":
+        return rosbag_main(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

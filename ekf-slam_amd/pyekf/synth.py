@@ -199,3 +199,42 @@ def lidar_scans(poses, circles, arena=(10.0, 5.0), n_beams=360, sigma=0.0, seed=
     if sigma > 0.0:
         best = best + np.random.default_rng(seed).normal(0.0, sigma, best.shape)
     return best.astype(np.float32)
+
+
+def lidar_world(n_scans: int = 426, n_obstacles: int = 20, seed: int = 20240317,
+                arena=(5.0, 4.0), obstacle_r: float = 0.038, sigma: float = 1e-3):
+    """Surrogate of BASELINE configs[4] (the rosbag2_2024_03_17-18_35_57 replay, whose .mcap payload
+    is missing from the reference snapshot): the bag's shape — 87 s, 426 lidar scans at ≈ 5 Hz,
+    ≈ 20 odometry ticks per scan, ≈ 20 landmarks (metadata.yaml:11-174) — as a unit-circle drive
+    at 0.2 rad/s through ``n_obstacles`` cylinders, 360-beam scans by ``lidar_scans``.
+    Returns (scenario with wheel ticks and truth, obstacles [(x, y, r)], scans float32 [T, 360])."""
+    rng = np.random.default_rng(seed + 104729)
+    obs = []
+    while len(obs) < n_obstacles:
+        p = rng.uniform([-arena[0] / 2 + 0.5, -arena[1] / 2 + 0.5],
+                        [arena[0] / 2 - 0.5, arena[1] / 2 - 0.5])
+        if abs(math.hypot(p[0], p[1]) - 1.0) < 0.35:
+            continue
+        if all(math.hypot(p[0] - q[0], p[1] - q[1]) > 0.5 for q in obs):
+            obs.append((float(p[0]), float(p[1]), obstacle_r))
+    lm = np.array([(x, y) for x, y, _ in obs])
+    sc = make_scenario(50, lm, n_scans, circle_radius=1.0, omega=0.2, tick_hz=100.0,
+                       ticks_per_msg=20, nearest=False, start_pose=(0.0, 1.0, 0.0), seed=seed)
+    scans = lidar_scans(sc.truth, obs, arena=arena, n_beams=360, sigma=sigma, seed=seed + 1)
+    return sc, obs, scans
+
+
+def with_markers(sc: Scenario, markers) -> Scenario:
+    """The scenario's drive with unknown-association marker arrays ``markers`` (per message a list
+    of body-frame (x, y)) in place of its fake-sensor ones (the `landmarks` node's output feeding
+    sensor_cb)."""
+    T = sc.n_messages
+    M = max(1, max(len(m) for m in markers))
+    rel = np.zeros((T, M, 2))
+    count = np.zeros(T, dtype=np.int32)
+    for t, m in enumerate(markers):
+        count[t] = len(m)
+        if len(m):
+            rel[t, :len(m)] = np.asarray(m, dtype=np.float64).reshape(-1, 2)
+    return Scenario(sc.n_landmarks, sc.landmarks, sc.wheel, np.full((T, M), -1, np.int32),
+                    np.zeros((T, M), np.int32), rel, count, sc.truth, sc.track, sc.radius)

@@ -66,3 +66,32 @@ def test_scan_to_posterior_matches_oracles():
     assert np.abs(S - Sr).max() < 1e-6 * max(1.0, np.abs(Sr).max() / 1e7)
     det.close()
     ekf.close()
+
+
+def test_rosbag_surrogate_pose_trace_matches_cpu():
+    """BASELINE configs[4] surrogate (the bag's .mcap payload is missing; synth.lidar_world has its
+    shape: 426 scans at 5 Hz, 20 odometry ticks per scan, 20 obstacles): scans → lm_detect →
+    slam node (joint states + unknown-association MarkerArrays, slam_replay) on the GPU, against
+    laser_callback → the C oracle's node loop. Pose trace within 1e-8 of the CPU pipeline."""
+    import pyekf
+    from pyekf import synth
+    from pyekf.landmarks import Detector
+    sc, _, scans = synth.lidar_world()
+    T = len(scans)
+    inc = float(np.float32(2 * math.pi / 360))
+    det = Detector(max_scans=T, max_beams=360)
+    cnt, mk = det.detect(scans, np.zeros(T), np.full(T, inc))
+    det.close()
+    gpu_mk = [[(m["x"], m["y"]) for m in mk[t, :cnt[t]]] for t in range(T)]
+    cpu_mk = [[(w[1], w[2]) for w in L.laser_callback(scans[t], 0.0, inc)] for t in range(T)]
+    for g, c in zip(gpu_mk, cpu_mk):
+        assert len(g) == len(c)
+        assert np.abs(np.array(g) - np.array(c)).max(initial=0.0) < 1e-9
+    s = pyekf.Slam(n_landmarks=50, source=pyekf.SOURCE_ASSOC)
+    rc, poses, tmo = s.replay(synth.with_markers(sc, gpu_mk))
+    _, _, counter = s.filter_state(sigma=False)
+    s.close()
+    o = orc.run_scenario(synth.with_markers(sc, cpu_mk), True)
+    assert counter == o["counter"] >= 10
+    assert np.abs(poses - o["poses"]).max() < 1e-8
+    assert np.abs(tmo - o["tmo"]).max() < 1e-8
