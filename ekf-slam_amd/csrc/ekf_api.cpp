@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <array>
 #include <cstdlib>
 #include <cmath>
@@ -46,6 +47,8 @@ struct ProfEvents {
 
 }  // namespace
 
+static_assert(EKF_RESIDENT_MAX_N == kResidentMaxN, "ekf.h and ekf_launch.hpp agree");
+
 struct ekf_ctx {
   ekf_config cfg{};
   int n = 0, ld = 0, ldk = 0, F = 0;
@@ -53,6 +56,7 @@ struct ekf_ctx {
   hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
+  bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
   hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
   bool devsync = false;                   // streams synchronise through device epochs
@@ -87,11 +91,11 @@ struct ekf_ctx {
   std::vector<std::vector<Marker>> msgs;
   // profiling
   bool prof = false;
-  ProfEvents pe[4];
+  ProfEvents pe[5];
   std::vector<hipEvent_t> pool;
-  long long prof_launches[4] = {0, 0, 0, 0};
+  long long prof_launches[5] = {0, 0, 0, 0, 0};
   long long prof_chunks = 0;  // chunks the timed chain launches walked
-  double prof_ms[4] = {0, 0, 0, 0};
+  double prof_ms[5] = {0, 0, 0, 0, 0};
 };
 
 #define HIPCHK(expr)                       \
@@ -143,7 +147,7 @@ hipEvent_t pool_get(ekf_ctx* h) {
 }
 
 // Launch `fn` bracketed by events when profiling (kind 0 = Σ pass, 1 = chain, 2 = association,
-// 3 = factors).
+// 3 = factors, 4 = resident filter kernel).
 template <typename Fn>
 int timed(ekf_ctx* h, int kind, hipStream_t st, Fn fn) {
   (void)st;
@@ -432,8 +436,60 @@ int posterior_launch(ekf_ctx* h, const MsgDesc* dp, int f0, int nf) {
   return e == hipSuccess ? EKF_OK : EKF_E_HIP;
 }
 
+// Resident path: the plan's descriptors and its entry list (packed behind them, in MsgDesc-sized
+// slots) go up with one copy, then ONE kernel launch runs the whole plan, a workgroup per filter.
+int flush_resident(ekf_ctx* h) {
+  const size_t nd = h->plan_d.size(), nl = h->plan_l.size();
+  if (nl == 0) return EKF_OK;
+  const size_t pslots = (nl * sizeof(PlanEntry) + sizeof(MsgDesc) - 1) / sizeof(MsgDesc);
+  const size_t ns = nd + pslots;
+  if (ns > h->ddesc_cap) {  // the previous launch may still read the old buffer
+    if (drain(h)) return EKF_E_HIP;
+    if (h->ddesc) HIPCHK(hipFree(h->ddesc));
+    h->ddesc = nullptr;
+    const size_t cap = std::max(ns, 2 * h->ddesc_cap);
+    if (hipMalloc(&h->ddesc, cap * sizeof(MsgDesc)) != hipSuccess) return EKF_E_NOMEM;
+    h->ddesc_cap = cap;
+  }
+  StageSlot& sl = h->ring[h->ring_next];
+  h->ring_next = (h->ring_next + 1) % kRing;
+  if (sl.used) HIPCHK(hipEventSynchronize(sl.ev));
+  if (ns > sl.cap) {
+    if (sl.p) HIPCHK(hipHostFree(sl.p));
+    sl.p = nullptr;
+    const size_t cap = std::max<size_t>(ns, 64);
+    if (hipHostMalloc(reinterpret_cast<void**>(&sl.p), cap * sizeof(MsgDesc),
+                      hipHostMallocDefault) != hipSuccess)
+      return EKF_E_NOMEM;
+    sl.cap = cap;
+  }
+  std::memcpy(sl.p, h->plan_d.data(), nd * sizeof(MsgDesc));
+  PlanEntry* pe = reinterpret_cast<PlanEntry*>(sl.p + nd);
+  int flo = INT_MAX, fhi = 0;
+  for (size_t i = 0; i < nl; ++i) {
+    const Launch& L = h->plan_l[i];
+    pe[i] = PlanEntry{static_cast<int>(L.off), L.f0, L.nf, L.kind};
+    flo = std::min(flo, L.f0);
+    fhi = std::max(fhi, L.f0 + L.nf);
+  }
+  HIPCHK(hipMemcpyAsync(h->ddesc, sl.p, ns * sizeof(MsgDesc), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipEventRecord(sl.ev, h->stream));
+  sl.used = true;
+  const PassArgs<double> a = args<double>(h, h->ddesc, 0);
+  const PlanEntry* dplan = reinterpret_cast<const PlanEntry*>(h->ddesc + nd);
+  const int rc = timed(h, 4, h->stream, [&](hipEvent_t e0, hipEvent_t e1) {
+    return launch_resident(a, dplan, static_cast<int>(nl), flo, fhi - flo, h->stream, e0, e1);
+  });
+  h->plan_d.clear();
+  h->plan_l.clear();
+  std::fill(h->last_desc.begin(), h->last_desc.end(), -1L);
+  std::fill(h->prev_m.begin(), h->prev_m.end(), -1);
+  return rc;
+}
+
 // Upload the whole plan with one copy, then enqueue its launches in order.
 int flush(ekf_ctx* h) {
+  if (h->resident) return flush_resident(h);
   const size_t nd = h->plan_d.size();
   if (nd == 0) return EKF_OK;
   if (nd > h->ddesc_cap) {  // grow the device descriptor buffer (kernels may still read the old one)
@@ -613,6 +669,10 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   };
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
   if (const char* e = std::getenv("EKF_SERIAL")) h->serial = std::atoi(e) != 0;
+  {  // EKF_RESIDENT=0: the HBM pipeline at every size (tests compare the two)
+    const char* e = std::getenv("EKF_RESIDENT");
+    h->resident = cfg.dtype == EKF_F64 && h->n <= kResidentMaxN && !(e && std::atoi(e) == 0);
+  }
   if (create_streams(h) != EKF_OK ||
       hipEventCreateWithFlags(&h->ev_chain, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -703,6 +763,12 @@ int ekf_dims(ekf_t h, int* n, int* ld, int* nf) {
   if (n) *n = h->n;
   if (ld) *ld = h->ld;
   if (nf) *nf = h->F;
+  return EKF_OK;
+}
+
+int ekf_get_path(ekf_t h, int* path) {
+  if (!h || !path) return EKF_E_ARG;
+  *path = h->resident ? EKF_PATH_RESIDENT : EKF_PATH_PIPELINE;
   return EKF_OK;
 }
 
@@ -957,7 +1023,7 @@ int ekf_profile_enable(ekf_t h, int enable) {
 }
 
 int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
-  if (!h || kind < 0 || kind > 3) return EKF_E_ARG;
+  if (!h || kind < 0 || kind > 4) return EKF_E_ARG;
   if (drain(h)) return EKF_E_HIP;
   auto& pe = h->pe[kind];
   for (size_t i = 0; i < pe.start.size(); ++i) {

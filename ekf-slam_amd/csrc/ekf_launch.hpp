@@ -64,6 +64,18 @@ hipError_t launch_assoc(const PassArgs<T>& a, int n_filters, hipStream_t s,
 template <typename T>
 hipError_t launch_posterior(const PassArgs<T>& a, int n_filters, hipStream_t s);
 
+// Resident path (ekf_resident.hip): n ≤ kResidentMaxN, fp64. One plan entry = the descriptors
+// desc[off + f − f0] of filters [f0, f0 + nf) (kind as ekf_api.cpp's Launch: 0 known chunk,
+// 1 association + correction, 2 posterior only). One 1024-thread workgroup per filter
+// [flo, flo + nfil) keeps Σ and x in registers across every entry of the plan.
+constexpr int kResidentMaxN = 128;
+struct alignas(16) PlanEntry {
+  int off, f0, nf, kind;
+};
+hipError_t launch_resident(const PassArgs<double>& a, const PlanEntry* plan, int nplan, int flo,
+                           int nfil, hipStream_t s, hipEvent_t e0 = nullptr,
+                           hipEvent_t e1 = nullptr);
+
 // Σ₀ diagonal: Σ[i][i] = v for i ≥ 3 (the rest is zero-filled by the caller).
 template <typename T>
 hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int nf, hipStream_t s);

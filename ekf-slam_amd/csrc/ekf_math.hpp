@@ -1,0 +1,109 @@
+// Device math shared by the EKF kernels (ekf_kernels.hip, ekf_resident.hip): the predict's
+// pose and At entries, refined reciprocals, the range-bearing model and the 2×2 inverse.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ekf_device.hpp"
+#include "geom.hpp"
+
+namespace ekfslam {
+
+#define EKF_FLAG_RANGE_D 1u
+#define EKF_FLAG_NUMERIC_D 2u
+
+__device__ __forceinline__ double alpha_of(int idx, double a1, double a2) {
+  return idx == 1 ? a1 : (idx == 2 ? a2 : 0.0);
+}
+
+// Predicted pose and the two nonzeros of At (slam.cpp:184-196). xin = posterior of the last
+// message = filter_previous_configuration (slam.cpp:291).
+__device__ __forceinline__ void predicted_pose(const double* tmo, const MsgDesc& d,
+                                               const double* xin, double* pose, double* a1,
+                                               double* a2) {
+  if (d.flags & kFirst) {
+    const Pose2 cur = compose(Pose2{tmo[0], tmo[1], tmo[2]},
+                              Pose2{d.odom[0], d.odom[1], d.odom[2]});
+    *a1 = -(cur.y - xin[2]);
+    *a2 = cur.x - xin[1];
+    pose[0] = normalize_angle(cur.theta);
+    pose[1] = cur.x;
+    pose[2] = cur.y;
+  } else {
+    *a1 = 0.0;
+    *a2 = 0.0;
+    pose[0] = xin[0];
+    pose[1] = xin[1];
+    pose[2] = xin[2];
+  }
+}
+
+// 1/x and 1/√x from the hardware estimate plus two Newton steps (≤ 1 ulp; the f64 division
+// sequence is ~3× longer and sits on the correction chain).
+__device__ __forceinline__ double rcp_refined(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double rsq_refined(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double e = fma(-h * y, y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-h * y, y, 0.5);
+  return fma(y, e, y);
+}
+
+// Range-bearing model for landmark at (lx, ly) seen from pose: ẑ and the 2×5 H over
+// {θ, x, y, jx, jy} (slam.cpp:219-249).
+// bear_raw / bear_ok: the bearing before normalisation and whether the branch-free normalisation
+// applied (|θ| ≤ π keeps it so); when not, the caller sets zhat[1] = normalize_angle(bear_raw).
+__device__ __forceinline__ void range_bearing(const double* pose, double lx, double ly,
+                                              double* zhat, double* H0, double* H1,
+                                              double* bear_raw, bool* bear_ok) {
+  const double ex = lx - pose[1], ey = ly - pose[2];
+  const double d = ex * ex + ey * ey;
+  const double isd = rsq_refined(d), id = isd * isd;
+  zhat[0] = d * isd;
+  *bear_raw = atan2_fast(ey, ex) - pose[0];
+  zhat[1] = normalize_angle_near(*bear_raw, bear_ok);
+  H0[0] = 0.0;
+  H0[1] = -ex * isd;
+  H0[2] = -ey * isd;
+  H0[3] = ex * isd;
+  H0[4] = ey * isd;
+  H1[0] = -1.0;
+  H1[1] = ey * id;
+  H1[2] = -ex * id;
+  H1[3] = -ey * id;
+  H1[4] = ex * id;
+}
+
+// arma::inv on a 2×2 (closed form: adjugate / det, one reciprocal). false if singular / non-finite.
+__device__ __forceinline__ bool inv2(const double* A, double* o) {
+  const double det = A[0] * A[3] - A[1] * A[2];
+  if (!(fabs(det) > 0.0)) return false;
+  const double idet = rcp_refined(det);
+  o[0] = A[3] * idet;
+  o[1] = -A[1] * idet;
+  o[2] = -A[2] * idet;
+  o[3] = A[0] * idet;
+  return isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
+}
+
+// v − (k0·m0 + k1·m1) with one fixed evaluation order, so a value rebuilt on the fly from the
+// previous buffer is bit-identical to the one the block update stores.
+__device__ __forceinline__ double rank2_sub(double v, double k0, double k1, double m0, double m1) {
+  return v - fma(k0, m0, k1 * m1);
+}
+
+// lane l's double, wave-uniform (v_readlane ×2)
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(x), l);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(x >> 32), l);
+  return __hiloint2double(hi, lo);
+}
+
+}  // namespace ekfslam

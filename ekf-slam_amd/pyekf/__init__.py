@@ -17,12 +17,14 @@ EKF_OK, EKF_E_ARG, EKF_E_RANGE, EKF_E_EMPTY, EKF_E_NUMERIC, EKF_E_HIP, EKF_E_NOM
     0, -1, -2, -3, -4, -5, -6
 EKF_FLAG_RANGE, EKF_FLAG_NUMERIC = 1, 2
 EKF_F64, EKF_F32 = 0, 1
+EKF_PATH_PIPELINE, EKF_PATH_RESIDENT = 0, 1
 ADD, DELETE = 0, 2
 SOURCE_SIM, SOURCE_ASSOC = 0, 1
 
 # every symbol include/ekf.h and include/slam_core.h declare
 EXPORTS = [
-    "ekf_config_default", "ekf_strerror", "ekf_create", "ekf_destroy", "ekf_dims", "ekf_set_odom",
+    "ekf_config_default", "ekf_strerror", "ekf_create", "ekf_destroy", "ekf_dims", "ekf_get_path",
+    "ekf_set_odom",
     "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_predict",
     "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_get_pose",
     "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status",
@@ -63,6 +65,7 @@ def lib():
             "ekf_create": (_i, [C.POINTER(_vp), C.POINTER(Config)]),
             "ekf_destroy": (_i, [_vp]),
             "ekf_dims": (_i, [_vp, _ip, _ip, _ip]),
+            "ekf_get_path": (_i, [_vp, _ip]),
             "ekf_set_odom": (_i, [_vp, _i, _d, _d, _d]),
             "ekf_fake_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
             "ekf_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
@@ -147,6 +150,9 @@ class EKF:
         lib().ekf_dims(self.h, C.byref(n), C.byref(ld), C.byref(nf))
         self.n, self.ld, self.F = n.value, ld.value, nf.value
         self.N = n_landmarks
+        p = C.c_int()
+        _check(lib().ekf_get_path(self.h, C.byref(p)), "ekf_get_path")
+        self.path = p.value  # EKF_PATH_PIPELINE | EKF_PATH_RESIDENT
 
     def close(self):
         if getattr(self, "h", None):

@@ -63,6 +63,18 @@ int ekf_destroy(ekf_t h);
 /* n = 3+2N, ld = Σ row stride in elements, n_filters */
 int ekf_dims(ekf_t h, int* n, int* ld, int* n_filters);
 
+/* Which device path the handle runs (fixed at ekf_create):
+ *   EKF_PATH_PIPELINE  Σ in HBM; per chunk of ≤ EKF_MAX_CHUNK markers a chain, a factor kernel and
+ *                      one low-rank Σ pass (any n, fp64 or fp32);
+ *   EKF_PATH_RESIDENT  fp64 with n ≤ EKF_RESIDENT_MAX_N (the reference's N = 50 map): one launch
+ *                      per upload, Σ held in a workgroup's registers across all its messages.
+ * The environment variable EKF_RESIDENT=0 forces the pipeline (both give the same results up to
+ * summation order). */
+#define EKF_PATH_PIPELINE 0
+#define EKF_PATH_RESIDENT 1
+#define EKF_RESIDENT_MAX_N 128
+int ekf_get_path(ekf_t h, int* path);
+
 /* ---- the callbacks (fast path) ---- */
 
 /* t_odom_robot ← DiffDrive::FKin output (slam.cpp:633, jointStateCallback :599-634). */
@@ -119,7 +131,8 @@ int ekf_get_status(ekf_t h, int filter, unsigned* flags); /* and clears them */
 double ekf_normalize_angle(double rad);
 
 /* ---- measurement ---- */
-/* Per-kernel device time (0 = Σ pass, 1 = chain, 2 = association, 3 = factors) from HIP events
+/* Per-kernel device time (0 = Σ pass, 1 = chain, 2 = association, 3 = factors, 4 = resident filter
+ * kernel) from HIP events
  * carried by each timed dispatch (hipExtLaunchKernelGGL start/stop events: the kernel's own
  * execution, on the stream it runs on). Off by default. */
 int ekf_profile_enable(ekf_t h, int enable);
