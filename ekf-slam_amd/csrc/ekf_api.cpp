@@ -57,6 +57,7 @@ struct ekf_ctx {
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
+  bool defer = false;            // ekf_defer: plan now, upload and launch later
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
   hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
   bool devsync = false;                   // streams synchronise through device epochs
@@ -552,6 +553,20 @@ int flush(ekf_ctx* h) {
   return rc;
 }
 
+// Deferred submission (ekf_defer): callbacks append to the plan, which goes up with ONE upload and
+// runs as one resident launch (or one pipelined run) once it is large or the caller synchronises.
+constexpr size_t kFlushDesc = 8192;
+int submit(ekf_ctx* h) {
+  if (h->defer && h->plan_d.size() < kFlushDesc) return EKF_OK;
+  return flush(h);
+}
+
+// Before any host access to device state: run what is planned, then wait for it.
+int settle(ekf_ctx* h) {
+  if (int rc = flush(h)) return rc;
+  return drain(h) ? EKF_E_HIP : EKF_OK;
+}
+
 // Association with the decisions read back (synchronous), kMaxAssoc markers per upload.
 int assoc_sync(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int m_max, int* j_out,
                int* new_out) {
@@ -794,7 +809,7 @@ int ekf_fake_sensor(ekf_t h, int f, int m, const int* ids, const int* actions,
   }
   hipSetDevice(h->cfg.device);
   plan_known(h, f, 1, true);
-  return flush(h);
+  return submit(h);
 }
 
 int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int* is_new_out) {
@@ -811,7 +826,7 @@ int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int*
   hipSetDevice(h->cfg.device);
   if (!assoc_out && !is_new_out) {
     plan_assoc(h, f, 1, true, true, 0, m);
-    return flush(h);
+    return submit(h);
   }
   const int rc = assoc_sync(h, f, 1, true, true, m, assoc_out, is_new_out);
   if (rc) return rc;
@@ -838,10 +853,8 @@ int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, cons
   } else {
     plan_known(h, 0, h->F, true);
   }
-  return flush(h);
+  return submit(h);
 }
-
-constexpr size_t kFlushDesc = 8192;
 
 int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, const int* ids,
                const int* actions, const double* rel_xy, const double* odom, double* out_pose) {
@@ -881,7 +894,7 @@ int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, con
                          3 * sizeof(double), hipMemcpyDeviceToHost));
     }
   }
-  return flush(h);
+  return submit(h);
 }
 
 int ekf_predict(ekf_t h, int f) {
@@ -901,7 +914,7 @@ int ekf_correct(ekf_t h, int f, int id, double rx, double ry) {
   mk.push_back(k);
   hipSetDevice(h->cfg.device);
   plan_known(h, f, 1, false);
-  return flush(h);
+  return submit(h);
 }
 
 int ekf_associate_correct(ekf_t h, int f, double rx, double ry, int* j, int* is_new) {
@@ -931,17 +944,52 @@ int ekf_posterior(ekf_t h, int f) {
   } else {
     plan_posterior(h, f);
   }
-  return flush(h);
+  return submit(h);
 }
 
 int ekf_sync(ekf_t h) {
   if (!h) return EKF_E_ARG;
+  return settle(h);
+}
+
+int ekf_defer(ekf_t h, int on) {
+  if (!h) return EKF_E_ARG;
+  h->defer = on != 0;
+  return on ? EKF_OK : flush(h);
+}
+
+// Σ₀ = diag(0,0,0, init_var·I_2N), state 0, t_map_odom identity, counter 0 (slam.cpp:127-139),
+// on the device, for one filter or all (f < 0): a fresh run without reallocating.
+int ekf_reset(ekf_t h, int f) {
+  if (!h || f >= h->F) return EKF_E_ARG;
+  if (int rc = settle(h)) return rc;
+  hipSetDevice(h->cfg.device);
+  const int f0 = f < 0 ? 0 : f, nf = f < 0 ? h->F : 1;
+  for (int k = f0; k < f0 + nf; ++k) {
+    h->parity[k] = 0;
+    h->pending[k] = 0;
+    h->prev_m[k] = -1;
+    h->last_desc[k] = -1;
+  }
+  const size_t sb = h->sig_stride * h->w;
+  char* sig0 = static_cast<char*>(h->sig[0]) + f0 * sb;
+  HIPCHK(hipMemsetAsync(sig0, 0, sb * nf, h->stream));
+  HIPCHK(hipMemsetAsync(h->x[0] + f0 * h->x_stride, 0, h->x_stride * nf * sizeof(double),
+                        h->stream));
+  HIPCHK(hipMemsetAsync(h->ctl + f0, 0, sizeof(FilterCtl) * nf, h->stream));
+  const hipError_t e =
+      h->cfg.dtype == EKF_F32
+          ? launch_init_diag<float>(reinterpret_cast<float*>(sig0), h->sig_stride, h->n, h->ld,
+                                    h->cfg.init_var, nf, h->stream)
+          : launch_init_diag<double>(reinterpret_cast<double*>(sig0), h->sig_stride, h->n, h->ld,
+                                     h->cfg.init_var, nf, h->stream);
+  if (e != hipSuccess) return EKF_E_HIP;
   return drain(h);
 }
 
 int ekf_get_pose(ekf_t h, int f, double* p) {
   if (!valid(h, f) || !p) return EKF_E_ARG;
-  if (drain(h)) return EKF_E_HIP;
+  if (int rc = settle(h)) return rc;
   HIPCHK(hipMemcpy(p, h->x[h->parity[f]] + f * h->x_stride, 3 * sizeof(double),
                    hipMemcpyDeviceToHost));
   return EKF_OK;
@@ -949,14 +997,14 @@ int ekf_get_pose(ekf_t h, int f, double* p) {
 
 int ekf_get_map_odom(ekf_t h, int f, double* p) {
   if (!valid(h, f) || !p) return EKF_E_ARG;
-  if (drain(h)) return EKF_E_HIP;
+  if (int rc = settle(h)) return rc;
   HIPCHK(hipMemcpy(p, h->ctl[f].tmo, 3 * sizeof(double), hipMemcpyDeviceToHost));
   return EKF_OK;
 }
 
 int ekf_get_state(ekf_t h, int f, double* state, double* sigma, unsigned* counter) {
   if (!valid(h, f)) return EKF_E_ARG;
-  if (drain(h)) return EKF_E_HIP;
+  if (int rc = settle(h)) return rc;
   const int p = h->parity[f];
   if (state)
     HIPCHK(hipMemcpy(state, h->x[p] + f * h->x_stride, h->n * sizeof(double),
@@ -980,7 +1028,7 @@ int ekf_get_state(ekf_t h, int f, double* state, double* sigma, unsigned* counte
 int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, const double* tmo,
                   unsigned counter) {
   if (!valid(h, f)) return EKF_E_ARG;
-  if (drain(h)) return EKF_E_HIP;
+  if (int rc = settle(h)) return rc;
   h->prev_m[f] = -1;
   h->last_desc[f] = -1;
   const int p = h->parity[f];
@@ -1009,7 +1057,7 @@ int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, cons
 
 int ekf_get_status(ekf_t h, int f, unsigned* flags) {
   if (!valid(h, f) || !flags) return EKF_E_ARG;
-  if (drain(h)) return EKF_E_HIP;
+  if (int rc = settle(h)) return rc;
   HIPCHK(hipMemcpy(flags, &h->ctl[f].status, sizeof(unsigned), hipMemcpyDeviceToHost));
   const unsigned z = 0;
   HIPCHK(hipMemcpy(&h->ctl[f].status, &z, sizeof(unsigned), hipMemcpyHostToDevice));
@@ -1024,7 +1072,7 @@ int ekf_profile_enable(ekf_t h, int enable) {
 
 int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
   if (!h || kind < 0 || kind > 4) return EKF_E_ARG;
-  if (drain(h)) return EKF_E_HIP;
+  if (int rc = settle(h)) return rc;
   auto& pe = h->pe[kind];
   for (size_t i = 0; i < pe.start.size(); ++i) {
     float ms = 0.f;
@@ -1052,6 +1100,9 @@ double ekf_normalize_angle(double rad) { return normalize_angle(rad); }
 int ekfslam_diag_read_stamps(unsigned long long* out, int n);  // ekf_kernels.hip
 // dev only (libekfslam_diag.so): the chain kernel's s_memtime stamps of filter 0's last chunk
 int ekf_diag_stamps(unsigned long long* out, int n) { return ekfslam_diag_read_stamps(out, n); }
+int ekfslam_res_read_stamps(unsigned long long* out, int n);  // ekf_resident.hip
+// dev only: the resident kernel's stamps (filter flo, thread 0): 6 per correction
+int ekf_diag_res_stamps(unsigned long long* out, int n) { return ekfslam_res_read_stamps(out, n); }
 #endif
 
 double ekf_sigma_pass_bytes(ekf_t h, int nf) {

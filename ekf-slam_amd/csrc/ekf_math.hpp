@@ -98,6 +98,27 @@ __device__ __forceinline__ double rank2_sub(double v, double k0, double k1, doub
   return v - fma(k0, m0, k1 * m1);
 }
 
+// geom.hpp's compose / inverse with one sincos (one argument reduction for both) — the same
+// expressions, for device code where the trig sits on a latency chain
+__device__ __forceinline__ Pose2 compose_sc(const Pose2& a, const Pose2& b) {
+  double s, c;
+  sincos(a.theta, &s, &c);
+  Pose2 r;
+  r.theta = a.theta + b.theta;
+  r.x = c * b.x - s * b.y + a.x;
+  r.y = s * b.x + c * b.y + a.y;
+  return r;
+}
+__device__ __forceinline__ Pose2 inverse_sc(const Pose2& t) {
+  double s, c;
+  sincos(t.theta, &s, &c);
+  Pose2 r;
+  r.theta = -t.theta;
+  r.x = -t.x * c - t.y * s;
+  r.y = -t.y * c + t.x * s;
+  return r;
+}
+
 // lane l's double, wave-uniform (v_readlane ×2)
 __device__ __forceinline__ double readlane_f64(double v, int l) {
   const long long x = __double_as_longlong(v);

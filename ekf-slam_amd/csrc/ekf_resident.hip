@@ -18,7 +18,8 @@
 //
 // Numerics follow the chain kernel's helpers (range_bearing, inv2, rank2_sub, normalize_angle_near)
 // and k_assoc's distance expression, so decisions match the HBM pipeline's; Σ differs from it by
-// summation order only (tests/test_gpu_parity.py: both against the oracle).
+// summation order only (Σ_ij − K_i0·M_0j − K_i1·M_1j as two FMAs; tests/test_gpu_resident.py: both
+// paths against the oracle).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -31,6 +32,27 @@
 
 namespace ekfslam {
 
+// Diagnostic build only (libekfslam_diag.so, tools/resident_stamps.py): s_memtime of thread 0 of
+// the first workgroup at RS_STAMP points, 8 slots per correction for the first 64 corrections.
+#ifdef EKF_DIAG_STAMPS
+__device__ unsigned long long g_res_stamps[512];
+#define RS_STAMP(k, i)                                                        \
+  do {                                                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (k) < 64)                      \
+      g_res_stamps[8 * (k) + (i)] = __builtin_amdgcn_s_memtime();             \
+  } while (0)
+}  // namespace ekfslam
+extern "C" int ekfslam_res_read_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(ekfslam::g_res_stamps),
+                             sizeof(unsigned long long) * (n < 512 ? n : 512)) == hipSuccess ? 0 : -5;
+}
+namespace ekfslam {
+#else
+#define RS_STAMP(k, i) \
+  do {                 \
+  } while (0)
+#endif
+
 namespace {
 
 typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -39,14 +61,32 @@ typedef unsigned u2 __attribute__((ext_vector_type(2)));
 constexpr int kOOB = 0x7ffffff0;
 constexpr int kRW = 8;  // waves per workgroup (512 threads: 256 VGPRs per lane for the resident Σ)
 
-template <int RS, int CS>
+// The prefix of a MsgDesc the kernel reads (m … z), staged in LDS a block of plan entries at a time.
+struct alignas(16) ResMsg {
+  int m, flags, parity, assoc_slot;
+  double odom[3];
+  int prev_m, pad1;
+  int ids[kMaxChunk];
+  double z[kMaxChunk][2];
+};
+static_assert(offsetof(ResMsg, odom) == offsetof(MsgDesc, odom) &&
+                  offsetof(ResMsg, ids) == offsetof(MsgDesc, ids) &&
+                  offsetof(ResMsg, z) == offsetof(MsgDesc, z) && sizeof(ResMsg) % 16 == 0,
+              "ResMsg is MsgDesc's prefix");
+constexpr int kMsgQ = sizeof(ResMsg) / 16;  // 16-byte pieces per staged descriptor
+constexpr int kBlk = 16;                    // plan entries staged per block
+
+template <int W, int RS, int CS>
 struct ResShared {
+  ResMsg msg[kBlk];
+  int kind[kBlk];  // the entry's kind, −1: it does not name this filter
   double grow[2][5][64 * CS];  // Σ[idx_a][c]  (idx = {0, 1, 2, j, j+1})
-  double gcol[2][5][kRW * RS];  // Σ[r][idx_a]
-  double gx[2][8];              // x[idx_a]
-  double blk[(kRW * RS) / 2][4];  // association: Σ[jk..jk+1][jk..jk+1] of landmark k
-  double xall[kRW * RS];          // association: x
-  int dec[2];                     // association decision: slot j, is_new
+  double gcol[2][5][W * RS];   // Σ[r][idx_a]
+  double gx[2][8];             // x[idx_a]
+  double blk[(W * RS) / 2][4];  // association: Σ[jk..jk+1][jk..jk+1] of landmark k
+  double xall[W * RS];          // association: x
+  int dec[2];                   // association decision: slot j, is_new
+  double kw[W][RS][2];          // per wave: K[row(s)] of the current correction (wave-private)
 };
 
 __device__ __forceinline__ int pos5(int r, int j) {
@@ -58,10 +98,12 @@ __device__ __forceinline__ int pos5(int r, int j) {
 // One workgroup per filter flo + blockIdx.x; walks the whole plan (PlanEntry list, in order) and
 // applies the entries that name its filter. Σ / x are loaded on the first active entry from the
 // entry's parity and written back once, to the parity the host's plan ends on.
-template <int RS, int CS>
-__global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const PlanEntry* plan,
-                                                       int nplan, int flo) {
-  __shared__ ResShared<RS, CS> sh;
+template <int W, int RS, int CS>
+__global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const PlanEntry* plan,
+                                                     int nplan, int flo) {
+  constexpr int kRW = W;
+  static_assert(RS <= 32 && RS <= 64, "jump-table gather covers 32 slots; x is lane-distributed");
+  __shared__ ResShared<W, RS, CS> sh;
   const int f = flo + blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row offsets in SGPRs
@@ -74,22 +116,53 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
   const bool rown = lane < RS;
   double xl = 0.0;
   double tmo[3];
+  // posterior deferred to the next gather of the pose (the next message's predict gathers it
+  // anyway; nothing moves the pose in between): one barrier per message instead of two
+  bool post = false;
+  double podom[3] = {0.0, 0.0, 0.0};
   unsigned counter = 0, status = 0;
   int par = -1;          // current parity (−1: not loaded yet)
   bool dirty = false;    // Σ / x changed (a chunk entry ran)
   int b = 0;             // gather buffer
 
-  auto row = [&](int s) __attribute__((always_inline)) { return w + kRW * s; };
+  // wq: the wave index re-materialised per correction (an opaque copy), so the compiler recomputes
+  // the per-row conditions in a few scalar ops instead of hoisting them out of the plan loop into
+  // (spilled) SGPRs
+  int wq = w;
+  auto row = [&](int s) __attribute__((always_inline)) { return wq + kRW * s; };
   auto col = [&](int t) __attribute__((always_inline)) { return lane + 64 * t; };
 
   // rows / columns idx_a with a ≥ amin (j < 0: pose only) and their x into gather buffer bb
   auto gather = [&](int bb, int j, int amin) __attribute__((always_inline)) {
+    asm volatile("" : "+s"(wq));
+    // rows: θ, x, y are slot 0 of waves 0-2; jx, jy sit in slot r / W of wave r % W, picked by
+    // one jump-table switch each (a few scalar ops and one indirect branch: the scalar unit is
+    // shared by the CU's waves, a test per slot costs more)
+    if (amin == 0 && wq < 3) {
 #pragma unroll
-    for (int s = 0; s < RS; ++s) {
-      const int r = row(s), a = pos5(r, j);
-      if (a >= amin && r < n) {
+      for (int t = 0; t < CS; ++t) sh.grow[bb][wq][col(t)] = sg[0][t];
+    }
 #pragma unroll
-        for (int t = 0; t < CS; ++t) sh.grow[bb][a][col(t)] = sg[s][t];
+    for (int e = 0; e < 2; ++e) {
+      const int r = j + e;
+      if (j >= 0 && r < n && r % kRW == wq) {
+        double* dst = &sh.grow[bb][3 + e][0];
+        switch (r / kRW) {
+#define RES_SLOT(q)                                                      \
+  case q:                                                                \
+    if constexpr (q < RS) {                                              \
+      _Pragma("unroll") for (int t = 0; t < CS; ++t) dst[col(t)] = sg[q][t]; \
+    }                                                                    \
+    break;
+          RES_SLOT(0) RES_SLOT(1) RES_SLOT(2) RES_SLOT(3) RES_SLOT(4) RES_SLOT(5) RES_SLOT(6)
+          RES_SLOT(7) RES_SLOT(8) RES_SLOT(9) RES_SLOT(10) RES_SLOT(11) RES_SLOT(12) RES_SLOT(13)
+          RES_SLOT(14) RES_SLOT(15) RES_SLOT(16) RES_SLOT(17) RES_SLOT(18) RES_SLOT(19)
+          RES_SLOT(20) RES_SLOT(21) RES_SLOT(22) RES_SLOT(23) RES_SLOT(24) RES_SLOT(25)
+          RES_SLOT(26) RES_SLOT(27) RES_SLOT(28) RES_SLOT(29) RES_SLOT(30) RES_SLOT(31)
+#undef RES_SLOT
+          default:
+            break;
+        }
       }
     }
     {
@@ -112,12 +185,31 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
 
   // One correction against landmark column j = 3 + 2·id (slam.cpp:219-267 / :443-488). The
   // gather of idx into buffer b is done and the barrier passed.
+  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-291) from a gathered pose
+  auto posterior_from = [&](double p0, double p1, double p2) __attribute__((always_inline)) {
+    const Pose2 t = compose_sc(Pose2{p0, p1, p2}, inverse_sc(Pose2{podom[0], podom[1], podom[2]}));
+    tmo[0] = t.theta;
+    tmo[1] = t.x;
+    tmo[2] = t.y;
+    post = false;
+  };
+  auto posterior_now = [&]() __attribute__((always_inline)) {
+    b ^= 1;
+    if (rown && rl < 3) sh.gx[b][rl] = xl;
+    __syncthreads();
+    posterior_from(sh.gx[b][0], sh.gx[b][1], sh.gx[b][2]);
+  };
+  int ncorr = 0;  // corrections so far (diagnostic stamps)
   auto correct = [&](int j, double z0, double z1, bool noinit) __attribute__((always_inline)) {
+    RS_STAMP(ncorr, 1);
+    asm volatile("" : "+s"(wq));
     const double pose[3] = {sh.gx[b][0], sh.gx[b][1], sh.gx[b][2]};
     double lx = sh.gx[b][3], ly = sh.gx[b][4];
     if (!noinit && lx == 0.0 && ly == 0.0) {  // first sighting, slam.cpp:213-216
-      lx = pose[1] + z0 * cos(z1 + pose[0]);
-      ly = pose[2] + z0 * sin(z1 + pose[0]);
+      double sn, cs;
+      sincos(z1 + pose[0], &sn, &cs);
+      lx = pose[1] + z0 * cs;
+      ly = pose[2] + z0 * sn;
       set_x(j, lx);
       set_x(j + 1, ly);
     }
@@ -125,6 +217,7 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
     bool bok;
     range_bearing(pose, lx, ly, zhat, H0, H1, &braw, &bok);
     if (!bok) zhat[1] = normalize_angle(braw);
+    RS_STAMP(ncorr, 2);
     double mc0[CS], mc1[CS];  // (H·Σ)[:, c] of this lane's columns
 #pragma unroll
     for (int t = 0; t < CS; ++t) {
@@ -168,6 +261,7 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
     bool nok;
     const double nn = normalize_angle_near(z1 - zhat[1], &nok);
     const double nv1 = nok ? nn : normalize_angle(z1 - zhat[1]);
+    RS_STAMP(ncorr, 3);
     // K[rl] = (Σ·Hᵀ)[rl]·S⁻¹ on the lane that holds row rl, then every lane takes its rows' K
     double K0, K1;
     {
@@ -181,11 +275,19 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
       K0 = ka * Si[0] + kb * Si[2];
       K1 = ka * Si[1] + kb * Si[3];
     }
+    // the wave's rows' K through its own LDS slots (one wave: LDS ops complete in issue order)
+    if (rown) {
+      sh.kw[w][lane][0] = K0;
+      sh.kw[w][lane][1] = K1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int s = 0; s < RS; ++s) {
-      const double k0 = readlane_f64(K0, s), k1 = readlane_f64(K1, s);
+      const double k0 = sh.kw[w][s][0], k1 = sh.kw[w][s][1];  // broadcast reads
 #pragma unroll
-      for (int t = 0; t < CS; ++t) sg[s][t] = rank2_sub(sg[s][t], k0, k1, mc0[t], mc1[t]);
+      for (int t = 0; t < CS; ++t) sg[s][t] = fma(-k1, mc1[t], fma(-k0, mc0[t], sg[s][t]));
     }
     double xt = xl + (K0 * nv0 + K1 * nv1);  // slam.cpp:261
     if (rl == 0) {                            // slam.cpp:267
@@ -194,14 +296,32 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
       xt = tok ? tn : normalize_angle(xt);
     }
     xl = xt;
+    RS_STAMP(ncorr, 4);
+    ++ncorr;
   };
 
-  for (int li = 0; li < nplan; ++li) {
-    const PlanEntry L = plan[li];
-    if (f < L.f0 || f >= L.f0 + L.nf) continue;
-    const MsgDesc& d = A.desc[L.off + (f - L.f0)];
+  for (int l0 = 0; l0 < nplan; l0 += kBlk) {
+  // stage the block's descriptors: every thread fetches 16-byte pieces (plan entry → descriptor,
+  // one dependent pair of loads per thread, all in flight together), one barrier
+  const int nb = min(kBlk, nplan - l0);
+  __syncthreads();  // the previous block's entries are consumed
+  for (int t = tid; t < nb * kMsgQ; t += kRW * 64) {
+    const int e = t / kMsgQ, q = t - e * kMsgQ;
+    const PlanEntry L = plan[l0 + e];
+    const bool mine = f >= L.f0 && f < L.f0 + L.nf;
+    if (q == 0) sh.kind[e] = mine ? L.kind : -1;
+    if (mine)
+      reinterpret_cast<uint4*>(&sh.msg[e])[q] =
+          reinterpret_cast<const uint4*>(A.desc + L.off + (f - L.f0))[q];
+  }
+  __syncthreads();
+  for (int e = 0; e < nb; ++e) {
+    const int kind = sh.kind[e];
+    if (kind < 0) continue;
+    const ResMsg& d = sh.msg[e];
     const int flags = d.flags;
     if (!(flags & kActive)) continue;
+    const PlanEntry L{0, 0, 0, kind};
     if (par < 0) {  // first entry naming this filter: load it
       par = d.parity;
       const double* S = A.sig[par] + f * A.sig_stride;
@@ -227,22 +347,23 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
       tmo[2] = ctl->tmo[2];
       counter = ctl->counter;
     }
+    if (post && L.kind != 2 && !(flags & kFirst)) posterior_now();  // corrections follow
     if (L.kind != 2) {
       if (flags & kFirst) {  // predict, slam.cpp:184-198: Σ = AΣAᵀ + Q̄, A = I + α·e0ᵀ
         b ^= 1;
         gather(b, -8, 0);
         __syncthreads();
         const double prev[3] = {sh.gx[b][0], sh.gx[b][1], sh.gx[b][2]};
-        const Pose2 cur = compose(Pose2{tmo[0], tmo[1], tmo[2]},
-                                  Pose2{d.odom[0], d.odom[1], d.odom[2]});
+        if (post) posterior_from(prev[0], prev[1], prev[2]);  // the last message's posterior
+        const Pose2 cur = compose_sc(Pose2{tmo[0], tmo[1], tmo[2]},
+                                     Pose2{d.odom[0], d.odom[1], d.odom[2]});
         const double a1 = -(cur.y - prev[2]), a2 = cur.x - prev[1];
         const double s00 = sh.grow[b][0][0];
-        const double c0l = sh.gcol[b][0][rl];  // Σ[rl][0], lane-distributed
 #pragma unroll
         for (int s = 0; s < RS; ++s) {
           const int r = row(s);
           const double aa = alpha_of(r, a1, a2);
-          const double cr0 = readlane_f64(c0l, s);
+          const double cr0 = sh.gcol[b][0][r];  // Σ[r][0], broadcast
 #pragma unroll
           for (int t = 0; t < CS; ++t) {
             const int c = col(t);
@@ -261,8 +382,10 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
         for (int c = 0; c < d.m; ++c) {
           const int id = d.ids[c];
           if (id < 0 || id >= N) continue;  // validated on the host; never reached
+          RS_STAMP(ncorr, 0);
           b ^= 1;
           gather(b, 3 + 2 * id, 0);
+          RS_STAMP(ncorr, 5);
           __syncthreads();
           correct(3 + 2 * id, d.z[c][0], d.z[c][1], (flags & kNoInit) != 0);
         }
@@ -372,8 +495,10 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
           const int j = 3 + 2 * k;
           if (sh.dec[1]) {  // slam.cpp:351-356, kept (:421)
             const double p0 = sh.gx[b][0], p1 = sh.gx[b][1], p2 = sh.gx[b][2];
-            set_x(j, p1 + z0 * cos(z1 + p0));
-            set_x(j + 1, p2 + z0 * sin(z1 + p0));
+            double sn, cs;
+            sincos(z1 + p0, &sn, &cs);
+            set_x(j, p1 + z0 * cs);
+            set_x(j + 1, p2 + z0 * sn);
             ++counter;
           }
           gather(b, j, 3);  // the pose rows / columns are in b already
@@ -384,18 +509,16 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
       par ^= 1;
       dirty = true;
     }
-    if ((flags & kLast) || L.kind == 2) {  // posterior, slam.cpp:273-291
-      b ^= 1;
-      if (rown && rl < 3) sh.gx[b][rl] = xl;
-      __syncthreads();
-      const Pose2 t = compose(Pose2{sh.gx[b][0], sh.gx[b][1], sh.gx[b][2]},
-                              inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
-      tmo[0] = t.theta;
-      tmo[1] = t.x;
-      tmo[2] = t.y;
+    if ((flags & kLast) || L.kind == 2) {  // posterior, slam.cpp:273-291 (deferred)
+      post = true;
+      podom[0] = d.odom[0];
+      podom[1] = d.odom[1];
+      podom[2] = d.odom[2];
     }
   }
+  }
   if (par < 0) return;  // the plan does not name this filter
+  if (post) posterior_now();
   if (dirty) {
     double* S = A.sig[par] + f * A.sig_stride;
     double* X = A.x[par] + f * A.x_stride;
@@ -425,17 +548,22 @@ __global__ __launch_bounds__(kRW * 64) void k_resident(PassArgs<double> A, const
 hipError_t launch_resident(const PassArgs<double>& a, const PlanEntry* plan, int nplan, int flo,
                            int nfil, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   if (a.n > kResidentMaxN || nfil <= 0) return hipErrorInvalidValue;
-  const dim3 grid(nfil), block(kRW * 64);
-  auto go = [&](auto kernel) {
+  const dim3 grid(nfil);
+  auto go = [&](auto kernel, int waves) {
+    const dim3 block(64 * waves);
     if (e0 && e1)
       hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, a, plan, nplan, flo);
     else
       hipLaunchKernelGGL(kernel, grid, block, 0, s, a, plan, nplan, flo);
   };
+  // 4 waves (one per SIMD): the per-correction scalar work (geometry, S, gather control) runs
+  // once per wave on the CU's one scalar unit, so fewer, wider waves finish a step sooner
   if (a.n <= 64)
-    go(k_resident<8, 1>);
+    go(k_resident<4, 16, 1>, 4);
+  else if (a.n <= 4 * 26)
+    go(k_resident<4, 26, 2>, 4);  // N = 50 (n = 103): no idle row slots
   else
-    go(k_resident<16, 2>);
+    go(k_resident<4, 32, 2>, 4);
   return hipGetLastError();
 }
 

@@ -78,11 +78,22 @@ int slam_map_odom(slam_t s, double* p) {
 
 ekf_t slam_filter(slam_t s) { return s ? s->ekf : nullptr; }
 
+int slam_reset(slam_t s) {
+  if (!s) return EKF_E_ARG;
+  s->ddrive = DiffDrive(s->track, s->radius);
+  s->t_odom_robot = Pose2{};
+  const int rc = ekf_reset(s->ekf, 0);
+  if (rc) return rc;
+  return ekf_set_odom(s->ekf, 0, 0.0, 0.0, 0.0);
+}
+
 int slam_replay(slam_t s, int T, int ticks, const double* wheel, int m_max, const int* counts,
                 const int* ids, const int* actions, const double* rel_xy, double* out_pose,
                 double* out_tmo) {
   if (!s || T < 0 || ticks < 0 || !wheel || !counts || (m_max > 0 && !rel_xy)) return EKF_E_ARG;
   int first_rc = EKF_OK;
+  const bool defer = !out_pose && !out_tmo;
+  if (defer) ekf_defer(s->ekf, 1);
   for (int t = 0; t < T; ++t) {
     for (int k = 0; k < ticks; ++k) {
       const double* w = wheel + (static_cast<size_t>(t) * ticks + k) * 2;
@@ -94,6 +105,10 @@ int slam_replay(slam_t s, int T, int ticks, const double* wheel, int m_max, cons
     if (rc && !first_rc) first_rc = rc;
     if (out_pose) ekf_get_pose(s->ekf, 0, out_pose + 3 * static_cast<size_t>(t));
     if (out_tmo) ekf_get_map_odom(s->ekf, 0, out_tmo + 3 * static_cast<size_t>(t));
+  }
+  if (defer) {
+    const int rc = ekf_defer(s->ekf, 0);
+    if (rc && !first_rc) first_rc = rc;
   }
   return first_rc;
 }

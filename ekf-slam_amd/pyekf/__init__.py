@@ -27,7 +27,8 @@ EXPORTS = [
     "ekf_set_odom",
     "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_predict",
     "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_get_pose",
-    "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status",
+    "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status", "ekf_defer",
+    "ekf_reset", "slam_reset",
     "ekf_profile_enable", "ekf_profile_read", "ekf_sigma_pass_bytes", "ekf_normalize_angle",
     "slam_create", "slam_destroy", "slam_joint_states", "slam_markers", "slam_initial_pose",
     "slam_odom", "slam_map_odom", "slam_filter", "slam_replay", "slam_integrate_odometry",
@@ -81,6 +82,9 @@ def lib():
             "ekf_get_state": (_i, [_vp, _i, _vp, _vp, _vp]),
             "ekf_set_state": (_i, [_vp, _i, _vp, _vp, _vp, C.c_uint]),
             "ekf_get_status": (_i, [_vp, _i, C.POINTER(C.c_uint)]),
+            "ekf_defer": (_i, [_vp, _i]),
+            "ekf_reset": (_i, [_vp, _i]),
+            "slam_reset": (_i, [_vp]),
             "ekf_profile_enable": (_i, [_vp, _i]),
             "ekf_profile_read": (_i, [_vp, _i, C.POINTER(C.c_longlong), _dp]),
             "ekf_sigma_pass_bytes": (C.c_double, [_vp, _i]),
@@ -242,6 +246,12 @@ class EKF:
         _check(lib().ekf_set_state(self.h, f, _ptr(state), _ptr(sigma), _ptr(tmo), counter),
                "ekf_set_state")
 
+    def defer(self, on=True):
+        _check(lib().ekf_defer(self.h, int(on)), "ekf_defer")
+
+    def reset(self, f=-1):
+        _check(lib().ekf_reset(self.h, f), "ekf_reset")
+
     def status(self, f=0) -> int:
         fl = C.c_uint(0)
         _check(lib().ekf_get_status(self.h, f, C.byref(fl)), "ekf_get_status")
@@ -270,6 +280,9 @@ class Slam:
                "slam_create")
         self.h = h
         self.n = 3 + 2 * n_landmarks
+        p = C.c_int()
+        _check(lib().ekf_get_path(lib().slam_filter(self.h), C.byref(p)), "ekf_get_path")
+        self.path = p.value
 
     def close(self):
         if getattr(self, "h", None):
@@ -277,6 +290,10 @@ class Slam:
             self.h = None
 
     __del__ = close
+
+    def reset(self):
+        """A fresh node on the same handle (slam_reset)."""
+        _check(lib().slam_reset(self.h), "slam_reset")
 
     def joint_states(self, left, right):
         return lib().slam_joint_states(self.h, float(left), float(right))

@@ -115,6 +115,18 @@ int ekf_associate_correct(ekf_t h, int filter, double rel_x, double rel_y, int* 
 /* Posterior (slam.cpp:273-291): t_map_odom = T(x, y, θ)·t_odom_robot⁻¹. */
 int ekf_posterior(ekf_t h, int filter);
 
+/* Deferred submission. While on, the callbacks above only plan their work on the host; the plan
+ * goes to the device in one upload (and, on the resident path, one kernel launch) when it reaches
+ * 8192 descriptors, when a synchronising call below needs the state, or when deferral is turned
+ * off (which submits what is planned). Off by default: each callback is submitted as it is made.
+ * A replay driver with no per-message outputs (slam_replay) turns it on. */
+int ekf_defer(ekf_t h, int on);
+
+/* Back to the constructor's state (slam.cpp:127-139) on the device for filter `filter`, or every
+ * filter when filter < 0: Σ₀, state 0, t_map_odom identity, counter 0, status clear. Host-side
+ * odometry set by ekf_set_odom is kept. Synchronises. */
+int ekf_reset(ekf_t h, int filter);
+
 /* ---- state access (synchronising) ---- */
 int ekf_sync(ekf_t h);
 int ekf_get_pose(ekf_t h, int filter, double* theta_x_y);

@@ -30,13 +30,18 @@ int slam_joint_states(slam_t s, double left, double right);
 /* one MarkerArray; ids/actions ignored for SLAM_SOURCE_ASSOC (may be NULL) */
 int slam_markers(slam_t s, int m, const int* ids, const int* actions, const double* rel_xy);
 int slam_initial_pose(slam_t s, double x, double y, double theta);
+/* A fresh node on the same handle: the filter back to its constructor state (ekf_reset), the
+ * DiffDrive and t_odom_robot back to the origin (slam.cpp:86, :650). */
+int slam_reset(slam_t s);
 int slam_odom(slam_t s, double* theta_x_y);    /* t_odom_robot */
 int slam_map_odom(slam_t s, double* theta_x_y); /* t_map_odom (synchronises) */
 ekf_t slam_filter(slam_t s);
 /* Replay a recorded run natively: per message, `ticks` joint_states (wheel[T][ticks][2]) then one
  * MarkerArray (counts[T], ids/actions[T][m_max], rel_xy[T][m_max][2]). out_pose / out_tmo
  * [T][3] (nullable) receive the posterior pose and t_map_odom after each message. Returns the
- * first non-OK status (processing continues, like a node that logs and carries on). */
+ * first non-OK status (processing continues, like a node that logs and carries on). With no
+ * per-message output the messages are planned on the host and submitted together (ekf_defer):
+ * asynchronous on return, like ekf_replay. */
 int slam_replay(slam_t s, int T, int ticks, const double* wheel, int m_max, const int* counts,
                 const int* ids, const int* actions, const double* rel_xy, double* out_pose,
                 double* out_tmo);

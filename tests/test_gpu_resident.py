@@ -213,3 +213,40 @@ def test_resident_counter_overflow_matches_pipeline(monkeypatch):
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
     assert np.abs(xr - xp).max() < TOL
     assert np.abs(Sr - Sp).max() < TOL
+
+
+@pytest.mark.parametrize("resident", [True, False], ids=["resident", "pipeline"])
+def test_deferred_submission_and_reset(resident, monkeypatch):
+    """slam_replay with no per-message output plans the whole drive and submits it once
+    (ekf_defer); with the pose trace every message is submitted and read back. Same final state
+    (resident: bit for bit — per correction the same arithmetic whatever the launch boundaries;
+    pipeline: chunks then pipeline across messages, a different summation order). slam_reset
+    then gives a fresh node on the same handle: the second drive equals the first bit for bit."""
+    _env(monkeypatch, resident)
+    sc, g = load_golden("crowded_assoc")
+    s = pyekf.Slam(n_landmarks=sc.n_landmarks, source=pyekf.SOURCE_ASSOC, track=sc.track,
+                   radius=sc.radius)
+    assert s.path == (pyekf.EKF_PATH_RESIDENT if resident else pyekf.EKF_PATH_PIPELINE)
+    rc, _, _ = s.replay(sc, poses=False)
+    assert rc == pyekf.EKF_OK
+    x1, S1, c1 = s.filter_state()
+    s.reset()
+    x0, S0, c0 = s.filter_state()
+    assert c0 == 0 and not np.any(x0)
+    assert np.array_equal(np.diag(S0)[3:], np.full(sc.n_landmarks * 2, 1e7))
+    rc, poses, _ = s.replay(sc, poses=True)
+    assert rc == pyekf.EKF_OK
+    x2, S2, c2 = s.filter_state()
+    s.reset()
+    s.replay(sc, poses=False)
+    x3, S3, c3 = s.filter_state()
+    s.close()
+    assert c1 == c2 == c3 == int(g["counter"])
+    np.testing.assert_array_equal(x1, x3)
+    np.testing.assert_array_equal(S1, S3)
+    if resident:
+        np.testing.assert_array_equal(x1, x2)
+        np.testing.assert_array_equal(S1, S2)
+    assert np.abs(x1 - x2).max() < 1e-9 and np.abs(S1 - S2).max() < 1e-9
+    assert np.abs(poses - g["poses"]).max() < TOL
+    assert np.abs(S1 - g["sigma"]).max() < TOL
