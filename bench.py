@@ -255,6 +255,11 @@ def rosbag_main(args):
     for _ in range(args.steps):
         scg, _ = gpu_run(False)
     dt = (time.perf_counter() - t0) / args.steps
+    # device time of the EKF kernels over one more (untimed) drive, HIP events per launch
+    s.profile(True)
+    gpu_run(False)
+    dev = {k: s.profile_read(k) for k in (4, 1, 2, 3, 0)}
+    s.profile(False)
     scg, poses = gpu_run(True)  # the pose trace for parity, untimed
     det.close()
     s.close()
@@ -273,6 +278,10 @@ def rosbag_main(args):
                    "step": "slam_reset + lm_detect batch + 426 slam_markers messages with "
                            "wheel ticks (one deferred submission) + state read-back",
                    "device_path": "resident" if s.path == pyekf.EKF_PATH_RESIDENT else "pipeline"},
+        "ekf_device_ms_per_step": sum(v[1] for v in dev.values()),
+        "ekf_device_launches_per_step": {
+            {4: "k_resident", 1: "k_chain", 2: "k_assoc", 3: "k_factors", 0: "k_sigma_pass"}[k]: v[0]
+            for k, v in dev.items() if v[0]},
         "pose_rmse_vs_truth_m": float(np.sqrt(np.mean(np.sum((poses[:, 1:] - tr[:, 1:]) ** 2,
                                                                1)))),
     }
@@ -305,7 +314,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     traffic, traffic_err = None, "not measured (--traffic off or N>1)"
-    if args.traffic == "auto" and world == 1:
+    N_, dt_ = WORKLOADS[args.workload][:2]
+    resident = dt_ == "f64" and 3 + 2 * N_ <= 128 and os.environ.get("EKF_RESIDENT") != "0"
+    if resident:
+        traffic_err = "resident path: Σ crosses HBM once per launch (no Σ pass to count)"
+    if args.traffic == "auto" and world == 1 and not resident:
         traffic, traffic_err = pmc_traffic(args)
     import torch
     import torch.distributed as dist
@@ -372,7 +385,10 @@ def main():
     n_sig, ms_sig = ekf.profile_read(0)
     n_gain, ms_gain = ekf.profile_read(1)
     n_fac, ms_fac = ekf.profile_read(3)
+    n_res, ms_res = ekf.profile_read(4)
     ekf.profile(False)
+    res_corr = int(np.count_nonzero((act[ps] == 0) & (np.arange(act.shape[2]) <
+                                                      counts[ps][..., None])))
     bytes_per_launch = ekf.sigma_pass_bytes()
     avg_sig_s = ms_sig / max(n_sig, 1) / 1e3
     achieved = bytes_per_launch / avg_sig_s / 1e9 if n_sig else 0.0
@@ -423,6 +439,24 @@ def main():
                 "factor_kernel_avg_us": ms_fac / max(n_fac, 1) * 1e3,
             },
         }
+        if n_res:
+            # resident path (ekf_resident.hip): one launch runs the whole replay, Σ in registers;
+            # its bound is the sequential f64 chain of one CU per filter, priced against that
+            # CU's share of the fp64 vector peak (78.6 TF / 256 CUs)
+            flops = 4.0 * n * n * res_corr  # Σ ← Σ − K·(HΣ): 2 FMAs per element per correction
+            sec = ms_res / n_res / 1e3
+            cu_peak = MFMA_PEAK_TF["f64"] / 256 * min(F, 256)
+            result["roofline"] = {
+                "kernel": "k_resident", "bound": "fp64-valu, one CU per filter (latency chain)",
+                "achieved": flops / sec / 1e12, "peak": cu_peak, "unit": "TFLOP/s",
+                "frac": flops / sec / 1e12 / cu_peak, "traffic": None,
+                "traffic_detail": traffic_err,
+                "flops_formula": f"4*n^2*corrections = 4*{n}^2*{res_corr}",
+                "avg_launch_us": sec * 1e6, "launches": n_res,
+                "us_per_correction": sec * 1e6 / max(res_corr, 1),
+                "hbm_bytes_per_launch": 2.0 * n * n * 8 * F,
+            }
+            result["config"]["device_path"] = "resident"
     # ---- CPU baseline + parity (rank 0, N=1 only) ----
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, N, warm_state[0], counts, ids, act, rel, odom,

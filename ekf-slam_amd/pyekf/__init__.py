@@ -295,6 +295,15 @@ class Slam:
         """A fresh node on the same handle (slam_reset)."""
         _check(lib().slam_reset(self.h), "slam_reset")
 
+    def profile(self, enable=True):
+        lib().ekf_profile_enable(lib().slam_filter(self.h), int(enable))
+
+    def profile_read(self, kernel):
+        n, ms = C.c_longlong(0), C.c_double(0)
+        _check(lib().ekf_profile_read(lib().slam_filter(self.h), kernel, C.byref(n), C.byref(ms)),
+               "profile_read")
+        return n.value, ms.value
+
     def joint_states(self, left, right):
         return lib().slam_joint_states(self.h, float(left), float(right))
 
