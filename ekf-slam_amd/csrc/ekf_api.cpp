@@ -58,6 +58,7 @@ struct ekf_ctx {
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
   bool defer = false;            // ekf_defer: plan now, upload and launch later
+  bool joseph = false;           // ekf_set_joseph (resident path)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
   hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
   bool devsync = false;                   // streams synchronise through device epochs
@@ -133,6 +134,7 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.q = h->cfg.q_noise;
   a.r = h->cfg.r_noise;
   a.gate = h->cfg.mah_gate;
+  a.joseph = h->joseph ? 1 : 0;
   return a;
 }
 
@@ -950,6 +952,14 @@ int ekf_posterior(ekf_t h, int f) {
 int ekf_sync(ekf_t h) {
   if (!h) return EKF_E_ARG;
   return settle(h);
+}
+
+int ekf_set_joseph(ekf_t h, int on) {
+  if (!h) return EKF_E_ARG;
+  if (on && !h->resident) return EKF_E_ARG;  // the pipeline's low-rank factors: simple form only
+  if (int rc = flush(h)) return rc;           // what is planned runs with the form it was planned in
+  h->joseph = on != 0;
+  return EKF_OK;
 }
 
 int ekf_defer(ekf_t h, int on) {

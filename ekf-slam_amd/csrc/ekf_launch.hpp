@@ -34,6 +34,7 @@ struct PassArgs {
   int desc_stride;      // descriptors between consecutive chunks of a chain launch
   int n, ld, N, f0;
   double q, r, gate;
+  int joseph;           // resident path: Joseph-form Σ update (ekf_set_joseph)
 };
 
 // Chain kernel: the chunk's sequential corrections on the |U|×|U| block (predict folded in),

@@ -86,7 +86,7 @@ struct ResShared {
   double blk[(W * RS) / 2][4];  // association: Σ[jk..jk+1][jk..jk+1] of landmark k
   double xall[W * RS];          // association: x
   int dec[2];                   // association decision: slot j, is_new
-  double kw[W][RS][2];          // per wave: K[row(s)] of the current correction (wave-private)
+  double kw[W][RS][4];          // per wave: K[row(s)] (and Joseph: (Σ·Hᵀ)[row(s)]), wave-private
 };
 
 __device__ __forceinline__ int pos5(int r, int j) {
@@ -263,9 +263,8 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
     const double nv1 = nok ? nn : normalize_angle(z1 - zhat[1]);
     RS_STAMP(ncorr, 3);
     // K[rl] = (Σ·Hᵀ)[rl]·S⁻¹ on the lane that holds row rl, then every lane takes its rows' K
-    double K0, K1;
+    double K0, K1, ka = 0.0, kb = 0.0;
     {
-      double ka = 0.0, kb = 0.0;
 #pragma unroll
       for (int a = 0; a < 5; ++a) {
         const double v = sh.gcol[b][a][rl];
@@ -279,15 +278,48 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
     if (rown) {
       sh.kw[w][lane][0] = K0;
       sh.kw[w][lane][1] = K1;
+      sh.kw[w][lane][2] = ka;
+      sh.kw[w][lane][3] = kb;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!A.joseph) {  // Σ ← Σ − K·(HΣ), slam.cpp:264-265
 #pragma unroll
-    for (int s = 0; s < RS; ++s) {
-      const double k0 = sh.kw[w][s][0], k1 = sh.kw[w][s][1];  // broadcast reads
+      for (int s = 0; s < RS; ++s) {
+        const double k0 = sh.kw[w][s][0], k1 = sh.kw[w][s][1];  // broadcast reads
 #pragma unroll
-      for (int t = 0; t < CS; ++t) sg[s][t] = fma(-k1, mc1[t], fma(-k0, mc0[t], sg[s][t]));
+        for (int t = 0; t < CS; ++t) sg[s][t] = fma(-k1, mc1[t], fma(-k0, mc0[t], sg[s][t]));
+      }
+    } else {
+      // Joseph form (opt-in): Σ ← (I−KH)Σ(I−KH)ᵀ + KRKᵀ = Σ − K·(HΣ) − (ΣHᵀ)·Kᵀ + K·S·Kᵀ. Per
+      // column c: K[c] from (ΣHᵀ)[c] (the gathered columns at row c) and u = S·K[c]ᵀ; then each
+      // element takes Σ_rc − K_r·(M_c − u_c) − (ΣHᵀ)_r·K_cᵀ, four FMAs
+      double kc0[CS], kc1[CS];
+#pragma unroll
+      for (int t = 0; t < CS; ++t) {
+        const int c = min(col(t), kRW * RS - 1);  // columns ≥ n: never stored
+        double pa = 0.0, pb = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          const double v = sh.gcol[b][a][c];
+          pa += v * H0[a];
+          pb += v * H1[a];
+        }
+        kc0[t] = pa * Si[0] + pb * Si[2];
+        kc1[t] = pa * Si[1] + pb * Si[3];
+        mc0[t] -= Sm[0] * kc0[t] + Sm[1] * kc1[t];
+        mc1[t] -= Sm[2] * kc0[t] + Sm[3] * kc1[t];
+      }
+#pragma unroll
+      for (int s = 0; s < RS; ++s) {
+        const double k0 = sh.kw[w][s][0], k1 = sh.kw[w][s][1];
+        const double p0 = sh.kw[w][s][2], p1 = sh.kw[w][s][3];
+#pragma unroll
+        for (int t = 0; t < CS; ++t)
+          sg[s][t] = fma(-p1, kc1[t], fma(-p0, kc0[t],
+                         fma(-k1, mc1[t], fma(-k0, mc0[t], sg[s][t]))));
+      }
     }
     double xt = xl + (K0 * nv0 + K1 * nv1);  // slam.cpp:261
     if (rl == 0) {                            // slam.cpp:267

@@ -28,6 +28,7 @@ EXPORTS = [
     "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_predict",
     "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_get_pose",
     "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status", "ekf_defer",
+    "ekf_set_joseph",
     "ekf_reset", "slam_reset",
     "ekf_profile_enable", "ekf_profile_read", "ekf_sigma_pass_bytes", "ekf_normalize_angle",
     "slam_create", "slam_destroy", "slam_joint_states", "slam_markers", "slam_initial_pose",
@@ -83,6 +84,7 @@ def lib():
             "ekf_set_state": (_i, [_vp, _i, _vp, _vp, _vp, C.c_uint]),
             "ekf_get_status": (_i, [_vp, _i, C.POINTER(C.c_uint)]),
             "ekf_defer": (_i, [_vp, _i]),
+            "ekf_set_joseph": (_i, [_vp, _i]),
             "ekf_reset": (_i, [_vp, _i]),
             "slam_reset": (_i, [_vp]),
             "ekf_profile_enable": (_i, [_vp, _i]),
@@ -252,6 +254,9 @@ class EKF:
     def reset(self, f=-1):
         _check(lib().ekf_reset(self.h, f), "ekf_reset")
 
+    def set_joseph(self, on=True) -> int:
+        return lib().ekf_set_joseph(self.h, int(on))
+
     def status(self, f=0) -> int:
         fl = C.c_uint(0)
         _check(lib().ekf_get_status(self.h, f, C.byref(fl)), "ekf_get_status")
@@ -294,6 +299,9 @@ class Slam:
     def reset(self):
         """A fresh node on the same handle (slam_reset)."""
         _check(lib().slam_reset(self.h), "slam_reset")
+
+    def set_joseph(self, on=True) -> int:
+        return lib().ekf_set_joseph(lib().slam_filter(self.h), int(on))
 
     def profile(self, enable=True):
         lib().ekf_profile_enable(lib().slam_filter(self.h), int(enable))

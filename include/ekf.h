@@ -115,6 +115,12 @@ int ekf_associate_correct(ekf_t h, int filter, double rel_x, double rel_y, int* 
 /* Posterior (slam.cpp:273-291): t_map_odom = T(x, y, θ)·t_odom_robot⁻¹. */
 int ekf_posterior(ekf_t h, int filter);
 
+/* Joseph-form covariance update, opt-in (off by default, like the reference, which applies
+ * Σ ← (I − KH)Σ at slam.cpp:264-265): Σ ← (I − KH)Σ(I − KH)ᵀ + KRKᵀ for every later correction.
+ * Equal in exact arithmetic with the optimal gain; it differs only in rounding. Resident path only
+ * (EKF_E_ARG on the pipeline, whose rank-(2+2m) factors carry the simple form). */
+int ekf_set_joseph(ekf_t h, int on);
+
 /* Deferred submission. While on, the callbacks above only plan their work on the host; the plan
  * goes to the device in one upload (and, on the resident path, one kernel launch) when it reaches
  * 8192 descriptors, when a synchronising call below needs the state, or when deferral is turned

@@ -90,6 +90,7 @@ struct orc_ekf {
   int N, n;
   double q, r, init_var, gate;
   int literal;
+  int joseph;     /* Joseph-form Σ update (opt-in; the reference uses (I − KH)Σ) */
   double* x;      /* n    */
   double* S;      /* n×n  */
   double* T1;     /* n×n scratch (literal mode) */
@@ -97,6 +98,7 @@ struct orc_ekf {
   double* PHt;    /* n×2  */
   double* HP;     /* 2×n  */
   double* H;      /* 2×n dense (literal mode) */
+  double* PH0;    /* n×2 : Σ·Hᵀ kept for the Joseph form (PHt is overwritten by K) */
   unsigned counter;      /* counter_obstacles, slam.cpp:670 */
   double tmo[3];         /* t_map_odom, slam.cpp:659 */
   double prev[3];        /* filter_previous_configuration, slam.cpp:660 */
@@ -140,6 +142,7 @@ orc_ekf* orc_ekf_create(int n_landmarks, double q_noise, double r_noise, double 
   f->PHt = (double*)calloc((size_t)n * 2, sizeof(double));
   f->HP = (double*)calloc((size_t)n * 2, sizeof(double));
   f->H = (double*)calloc((size_t)n * 2, sizeof(double));
+  f->PH0 = (double*)calloc((size_t)n * 2, sizeof(double));
   if (literal) {
     f->T1 = (double*)calloc((size_t)n * n, sizeof(double));
     f->T2 = (double*)calloc((size_t)n * n, sizeof(double));
@@ -152,10 +155,21 @@ orc_ekf* orc_ekf_create(int n_landmarks, double q_noise, double r_noise, double 
 void orc_ekf_destroy(orc_ekf* f) {
   if (!f) return;
   free(f->x); free(f->S); free(f->PHt); free(f->HP); free(f->H); free(f->T1); free(f->T2);
+  free(f->PH0);
   free(f);
 }
 
 int orc_ekf_dim(const orc_ekf* f) { return f->n; }
+
+/* Joseph form, opt-in (BASELINE.json north_star; SURVEY.md §8b `joseph`): Σ ← (I−KH)Σ(I−KH)ᵀ + KRKᵀ
+ * in place of slam.cpp:264-265's (I−KH)Σ. Equal in exact arithmetic with the optimal gain. */
+void orc_ekf_set_joseph(orc_ekf* f, int on) {
+  f->joseph = on;
+  if (on && f->literal && !f->T1) {
+    f->T1 = (double*)calloc((size_t)f->n * f->n, sizeof(double));
+    f->T2 = (double*)calloc((size_t)f->n * f->n, sizeof(double));
+  }
+}
 
 void orc_ekf_set_odom(orc_ekf* f, double theta, double x, double y) {
   f->todom[0] = theta; f->todom[1] = x; f->todom[2] = y;
@@ -282,6 +296,7 @@ static int correct_slot(orc_ekf* f, int k, double zr, double zb) {
   const double nu0 = zr - zhat[0];
   const double nu1 = orc_normalize_angle(zb - zhat[1]);
   /* K = (Σ*Hᵀ)*inv(S) (n×2), state += K·ν (:261) */
+  if (f->joseph) memcpy(f->PH0, PHt, sizeof(double) * 2 * (size_t)n);
   for (int i = 0; i < n; ++i) {
     const double p0 = PHt[2 * i], p1 = PHt[2 * i + 1];
     const double k0 = p0 * Si[0] + p1 * Si[2];
@@ -290,7 +305,39 @@ static int correct_slot(orc_ekf* f, int k, double zr, double zb) {
     f->x[i] = f->x[i] + (k0 * nu0 + k1 * nu1);
   }
   /* Σ = (I − K*Hj)*Σ (:264-265) */
-  if (f->literal) {
+  if (f->joseph && f->literal) {
+    /* (I − KH)·Σ·(I − KH)ᵀ + K·R·Kᵀ as dense products */
+    double* IKH = f->T1;
+    const double* Hd = f->H;
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < n; ++c)
+        IKH[(size_t)i * n + c] = (i == c ? 1.0 : 0.0) - (PHt[2 * i] * Hd[c] + PHt[2 * i + 1] * Hd[n + c]);
+    gemm_nn(n, IKH, S, f->T2);                       /* T2 = (I − KH)Σ */
+    for (int i = 0; i < n; ++i)                      /* T1 ← (I − KH)ᵀ */
+      for (int c = i + 1; c < n; ++c) {
+        const double t = IKH[(size_t)i * n + c];
+        IKH[(size_t)i * n + c] = IKH[(size_t)c * n + i];
+        IKH[(size_t)c * n + i] = t;
+      }
+    gemm_nn(n, f->T2, IKH, S);                       /* Σ = T2 (I − KH)ᵀ */
+    for (int i = 0; i < n; ++i)                      /* + K R Kᵀ, R = r·I₂ */
+      for (int c = 0; c < n; ++c)
+        S[(size_t)i * n + c] += f->r * (PHt[2 * i] * PHt[2 * c] + PHt[2 * i + 1] * PHt[2 * c + 1]);
+  } else if (f->joseph) {
+    /* Σ − K·(HΣ) − (ΣHᵀ)·Kᵀ + K·S·Kᵀ, S = HΣHᵀ + R (the expansion of the Joseph form) */
+    const double* P0 = f->PH0;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+      const double k0 = PHt[2 * i], k1 = PHt[2 * i + 1];
+      const double p0 = P0[2 * i], p1 = P0[2 * i + 1];
+      double* row = S + (size_t)i * n;
+      for (int c = 0; c < n; ++c) {
+        const double q0 = PHt[2 * c], q1 = PHt[2 * c + 1];
+        const double ks = k0 * (Sm[0] * q0 + Sm[1] * q1) + k1 * (Sm[2] * q0 + Sm[3] * q1);
+        row[c] = row[c] - (k0 * HP[c] + k1 * HP[n + c]) - (p0 * q0 + p1 * q1) + ks;
+      }
+    }
+  } else if (f->literal) {
     double* IKH = f->T1;
     const double* Hd = f->H;
     for (int i = 0; i < n; ++i)

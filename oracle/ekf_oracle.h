@@ -40,6 +40,8 @@ orc_ekf* orc_ekf_create(int n_landmarks, double q_noise, double r_noise, double 
                         double mah_gate, int literal);
 void orc_ekf_destroy(orc_ekf* f);
 int  orc_ekf_dim(const orc_ekf* f);
+/* opt-in Joseph-form update (I−KH)Σ(I−KH)ᵀ + KRKᵀ in place of slam.cpp:264-265's (I−KH)Σ */
+void orc_ekf_set_joseph(orc_ekf* f, int on);
 void orc_ekf_set_odom(orc_ekf* f, double theta, double x, double y);   /* t_odom_robot */
 void orc_ekf_predict(orc_ekf* f);                                        /* slam.cpp:184-198 */
 int  orc_ekf_correct(orc_ekf* f, int id, double rel_x, double rel_y);    /* slam.cpp:207-268 */

@@ -54,6 +54,7 @@ def lib():
         L.orc_ekf_set.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_uint]
         L.orc_ekf_get_prev.argtypes = [C.c_void_p, _dp]
+        L.orc_ekf_set_joseph.argtypes = [C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -94,11 +95,13 @@ class OracleEKF:
     """One filter of the C oracle. literal=True is the reference's dense O(n³) arithmetic."""
 
     def __init__(self, n_landmarks=50, q_noise=1e-2, r_noise=1e-2, init_var=10e6,
-                 mah_gate=2.0, literal=False):
+                 mah_gate=2.0, literal=False, joseph=False):
         self.N = n_landmarks
         self.n = 3 + 2 * n_landmarks
         self.h = lib().orc_ekf_create(n_landmarks, q_noise, r_noise, init_var, mah_gate,
                                       int(literal))
+        if joseph:
+            lib().orc_ekf_set_joseph(self.h, 1)
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -250,3 +250,38 @@ def test_deferred_submission_and_reset(resident, monkeypatch):
     assert np.abs(x1 - x2).max() < 1e-9 and np.abs(S1 - S2).max() < 1e-9
     assert np.abs(poses - g["poses"]).max() < TOL
     assert np.abs(S1 - g["sigma"]).max() < TOL
+
+
+@pytest.mark.parametrize("name", ["basic_world_known", "basic_world_assoc", "synth16_known",
+                                  "crowded_assoc"])
+def test_joseph_form_matches_oracle(name, monkeypatch):
+    """Opt-in Joseph-form update (BASELINE.json north_star; off by default like slam.cpp:264-265)
+    against the C oracle's Joseph mode on the same drive. Same tolerance as the swarm test: the
+    Joseph expansion adds two rank-2 terms whose rounding meets the 1e7 first-sighting
+    cancellation (the oracle's literal and structured Joseph modes differ by up to 4e-9)."""
+    _env(monkeypatch, True)
+    sc, g = load_golden(name)
+    assoc = bool(g["assoc"])
+    s = pyekf.Slam(n_landmarks=sc.n_landmarks,
+                   source=pyekf.SOURCE_ASSOC if assoc else pyekf.SOURCE_SIM,
+                   track=sc.track, radius=sc.radius)
+    assert s.set_joseph(True) == pyekf.EKF_OK
+    rc, poses, _ = s.replay(sc)
+    x, S, cnt = s.filter_state()
+    s.close()
+    o = orc.run_scenario(sc, assoc, joseph=True)
+    assert rc == pyekf.EKF_OK
+    assert cnt == o["counter"]
+    assert np.abs(poses - o["poses"]).max() < SWARM_TOL
+    assert np.abs(x - o["state"]).max() < SWARM_TOL
+    assert np.abs(S - o["sigma"]).max() < SWARM_TOL
+    # the simple form and the Joseph form agree to rounding
+    assert np.abs(poses - g["poses"]).max() < 1e-7
+
+
+def test_joseph_form_rejected_on_pipeline(monkeypatch):
+    _env(monkeypatch, False)
+    e = pyekf.EKF(n_landmarks=50)
+    assert e.path == pyekf.EKF_PATH_PIPELINE
+    assert e.set_joseph(True) == pyekf.EKF_E_ARG
+    assert e.set_joseph(False) == pyekf.EKF_OK

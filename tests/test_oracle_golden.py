@@ -49,3 +49,20 @@ def test_oracle_delete_only_message_is_predict_only():
     x, S, tmo, _ = f.get()
     assert np.allclose(x[:3], [0.1, 0.2, 0.0]) and np.all(x[3:] == 0)
     assert np.allclose(np.diag(S)[:3], 1e-2)
+
+
+@pytest.mark.parametrize("assoc", [False, True], ids=["known", "assoc"])
+def test_oracle_joseph_modes_agree(assoc):
+    """The opt-in Joseph form in the C oracle: the literal dense (I−KH)Σ(I−KH)ᵀ + KRKᵀ and the
+    structured expansion Σ − K·HΣ − ΣHᵀ·Kᵀ + K·S·Kᵀ agree, and both stay within rounding of the
+    reference's simple form (slam.cpp:264-265; equal in exact arithmetic with the optimal gain)."""
+    from pyekf import synth
+    sc = synth.synthetic(20, 30, seed=7, max_markers=6, shuffle=assoc)
+    js = orc.run_scenario(sc, assoc, joseph=True)
+    jl = orc.run_scenario(sc, assoc, joseph=True, literal=True)
+    simple = orc.run_scenario(sc, assoc)
+    assert js["counter"] == jl["counter"] == simple["counter"]
+    assert np.abs(js["sigma"] - jl["sigma"]).max() < 1e-8
+    assert np.abs(js["poses"] - jl["poses"]).max() < 1e-9
+    assert np.abs(js["sigma"] - simple["sigma"]).max() < 3e-8
+    assert np.abs(js["poses"] - simple["poses"]).max() < 1e-9
