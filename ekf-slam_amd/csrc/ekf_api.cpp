@@ -726,6 +726,12 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     if (hipMemsetAsync(h->x[p], 0, h->x_stride * h->F * sizeof(double), h->stream) != hipSuccess)
       return fail(EKF_E_HIP);
   }
+  // chunk records and the rows hand-off start zeroed: no kernel ever sees a previous process's
+  // bytes, whatever the stream interleaving
+  if (hipMemsetAsync(h->rec, 0, 2 * sizeof(ChunkRec) * h->F, h->stream) != hipSuccess ||
+      (h->rows && hipMemsetAsync(h->rows, 0, sizeof(double) * kRowW * h->ldk * h->F,
+                                 h->stream) != hipSuccess))
+    return fail(EKF_E_HIP);
   if (hipMemsetAsync(h->kcat, 0, km_bytes, h->stream) != hipSuccess ||
       hipMemsetAsync(h->mcat, 0, km_bytes, h->stream) != hipSuccess ||
       hipMemsetAsync(h->ctl, 0, sizeof(FilterCtl) * h->F, h->stream) != hipSuccess)

@@ -86,6 +86,8 @@ struct ResShared {
   double blk[(W * RS) / 2][4];  // association: Σ[jk..jk+1][jk..jk+1] of landmark k
   double xall[W * RS];          // association: x
   int dec[2];                   // association decision: slot j, is_new
+  int decj[kMaxAssoc], decn[kMaxAssoc];  // decisions by slot, stored to FilterCtl at the end
+  double junk[64];                        // sink of the branch-free block gather
   double kw[W][RS][4];          // per wave: K[row(s)] (and Joseph: (Σ·Hᵀ)[row(s)]), wave-private
 };
 
@@ -98,7 +100,7 @@ __device__ __forceinline__ int pos5(int r, int j) {
 // One workgroup per filter flo + blockIdx.x; walks the whole plan (PlanEntry list, in order) and
 // applies the entries that name its filter. Σ / x are loaded on the first active entry from the
 // entry's parity and written back once, to the parity the host's plan ends on.
-template <int W, int RS, int CS>
+template <int W, int RS, int CS, bool JOSEPH>
 __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const PlanEntry* plan,
                                                      int nplan, int flo) {
   constexpr int kRW = W;
@@ -121,6 +123,7 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
   bool post = false;
   double podom[3] = {0.0, 0.0, 0.0};
   unsigned counter = 0, status = 0;
+  unsigned long long dslots = 0;  // association slots decided in this launch (sh.decj/decn)
   int par = -1;          // current parity (−1: not loaded yet)
   bool dirty = false;    // Σ / x changed (a chunk entry ran)
   int b = 0;             // gather buffer
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!A.joseph) {  // Σ ← Σ − K·(HΣ), slam.cpp:264-265
+    if constexpr (!JOSEPH) {  // Σ ← Σ − K·(HΣ), slam.cpp:264-265
 #pragma unroll
       for (int s = 0; s < RS; ++s) {
         const double k0 = sh.kw[w][s][0], k1 = sh.kw[w][s][1];  // broadcast reads
@@ -427,27 +430,37 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
         if (counter >= static_cast<unsigned>(N)) {  // the reference indexes out of range
           status |= EKF_FLAG_RANGE_D;
           if (tid == 0) {
-            ctl->assoc_j[slot] = -1;
-            ctl->assoc_new[slot] = 0;
+            sh.decj[slot] = -1;
+            sh.decn[slot] = 0;
           }
+          dslots |= 1ull << slot;
         } else {
+          RS_STAMP(ncorr, 0);
           b ^= 1;
           gather(b, -8, 0);  // pose rows / columns and pose x
-          // landmark 2×2 blocks and every x
+          // landmark 2×2 blocks of the seen landmarks (rows < 3 + 2·counter): every (slot,
+          // column) element stores — to its block entry when it is one, else to this lane's junk
+          // slot. The row index is taken as a vector value (tid >> 6 unmerged), so the index
+          // math runs on each SIMD's VALU, not on the CU's one scalar unit.
+          {
+            const int wv = static_cast<int>(threadIdx.x) >> 6;
+            const int rmax = 3 + 2 * static_cast<int>(counter);
 #pragma unroll
-          for (int s = 0; s < RS; ++s) {
-            const int r = row(s);
-            if (r >= 3 && r < n) {
+            for (int s = 0; s < RS; ++s) {
+              if (row(s) >= rmax) break;  // rows grow with s
+              const int r = wv + kRW * s;
               const int k = (r - 3) >> 1, e = (r - 3) & 1;
 #pragma unroll
               for (int t = 0; t < CS; ++t) {
                 const int dc = col(t) - (3 + 2 * k);
-                if (dc == 0 || dc == 1) sh.blk[k][2 * e + dc] = sg[s][t];
+                const bool in = r >= 3 && (dc == 0 || dc == 1);
+                *(in ? &sh.blk[k < 0 ? 0 : k][2 * e + dc] : &sh.junk[lane]) = sg[s][t];
               }
             }
           }
           if (rown && rl >= 3 && rl < n) sh.xall[rl] = xl;
           __syncthreads();
+          RS_STAMP(ncorr, 6);
           if (w == 0) {
             const double pose[3] = {sh.gx[b][0], sh.gx[b][1], sh.gx[b][2]};
             double bestd = INFINITY;
@@ -518,11 +531,12 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
               const int jsel = nw ? static_cast<int>(counter) : bestk;
               sh.dec[0] = jsel;
               sh.dec[1] = nw;
-              ctl->assoc_j[slot] = jsel;
-              ctl->assoc_new[slot] = nw;
+              sh.decj[slot] = jsel;
+              sh.decn[slot] = nw;
             }
           }
           __syncthreads();
+          dslots |= 1ull << slot;
           const int k = sh.dec[0];
           const int j = 3 + 2 * k;
           if (sh.dec[1]) {  // slam.cpp:351-356, kept (:421)
@@ -533,7 +547,9 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
             set_x(j + 1, p2 + z0 * sn);
             ++counter;
           }
+          RS_STAMP(ncorr, 7);
           gather(b, j, 3);  // the pose rows / columns are in b already
+          RS_STAMP(ncorr, 5);
           __syncthreads();
           correct(j, z0, z1, true);
         }
@@ -551,6 +567,11 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
   }
   if (par < 0) return;  // the plan does not name this filter
   if (post) posterior_now();
+  __syncthreads();  // the decisions in LDS
+  if (tid < kMaxAssoc && (dslots >> tid & 1)) {
+    ctl->assoc_j[tid] = sh.decj[tid];
+    ctl->assoc_new[tid] = sh.decn[tid];
+  }
   if (dirty) {
     double* S = A.sig[par] + f * A.sig_stride;
     double* X = A.x[par] + f * A.x_stride;
@@ -590,12 +611,13 @@ hipError_t launch_resident(const PassArgs<double>& a, const PlanEntry* plan, int
   };
   // 4 waves (one per SIMD): the per-correction scalar work (geometry, S, gather control) runs
   // once per wave on the CU's one scalar unit, so fewer, wider waves finish a step sooner
+  // Joseph form is its own instantiation: the default update keeps its register budget
   if (a.n <= 64)
-    go(k_resident<4, 16, 1>, 4);
-  else if (a.n <= 4 * 26)
-    go(k_resident<4, 26, 2>, 4);  // N = 50 (n = 103): no idle row slots
+    a.joseph ? go(k_resident<4, 16, 1, true>, 4) : go(k_resident<4, 16, 1, false>, 4);
+  else if (a.n <= 4 * 26)  // N = 50 (n = 103): no idle row slots
+    a.joseph ? go(k_resident<4, 26, 2, true>, 4) : go(k_resident<4, 26, 2, false>, 4);
   else
-    go(k_resident<4, 32, 2>, 4);
+    a.joseph ? go(k_resident<4, 32, 2, true>, 4) : go(k_resident<4, 32, 2, false>, 4);
   return hipGetLastError();
 }
 

@@ -220,6 +220,7 @@ def test_n1024_fp32_warm_state_against_oracle():
         d = np.abs(poses[t, 0] - xr[:3])
         assert d.max() < 2e-4, (t, d)
     x32, S32, _ = ekf32.state()
+    assert ekf32.status() == 0  # no numeric skip, no epoch-poll timeout
     seen = np.abs(np.diag(S32)) < 1e6
     assert np.all(np.diag(S32)[seen][3:] > 0)
     assert np.all(np.isfinite(S32))

@@ -15,12 +15,13 @@ import pyekf  # noqa: E402
 from pyekf import synth  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 50
-sc = synth.synthetic(N, 30, max_markers=4)
+assoc = len(sys.argv) > 2 and sys.argv[2] == "assoc"
+sc = synth.make_scenario(N, synth.random_landmarks(20, seed=5), 30, max_markers=4, shuffle=assoc)
 odom = pyekf.odometry(sc)
 e = pyekf.EKF(n_landmarks=N)
-print("path", e.path)
-e.replay(sc.count[:, None], sc.rel[:, None], odom[:, None], ids=sc.ids[:, None],
-         actions=sc.actions[:, None])
+print("path", e.path, "assoc" if assoc else "known")
+e.replay(sc.count[:, None], sc.rel[:, None], odom[:, None], ids=None if assoc else sc.ids[:, None],
+         actions=sc.actions[:, None], assoc=assoc)
 e.sync()
 L = pyekf.lib()
 st = (C.c_ulonglong * 512)()
@@ -30,5 +31,7 @@ s = np.array(st[:], dtype=np.int64).reshape(64, 8)
 for k in range(0, 24):
     r = s[k]
     nxt = s[k + 1][0] - r[0]
-    print(f"corr {k:2d}: gather {r[5]-r[0]:5d} barrier {r[1]-r[5]:5d} geom {r[2]-r[1]:5d} "
+    pre = (f"gatherA+barrier {r[6]-r[0]:5d} wave0 assoc+barrier {r[7]-r[6]:5d} gatherB {r[5]-r[7]:5d}"
+           if assoc else f"gather {r[5]-r[0]:5d}")
+    print(f"corr {k:2d}: {pre} barrier {r[1]-r[5]:5d} geom {r[2]-r[1]:5d} "
           f"S {r[3]-r[2]:5d} update {r[4]-r[3]:5d} -> next start {nxt:6d}")
