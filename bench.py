@@ -70,7 +70,7 @@ def _pmc_pass(args, counters):
     if not os.path.exists(exe):
         return None, "rocprofv3 not found"
     # the workload's own instantiation (the fp32 workload's fp64 warm-up lap is excluded)
-    kname = "k_sigma_pass<float>" if WORKLOADS[args.workload][1] == "f32" else "k_sigma_pass<double>"
+    kname = "k_sigma_pass<float," if WORKLOADS[args.workload][1] == "f32" else "k_sigma_pass<double,"
     d = tempfile.mkdtemp(prefix="ekf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     cmd = [exe, "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
            sys.executable, os.path.abspath(__file__), "--workload", args.workload,

@@ -23,6 +23,7 @@
 #include <cfloat>
 #include <climits>
 #include <cstdint>
+#include <type_traits>
 
 #include "ekf_device.hpp"
 #include "ekf_launch.hpp"
@@ -1467,9 +1468,6 @@ __device__ __forceinline__ double ld_f64(__amdgpu_buffer_rsrc_t r, unsigned vo, 
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
 }
 
-#ifndef EKF_SIGMA64_TJ
-#define EKF_SIGMA64_TJ 2  // fp64 tile = 32 × 16·TJ
-#endif
 template <typename T>
 struct SigmaTile;
 
@@ -1528,10 +1526,14 @@ struct SigmaTile<float> {
   }
 };
 
-template <>
-struct SigmaTile<double> {
-  static constexpr int kRows = 32, kCols = 16 * EKF_SIGMA64_TJ;
-  static constexpr int TJ = EKF_SIGMA64_TJ;
+// fp64 tile of 32 × 16·TJ: TJ = 2 for a few filters (more waves per filter), TJ = 4 for swarms
+// (≥ 16 filters): the M operand rows are read once per 64 columns instead of per 32 — the
+// operand loads are the pass's VMEM bottleneck there (swarm pass 589 → 564 µs; one filter's pass
+// 5.2 → 7.6 µs, so it keeps TJ = 2)
+template <int TJ_>
+struct SigmaTile64 {
+  static constexpr int TJ = TJ_;
+  static constexpr int kRows = 32, kCols = 16 * TJ;
   // rows ≠ null (kRowsOut): also Σ_out[i, U_next] → rows[b·ldk + i] for the next chunk's factor
   // kernel, b = the first position of the column in U_next (nxt[0..nnu))
   static __device__ __forceinline__ void run(const double* Sin, double* Sout, const double* kc,
@@ -1616,14 +1618,20 @@ struct SigmaTile<double> {
         }
   }
 };
+template <>
+struct SigmaTile<double> : SigmaTile64<2> {};
+// the tile a Σ pass of T runs: WIDE (swarms) takes the 32 × 64 fp64 tile
+template <typename T, bool WIDE>
+using PassTile = typename std::conditional<sizeof(T) == 8 && WIDE, SigmaTile64<4>, SigmaTile<T>>::type;
 
 // xcd_b = 0: grid (blocks per filter, filters). xcd_b = B > 0 (many filters): a 1-D grid whose
 // block L runs on XCD L % 8 (dispatch deals blocks round-robin over the XCDs); it is given filter
 // 8·⌊(L/8)/B⌋ + L % 8, tile block (L/8) % B, so all of a filter's blocks share one XCD and its
 // Kcat/Mcat are fetched into one L2 instead of eight. Placement only changes speed.
 // Waves take tiles row-major over a trows × tcols grid.
-template <typename T>
+template <typename T, bool WIDE>
 __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, int xcd_b, int nf) {
+  using Tile = PassTile<T, WIDE>;
   SIG_STAMP(0);
   int fb = blockIdx.y, bx = blockIdx.x;
   if (xcd_b > 0) {
@@ -1635,7 +1643,7 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
   const MsgDesc& d = A.desc[fb];
   __shared__ int cmap[4][64];  // per wave: kRowsOut column → position in U_next
   const int lane = threadIdx.x & 63;
-  const int trows = (A.n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows;
+  const int trows = (A.n + Tile::kRows - 1) / Tile::kRows;
   // the wave's tile index, provably wave-uniform (readfirstlane): the buffer descriptors built
   // from it stay in SGPRs instead of a waterfall loop around every buffer access
   const int t = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
@@ -1645,10 +1653,10 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
     const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
     const int tr = t / tcols, tc = t - tr * tcols;
     T* rows = (d.flags & kRowsOut) ? A.rows + f * A.rows_stride : nullptr;
-    SigmaTile<T>::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
+    Tile::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
                       A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
-                      (d.flags & kFirst) != 0, A.q, tr * SigmaTile<T>::kRows,
-                      tc * SigmaTile<T>::kCols, lane, rows, d.nxt_u, d.nxt_nu,
+                      (d.flags & kFirst) != 0, A.q, tr * Tile::kRows,
+                      tc * Tile::kCols, lane, rows, d.nxt_u, d.nxt_nu,
                       cmap[threadIdx.x >> 6]);
   }
   SIG_STAMP(3);
@@ -1907,15 +1915,20 @@ template <typename T>
 hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, hipStream_t s,
                              hipEvent_t e0, hipEvent_t e1) {
   constexpr int wpb = 4;  // waves per workgroup
-  const int trows = (a.n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows;
-  const int tcols = (a.n + SigmaTile<T>::kCols - 1) / SigmaTile<T>::kCols;
-  const int per_filter = (trows * tcols + wpb - 1) / wpb;
-  if (nf >= 16) {  // XCD-aware 1-D grid (see k_sigma_pass)
+  if (nf >= 16) {  // XCD-aware 1-D grid (see k_sigma_pass), wide fp64 tiles
+    using Tile = PassTile<T, true>;
+    const int trows = (a.n + Tile::kRows - 1) / Tile::kRows;
+    const int tcols = (a.n + Tile::kCols - 1) / Tile::kCols;
+    const int per_filter = (trows * tcols + wpb - 1) / wpb;
     const dim3 grid(8 * ((nf + 7) / 8) * per_filter);
-    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, per_filter, nf);
+    launch(k_sigma_pass<T, true>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, per_filter, nf);
   } else {
+    using Tile = PassTile<T, false>;
+    const int trows = (a.n + Tile::kRows - 1) / Tile::kRows;
+    const int tcols = (a.n + Tile::kCols - 1) / Tile::kCols;
+    const int per_filter = (trows * tcols + wpb - 1) / wpb;
     const dim3 grid(per_filter, nf);
-    launch(k_sigma_pass<T>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
+    launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
   }
   if constexpr (sizeof(T) == 4)
     hipLaunchKernelGGL(k_pend_scatter, dim3(nf), dim3(256), 0, s, a);
