@@ -36,6 +36,10 @@ WORKLOADS = {
     "swarm_n256_fp64": (256, "f64", 512, 16,
                         "configs[3]: N=256 landmarks x 512 independent filters per GPU, fp64"),
     "basic_world": (50, "f64", 1, 4, "configs[0]: basic_world 4 landmarks in 50 slots, fp64"),
+    # Monte-Carlo swarm at the reference's own map size (resident path, one CU-resident filter
+    # per workgroup): configs[0]'s filter × 1024 seeded runs per GPU
+    "swarm_basic_world": (50, "f64", 1024, 4,
+                          "configs[0] x 1024 Monte-Carlo runs per GPU (basic_world, fp64)"),
 }
 
 
@@ -444,7 +448,7 @@ def main():
             # its bound is the sequential f64 chain of one CU per filter, priced against that
             # CU's share of the fp64 vector peak (78.6 TF / 256 CUs)
             flops = 4.0 * n * n * res_corr  # Σ ← Σ − K·(HΣ): 2 FMAs per element per correction
-            sec = ms_res / n_res / 1e3
+            sec = ms_res / 1e3  # every launch of the profiled replay (res_corr spans them all)
             cu_peak = MFMA_PEAK_TF["f64"] / 256 * min(F, 256)
             result["roofline"] = {
                 "kernel": "k_resident", "bound": "fp64-valu, one CU per filter (latency chain)",
@@ -452,9 +456,10 @@ def main():
                 "frac": flops / sec / 1e12 / cu_peak, "traffic": None,
                 "traffic_detail": traffic_err,
                 "flops_formula": f"4*n^2*corrections = 4*{n}^2*{res_corr}",
-                "avg_launch_us": sec * 1e6, "launches": n_res,
+                "avg_launch_us": sec * 1e6 / n_res, "launches": n_res,
                 "us_per_correction": sec * 1e6 / max(res_corr, 1),
                 "hbm_bytes_per_launch": 2.0 * n * n * 8 * F,
+                "kernel_corrections_per_s": res_corr / sec,
             }
             result["config"]["device_path"] = "resident"
     # ---- CPU baseline + parity (rank 0, N=1 only) ----

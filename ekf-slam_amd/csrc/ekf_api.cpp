@@ -356,7 +356,8 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
       int flags = kActive;
       if (chunk == 0 && (predict || h->pending[f])) flags |= kFirst;
       if (chunk == nchunks - 1 && predict) flags |= kLast;
-      if (h->prev_m[f] >= 0) flags |= kLook;  // rebuild from the chunk before (its Σ pass may run)
+      // rebuild from the chunk before (its Σ pass may run); the resident kernel carries Σ itself
+      if (h->prev_m[f] >= 0 && !h->resident) flags |= kLook;
       fill_desc(d, m, flags, h->parity[f], h->odom[f]);
       d->prev_m = h->prev_m[f];
       for (int i = 0; i < kMaxChunk; ++i) d->prev_ids[i] = h->prev_ids[f][i];
@@ -368,7 +369,7 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
       if (flags & kLook) index_map(d, h->cfg.n_landmarks);
       // fp64: the previous chunk's Σ pass (same plan, not uploaded yet) hands this chunk's factor
       // kernel Σ_in[i, U] as contiguous rows instead of a gather strided by ld
-      if (h->rows && h->last_desc[f] >= 0 && m > 0) {
+      if (h->rows && !h->resident && h->last_desc[f] >= 0 && m > 0) {
         MsgDesc* pd = &h->plan_d[h->last_desc[f]];
         pd->flags |= kRowsOut;
         pd->nxt_nu = 3 + 2 * m;
