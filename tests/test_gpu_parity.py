@@ -237,6 +237,8 @@ def _pipelined_final(sc, monkeypatch, env, dtype=pyekf.EKF_F64, F=1):
     rep = lambda a: np.repeat(a[:, None], F, 1)  # noqa: E731
     e.replay(rep(sc.count), rep(sc.rel), rep(odom), ids=rep(sc.ids), actions=rep(sc.actions))
     out = [e.state(f) for f in range(F)]
+    # no numeric skip and no epoch-poll timeout (EKF_FLAG_TIMEOUT = 4) in any schedule
+    assert [e.status(f) for f in range(F)] == [0] * F, env
     e.close()
     return out
 
