@@ -275,8 +275,10 @@ int create_streams(ekf_ctx* h) {
     for (int b = 0; b < cus; ++b) (b < split * kXcd ? mmain : mbulk)[b / 32] |= 1u << (b % 32);
     if (hipExtStreamCreateWithCUMask(&h->stream, words, mmain.data()) == hipSuccess &&
         hipExtStreamCreateWithCUMask(&h->bulk, words, mbulk.data()) == hipSuccess) {
+      // device-epoch hand-offs are opt-in (EKF_DEVSYNC=1): a rare non-finite result in that mode
+      // is open (known issue); the default synchronises the streams with events
       const char* e = std::getenv("EKF_DEVSYNC");
-      h->devsync = !(e && std::atoi(e) == 0);
+      h->devsync = e && std::atoi(e) == 1;
       return EKF_OK;
     }
     if (h->stream) hipStreamDestroy(h->stream);
