@@ -1,22 +1,23 @@
 // HIP kernels (gfx950 / CDNA4) for the EKF-SLAM predict → correct* → posterior path of
 // maxipalay/ekf-slam nuslam/src/slam.cpp.
 //
-// One message (up to kMaxChunk markers) is one launch pair:
+// A chunk (one message, up to kMaxChunk markers) runs as three kernels:
 //
-//   k_gain        The m corrections of a message only couple through the rows/columns the message
-//                 touches, U = {θ, x, y} ∪ {jx, jy per marker} (|U| ≤ 3+2m). Every workgroup first
-//                 replays the m corrections on the |U|×|U| block in LDS (predict folded in), which
-//                 gives each step's H, S⁻¹, ν and K[U], M[:,U]. Then every thread owns one row
-//                 (or one column) of Σ, gathers its |U| entries and runs the same m steps on them,
-//                 emitting K_c[i] (rows) / M_c[:,c] (columns) and the new state x[i].
+//   k_chain       One workgroup per filter. The m corrections of a chunk only couple through the
+//                 rows/columns the chunk touches, U = {θ, x, y} ∪ {jx, jy per marker} (|U| ≤ 3+2m).
+//                 The chain replays them on the |U|×|U| block in LDS (predict folded in) — the only
+//                 sequential part — and hands the factor kernel the row / column maps Z (|U|×2m) and
+//                 Y (2m×|U|) plus x[U] through a write-through record (ChunkRec).
+//   k_factors     Kcat = Σ_pred[:, U]·Z and Mcat = Y·Σ_pred[U, :] for every row / column on f64
+//                 MFMA (v_mfma_f64_16x16x4f64), plus the new state x.
 //   k_sigma_pass  Σ_out = Σ_in + Q̄ − Σ_k Kcat[k]ᵀ ⊗ Mcat[k], a rank-(2+2m) update of the dense
 //                 covariance: the predict's two rank-1 terms (A Σ Aᵀ, slam.cpp:198) and one rank-2
-//                 term per correction ((I − KH)Σ, slam.cpp:264-265). It streams Σ once per message
-//                 through MFMA (v_mfma_f64_16x16x4f64 / v_mfma_f32_16x16x4f32), so the HBM cost of
-//                 a correction is 2·n²·w / m instead of the 2·n²·w of a per-correction update.
+//                 term per correction ((I − KH)Σ, slam.cpp:264-265). It streams Σ once per chunk
+//                 through MFMA (v_mfma_f32_32x32x2f32 for fp32 Σ, v_mfma_f64_16x16x4f64 for fp64),
+//                 so the HBM cost of a correction is 2·n²·w / m instead of 2·n²·w.
 //
 // Equal to the reference's sequential dense algebra in exact arithmetic; the summation order
-// differs (tolerances in tests/). Unknown association adds k_assoc before each single-marker pair.
+// differs (tolerances in tests/). Unknown association adds k_assoc before each single-marker chunk.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 

@@ -4,8 +4,8 @@
 // kernel per marker) is built for covariances that live in HBM. At the reference's own map size
 // (N = 50 slots, n = 103: basic_world and the rosbag drive, BASELINE configs[0] and [4]) the whole
 // Σ is 83 KB, and that pipeline is launch- and hand-off-bound (≈ 94 µs per associated marker).
-// Here one 1024-thread workgroup owns one filter for an entire upload (every message of a replay):
-// Σ stays in VGPRs (wave w holds rows w, w+16, …; lane ℓ holds columns ℓ, ℓ+64, …), x with it,
+// Here one 256-thread workgroup (4 waves) owns one filter for an entire upload (every message of a
+// replay): Σ stays in VGPRs (wave w holds rows w, w+4, …; lane ℓ holds columns ℓ, ℓ+64), x with it,
 // and each correction is
 //   gather   the owners of rows / columns {θ, x, y, jx, jy} write them to LDS (10·n doubles);
 //   barrier  (one per correction: the gather buffers are double-buffered);

@@ -49,12 +49,13 @@ class Scenario:
         return int(self.ids.shape[0])
 
     def corrections(self, start: int = 0, stop: int | None = None) -> int:
-        """Number of non-DELETE markers (= EKF correction steps) in messages [start, stop)."""
+        """Number of non-DELETE markers (= EKF correction steps) in messages [start, stop):
+        slam.cpp:205 skips only DELETE; ADD, MODIFY and DELETEALL are corrected."""
         stop = self.n_messages if stop is None else stop
         c = 0
         for t in range(start, stop):
             k = int(self.count[t])
-            c += int(np.count_nonzero(self.actions[t, :k] == ADD))
+            c += int(np.count_nonzero(self.actions[t, :k] != DELETE))
         return c
 
 

@@ -20,6 +20,7 @@ import math
 import numpy as np
 
 PI = 3.14159265358979323846
+MARKER_DELETE = 2  # visualization_msgs::msg::Marker::DELETE
 
 
 def normalize_angle(rad: float) -> float:
@@ -191,7 +192,7 @@ class DenseEKF:
         """slam.cpp:180-316 (publishing omitted)."""
         self.predict()
         for i in range(len(ids)):
-            if actions[i]:
+            if actions[i] == MARKER_DELETE:  # slam.cpp:205: only DELETE (2) is skipped
                 continue
             self.correct_known(int(ids[i]), float(rel_xy[i, 0]), float(rel_xy[i, 1]))
         self.posterior()

@@ -19,6 +19,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#define ORC_MARKER_DELETE 2 /* visualization_msgs::msg::Marker::DELETE */
+
 static const double PI = 3.14159265358979323846;  /* turtlelib/include/turtlelib/geometry2d.hpp PI */
 
 /* turtlelib/src/geometry2d.cpp:5-14 */
@@ -468,11 +470,12 @@ int orc_ekf_fake_sensor_cb(orc_ekf* f, int m, const int* ids, const int* actions
                            const double* rel_xy) {
   if (m <= 0) return -3; /* msg.markers.at(0) throws on an empty array (:281) */
   for (int i = 0; i < m; ++i)
-    if (!actions[i] && (ids[i] < 0 || ids[i] >= f->N)) return -2;
+    if (actions[i] != ORC_MARKER_DELETE && (ids[i] < 0 || ids[i] >= f->N)) return -2;
   orc_ekf_predict(f);
   int rc = 0;
   for (int i = 0; i < m; ++i) {
-    if (actions[i]) continue; /* DELETE markers are skipped (:205) */
+    /* only DELETE (= 2) is skipped (:205); ADD, MODIFY and DELETEALL markers are corrections */
+    if (actions[i] == ORC_MARKER_DELETE) continue;
     const int e = orc_ekf_correct(f, ids[i], rel_xy[2 * i], rel_xy[2 * i + 1]);
     if (e && !rc) rc = e;
   }

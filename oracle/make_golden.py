@@ -66,8 +66,27 @@ def save(name, sc, out, assoc, **meta):
           f"final pose={out['poses'][-1]} counter={out['counter']}")
 
 
+def mixed_actions():
+    """(6) basic_world with the markers' action field varied: only DELETE (2) is skipped by the
+    reference (slam.cpp:205: `marker.action != DELETE`); ADD (0), MODIFY (1) and DELETEALL (3)
+    markers are corrections like any other."""
+    sc = synth.basic_world(60, n_delete=1, seed=20240319)
+    rng = np.random.default_rng(6)
+    for t in range(sc.n_messages):
+        k = int(sc.count[t])
+        for i in range(k):
+            if sc.actions[t, i] != synth.DELETE:
+                sc.actions[t, i] = rng.choice([0, 1, 3])
+    assert np.isin(sc.actions, [1]).any() and np.isin(sc.actions, [3]).any()
+    return sc
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
+    if sys.argv[1:] == ["mixed_actions"]:  # add only this fixture (the others stay as committed)
+        sc = mixed_actions()
+        save("mixed_actions_known", sc, run(sc, False), False)
+        return
     # (1) basic_world, known association, with one far DELETE marker per message (slam.cpp:205)
     sc = synth.basic_world(100, n_delete=1)
     save("basic_world_known", sc, run(sc, False), False)
@@ -87,6 +106,9 @@ def main():
     crowd = np.concatenate([base, base + rng.normal(0, 0.18, size=base.shape)])
     sc = synth.make_scenario(24, crowd, 60, max_markers=6, seed=13, shuffle=True)
     save("crowded_assoc", sc, run(sc, True), True)
+    # (6) MODIFY / DELETEALL actions are corrected, only DELETE is skipped
+    sc = mixed_actions()
+    save("mixed_actions_known", sc, run(sc, False), False)
 
 
 if __name__ == "__main__":

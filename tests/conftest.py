@@ -31,7 +31,7 @@ def built_libraries():
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 GOLDEN_CASES = ["basic_world_known", "basic_world_assoc", "synth16_known", "synth16_assoc",
-                "crowded_assoc"]
+                "crowded_assoc", "mixed_actions_known"]
 
 
 def load_golden(name):
