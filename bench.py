@@ -6,12 +6,20 @@ one filter per GPU, Σ in fp32, known association, 16 markers per sensor message
 A "step" is one sensor message = predict + 16 corrections + posterior (slam.cpp:180-316) through
 the C-ABI (ekf_replay → ekf_batch_sensor). value = corrections/s summed over ranks.
 
-Multi-GPU (torchrun, one process per GPU): every rank runs its own independent filter on its own
-seeded map (weak scaling, no data-path collective); the final poses are gathered once over RCCL.
+Inputs: filter g (global index over all ranks) is seeded --seed + g (its own map,
+slip and sensor noise); an untimed survey drive sights every landmark before the timed circle
+drive, so the timed messages update a fully populated, correlated Σ.
+
+Multi-GPU: `bench.py --gpus N` starts N ranks itself (torch.distributed.run as a child process,
+before anything touches a GPU), or runs as one rank under an external launcher. Every rank runs its
+own independent filters (weak scaling, no data-path collective); the final poses are all-gathered
+once over RCCL. configs[3] (N=256 × 4096 filters over 8 GPUs) is
+`bench.py --workload swarm_n256_fp64 --gpus 8` (512 filters per rank).
 
 Also reported: the Σ-pass roofline (HIP events on the library's stream), the CPU baseline (the
-oracle's literal dense restatement of slam.cpp on the host cores, rank 0 only) and pose parity of
-the first timed messages against the fp64 oracle.
+literal dense restatement of slam.cpp through numpy's OpenBLAS dgemm on the host cores, rank 0 at
+N=1 only; the C oracle's literal and O(n²) legs beside it) and pose parity of the first timed
+messages against the fp64 oracle.
 """
 from __future__ import annotations
 
@@ -43,7 +51,7 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
@@ -52,13 +60,13 @@ def parse():
                    choices=sorted(WORKLOADS) + ["frontend", "rosbag_surrogate"],
                    help="frontend: the landmark front-end (include/landmarks.h), scans/s; "
                         "rosbag_surrogate: configs[4]'s shape, scans → detect → slam node")
-    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    p.add_argument("--cpu-messages", type=int, default=3,
-                   help="messages in the CPU baseline sample (literal dense)")
+    p.add_argument("--seed", type=int, default=20240317,
+                   help="filter g (global index over ranks) uses seed + g (SURVEY.md §8d)")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and parity legs")
     p.add_argument("--parity-messages", type=int, default=10)
     p.add_argument("--traffic", choices=["auto", "off"], default="auto",
                    help="auto: measure the Σ pass's HBM bytes with two rocprofv3 --pmc child runs")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def _pmc_pass(args, counters):
@@ -133,31 +141,6 @@ def pmc_traffic(args):
                             "note": "SQ_VALU_MFMA_BUSY_CYCLES summed over the SIMDs, per "
                                     "k_sigma_pass dispatch; one --pmc pass, same child run shape"}
     return out, None
-
-
-def build_inputs(N, F, msgs, seed, m):
-    from pyekf import synth
-    import pyekf
-    # Monte-Carlo swarm: up to 8 distinct seeded runs, tiled over the filters (generation cost)
-    uniq = [synth.synthetic(N, msgs, seed=seed + f, max_markers=m) if N != 50 else
-            synth.basic_world(msgs, seed=seed + f) for f in range(min(F, 8))]
-    scs = [uniq[f % len(uniq)] for f in range(F)]
-    odo = [pyekf.odometry(s) for s in uniq]
-    M = max(s.ids.shape[1] for s in scs)
-    T = msgs
-    counts = np.zeros((T, F), np.int32)
-    ids = np.full((T, F, M), -1, np.int32)
-    act = np.zeros((T, F, M), np.int32)
-    rel = np.zeros((T, F, M, 2))
-    odom = np.zeros((T, F, 3))
-    for f, s in enumerate(scs):
-        k = s.ids.shape[1]
-        counts[:, f] = s.count
-        ids[:, f, :k] = s.ids
-        act[:, f, :k] = s.actions
-        rel[:, f, :k] = s.rel
-        odom[:, f] = odo[f % len(uniq)]
-    return scs, counts, ids, act, rel, odom
 
 
 def frontend_main(args):
@@ -308,44 +291,114 @@ def rosbag_main(args):
     print(json.dumps(result))
 
 
-def main():
-    args = parse()
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` outside a launcher: start N ranks (one process per GPU) with
+    torch.distributed.run as a CHILD process — this process never touches the GPU — relay
+    rank 0's output and exit with the launcher's status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__), *argv]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+class HipBackend:
+    """The product: libekfslam.so's HIP path on this rank's GPU, RCCL for the final gather."""
+    dist_backend = "nccl"
+    device = "cuda"
+
+    def __init__(self, local):
+        import torch
+        import pyekf
+        self.torch = torch
+        self.EKF = pyekf.EKF
+        self.F32, self.F64 = pyekf.EKF_F32, pyekf.EKF_F64
+        self.local = local
+        torch.cuda.set_device(local)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+
+def build_inputs(N, F, T, seed, m, rank):
+    """SURVEY.md §8d inputs for this rank's F filters: global filter g = rank·F + f is seeded
+    seed + g (its own map, slip and sensor noise); the survey warm-up (every landmark sighted)
+    precedes T messages of the circle drive. N = 50 is configs[0]'s basic_world (4 landmarks,
+    every one in view, no survey needed)."""
+    from pyekf import synth
+    import pyekf
+    if N == 50:
+        scs = [synth.basic_world(T, seed=seed + rank * F + f) for f in range(F)]
+        M = max(s.ids.shape[1] for s in scs)
+        counts = np.stack([s.count for s in scs], 1)
+        ids = np.full((T, F, M), -1, np.int32)
+        act = np.zeros((T, F, M), np.int32)
+        rel = np.zeros((T, F, M, 2))
+        for f, s in enumerate(scs):
+            ids[:, f], act[:, f], rel[:, f] = s.ids, s.actions, s.rel
+        odo = pyekf.odometry(scs[0])
+        return 0, counts, ids, act, rel, np.repeat(odo[:, None], F, 1), 4
+    sw = synth.swarm(N, F, T, seed=seed + rank * F, max_markers=m)
+    odo = pyekf.odometry(sw.scenario(0))  # encoders report the commanded drive: every filter's
+    return sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel, np.repeat(odo[:, None], F, 1), N
+
+
+def main(argv=None, backend=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
     if args.workload == "frontend":
         return frontend_main(args)
     if args.workload == "rosbag_surrogate":
         return rosbag_main(args)
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0 and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    world = max(world, 1)
+    if args.gpus not in (1, world) and backend is None:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    return run(args, rank, world, local, backend)[0]
+
+
+def run(args, rank, world, local, backend=None):
+    """One rank: its own filters (weak scaling, no collective on the data path), the timed K
+    messages between barriers, the slowest rank's time (MAX), corrections of all ranks (SUM), one
+    all_gather of the final poses (the path's only collective)."""
+    N, dt, F, m, cfgname = WORKLOADS[args.workload]
     traffic, traffic_err = None, "not measured (--traffic off or N>1)"
-    N_, dt_ = WORKLOADS[args.workload][:2]
-    resident = dt_ == "f64" and 3 + 2 * N_ <= 128 and os.environ.get("EKF_RESIDENT") != "0"
+    resident = dt == "f64" and 3 + 2 * N <= 128 and os.environ.get("EKF_RESIDENT") != "0"
     if resident:
         traffic_err = "resident path: Σ crosses HBM once per launch (no Σ pass to count)"
-    if args.traffic == "auto" and world == 1 and not resident:
-        traffic, traffic_err = pmc_traffic(args)
-    import torch
+    if args.traffic == "auto" and world == 1 and not resident and backend is None:
+        traffic, traffic_err = pmc_traffic(args)  # child runs, before this process uses the GPU
     import torch.distributed as dist
+    be = backend if backend is not None else HipBackend(local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    import pyekf
-
-    N, dt, F, m, cfgname = WORKLOADS[args.workload]
-    dtype = pyekf.EKF_F32 if dt == "f32" else pyekf.EKF_F64
+        dist.init_process_group(be.dist_backend)
+    dtype = be.F32 if dt == "f32" else be.F64
     W, K = args.warmup, args.steps
-    # fp32 cannot take first sightings against the 1e7 prior: an fp64 lap initialises the map
-    warm_lap = 63 if dt == "f32" else 0
-    seed = 20240317 + 1000 * rank
-    T = warm_lap + W + 2 * K
-    scs, counts, ids, act, rel, odom = build_inputs(N, F, T, seed, m)
+    t_gen = time.perf_counter()
+    n_warm, counts, ids, act, rel, odom, n_init_target = build_inputs(
+        N, F, W + 2 * K, args.seed, m, rank)
+    t_gen = time.perf_counter() - t_gen
 
-    ekf = pyekf.EKF(n_landmarks=N, n_filters=F, dtype=dtype, device=local)
+    def msgs(a, b, e=None):
+        sl = slice(a, b)
+        (e or ekf).replay(counts[sl], rel[sl], odom[sl], ids=ids[sl], actions=act[sl])
+
+    ekf = be.EKF(n_landmarks=N, n_filters=F, dtype=dtype, device=local)
+    # ---- untimed warm-up: the survey (every landmark initialised), then W messages ----
+    # fp32 cannot take first sightings against the 1e7 prior (slam.cpp:130): the survey runs on an
+    # fp64 handle whose state seeds the fp32 one
     warm_state = None
-    if warm_lap:
-        e64 = pyekf.EKF(n_landmarks=N, n_filters=F, device=local)
-        e64.replay(counts[:warm_lap], rel[:warm_lap], odom[:warm_lap], ids=ids[:warm_lap],
-                   actions=act[:warm_lap])
+    if dtype == be.F32 and n_warm:
+        e64 = be.EKF(n_landmarks=N, n_filters=F, device=local)
+        msgs(0, n_warm, e64)
         warm_state = []
         for f in range(F):
             x, S, cnt = e64.state(f)
@@ -353,46 +406,50 @@ def main():
             ekf.set_state(x, S, tmo=tmo, counter=cnt, f=f)
             warm_state.append((x, S, tmo, cnt))
         e64.close()
-    sl = slice(warm_lap, warm_lap + W)
+    elif n_warm:
+        msgs(0, n_warm)
     if W:
-        ekf.replay(counts[sl], rel[sl], odom[sl], ids=ids[sl], actions=act[sl])
+        msgs(n_warm, n_warm + W)
     ekf.sync()
-    if rank == 0 and warm_state is None:
-        x, S, cnt = ekf.state(0)
-        warm_state = [(x, S, ekf.map_odom(0), cnt)]
+    # landmarks initialised (state slot ≠ (0, 0), slam.cpp:213) in every filter of this rank
+    n_init = min(int(np.count_nonzero(np.any(ekf.state(f, sigma=False)[0][3:].reshape(-1, 2)
+                                             != 0.0, 1))) for f in range(F))
+    status = [ekf.status(f) for f in range(F)]
+    x0, S0, c0 = ekf.state(0)
+    ws0 = (x0, S0, ekf.map_odom(0), c0)
 
     # ---- timed region: exactly K messages ----
-    t0s = warm_lap + W
-    ts = slice(t0s, t0s + K)
+    t0s = n_warm + W
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    be.sync()
     t0 = time.perf_counter()
-    ekf.replay(counts[ts], rel[ts], odom[ts], ids=ids[ts], actions=act[ts])
+    msgs(t0s, t0s + K)
     ekf.sync()
-    torch.cuda.synchronize()
+    be.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    corrections = int(np.count_nonzero((act[ts] == 0) & (np.arange(act.shape[2]) <
-                                                          counts[ts][..., None])))
+    live = np.arange(act.shape[2]) < counts[t0s:t0s + K][..., None]
+    corrections = int(np.count_nonzero(live & (act[t0s:t0s + K] != 2)))  # slam.cpp:205
     poses = np.stack([ekf.pose(f) for f in range(F)])
+    status = [s | ekf.status(f) for f, s in enumerate(status)]
     if world > 1:
-        elapsed, total_corr, _ = reduce_ranks(elapsed, corrections, poses, "cuda")
+        elapsed, total_corr, all_poses = reduce_ranks(elapsed, corrections, poses, be.device)
     else:
-        total_corr = float(corrections)
+        total_corr, all_poses = float(corrections), poses
 
     # ---- roofline pass: same work, Σ-pass launches bracketed by HIP events ----
     ps = slice(t0s + K, t0s + 2 * K)
     ekf.profile(True)
-    ekf.replay(counts[ps], rel[ps], odom[ps], ids=ids[ps], actions=act[ps])
+    msgs(ps.start, ps.stop)
     n_sig, ms_sig = ekf.profile_read(0)
     n_gain, ms_gain = ekf.profile_read(1)
     n_fac, ms_fac = ekf.profile_read(3)
     n_res, ms_res = ekf.profile_read(4)
     ekf.profile(False)
-    res_corr = int(np.count_nonzero((act[ps] == 0) & (np.arange(act.shape[2]) <
-                                                      counts[ps][..., None])))
+    live = np.arange(act.shape[2]) < counts[ps][..., None]
+    res_corr = int(np.count_nonzero(live & (act[ps] != 2)))
     bytes_per_launch = ekf.sigma_pass_bytes()
     avg_sig_s = ms_sig / max(n_sig, 1) / 1e3
     achieved = bytes_per_launch / avg_sig_s / 1e9 if n_sig else 0.0
@@ -420,10 +477,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32" if dt == "f32" else "f64",
-            "data": "synthetic (seeded map + circle drive + nusim-style fake sensor)",
+            "data": "synthetic (seeded map per filter, survey warm-up sighting every landmark, "
+                    "then the circle drive with a nusim-style fake sensor)",
             "config": {"workload": args.workload, "baseline_config": cfgname,
                        "n_landmarks": N, "state_dim": n, "filters_per_gpu": F,
-                       "markers_per_message": m, "association": "known",
+                       "filters_total": F * world, "markers_per_message": m,
+                       "association": "known", "seeds": f"{args.seed} + global filter index",
+                       "survey_messages": n_warm,
+                       "landmarks_initialised_min": n_init,
+                       "landmarks_initialised_target": n_init_target,
+                       "status_flags_rank0": sorted(set(status)),
+                       "host_input_generation_s": t_gen,
                        "parallelism": f"independent filters x{world} ranks"},
             "roofline": {
                 "kernel": "k_sigma_pass", "bound": "hbm", "achieved": achieved,
@@ -443,6 +507,9 @@ def main():
                 "factor_kernel_avg_us": ms_fac / max(n_fac, 1) * 1e3,
             },
         }
+        if world > 1:
+            result["gathered_poses"] = {"filters": int(all_poses.shape[0]),
+                                        "all_finite": bool(np.all(np.isfinite(all_poses)))}
         if n_res:
             # resident path (ekf_resident.hip): one launch runs the whole replay, Σ in registers;
             # its bound is the sequential f64 chain of one CU per filter, priced against that
@@ -462,19 +529,21 @@ def main():
                 "kernel_corrections_per_s": res_corr / sec,
             }
             result["config"]["device_path"] = "resident"
-    # ---- CPU baseline + parity (rank 0, N=1 only) ----
-    if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(args, N, warm_state[0], counts, ids, act, rel, odom,
-                                              t0s)
-        result["parity"] = parity(args, N, ekf_first_poses(args, N, dtype, warm_state[0], counts,
-                                                           ids, act, rel, odom, t0s, local),
-                                  warm_state[0], counts, ids, act, rel, odom, t0s)
+    # ---- parity (rank 0) and the CPU baseline (rank 0, N=1 only) ----
+    ws = warm_state[0] if warm_state else ws0
+    if rank == 0 and not args.no_cpu:
+        result["parity"] = parity(args, N, ekf_first_poses(args, be, N, dtype, ws, counts, ids,
+                                                           act, rel, odom, t0s, local),
+                                  ws, counts, ids, act, rel, odom, t0s)
+        if world == 1:
+            result["cpu_baseline"] = cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s)
     if rank == 0:
-        print(json.dumps(result))
+        print(json.dumps(result), flush=True)
     ekf.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return result, all_poses
 
 
 def reduce_ranks(elapsed, corrections, poses, device):
@@ -493,12 +562,11 @@ def reduce_ranks(elapsed, corrections, poses, device):
     return float(t.item()), float(c.item()), np.concatenate([g.cpu().numpy() for g in gathered])
 
 
-def ekf_first_poses(args, N, dtype, ws, counts, ids, act, rel, odom, t0s, device):
-    """Posterior poses of the first timed messages from the same warm state (HIP path)."""
-    import pyekf
+def ekf_first_poses(args, be, N, dtype, ws, counts, ids, act, rel, odom, t0s, device):
+    """Posterior poses of the first timed messages of filter 0 from the same warm state."""
     k = args.parity_messages
     x, S, tmo, cnt = ws
-    e = pyekf.EKF(n_landmarks=N, dtype=dtype, device=device)
+    e = be.EKF(n_landmarks=N, dtype=dtype, device=device)
     e.set_state(x, S, tmo=tmo, counter=cnt)
     sl = slice(t0s, t0s + k)
     p = e.replay(counts[sl, :1], rel[sl, :1], odom[sl, :1], ids=ids[sl, :1], actions=act[sl, :1],
@@ -514,40 +582,70 @@ def _oracle():
     return orc
 
 
+def _blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max((p.get("num_threads", 1) for p in threadpool_info()
+                    if p.get("user_api") == "blas"), default=1)
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
-    """The oracle's literal dense restatement of slam.cpp (O(n³) per correction, the reference's
-    own algorithm) on the host cores, over a bounded sample of the same messages."""
+    """The reference's own algorithm on the host cores, over a bounded sample of the same
+    messages from the same warm state:
+      value       literal dense slam.cpp (At·Σ·Atᵀ, (I−KH)·Σ: O(n³) per correction) through numpy's
+                  OpenBLAS dgemm (oracle/ekf_numpy.py) — the reference's Armadillo→BLAS path;
+      c_literal   the same dense algebra in the C oracle (a blocked OpenMP GEMM, no BLAS);
+      structured  the O(n²) rank-2 restatement (the GPU's algorithm) in the C oracle."""
     orc = _oracle()
+    import ekf_numpy  # noqa: E402  (cpu_baseline leg only)
     x, S, tmo, cnt = ws
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    out = {}
     avail = counts.shape[0] - t0s
-    for literal, k in ((True, args.cpu_messages), (False, args.steps)):
+
+    def timed(step, k_min, budget):
+        ncorr, nmsg = 0, 0
+        t0 = time.perf_counter()
+        for t in range(t0s, t0s + avail):
+            if nmsg >= k_min and time.perf_counter() - t0 >= budget:
+                break
+            c = int(counts[t, 0])
+            step(t, c)
+            ncorr += int(np.count_nonzero(act[t, 0, :c] != 2))
+            nmsg += 1
+        return ncorr, nmsg, time.perf_counter() - t0
+
+    # numpy / OpenBLAS literal (the DenseEKF members of slam.cpp:657-676 set to the warm state)
+    d = ekf_numpy.DenseEKF(n_landmarks=N)
+    d.state, d.sigma, d.counter = x.copy(), S.copy(), int(cnt)
+    d.t_map_odom, d.prev = tuple(tmo), tuple(x[:3])
+
+    def np_step(t, c):
+        d.t_odom_robot = tuple(odom[t, 0])
+        d.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
+    nb, kb, tb = timed(np_step, 1, 10.0)
+    out = {}
+    for literal, k_min, budget in ((True, 1, 10.0), (False, args.steps, 0.0)):
         ref = orc.OracleEKF(n_landmarks=N, literal=literal)
         ref.set(x, S, tmo, x[:3], cnt)
-        ncorr = 0
-        t0 = time.perf_counter()
-        # at least k messages; the literal leg keeps going (over the same drive) until ~10 s of
-        # CPU work, so a small map's sample is not a few milliseconds
-        nmsg = 0
-        for t in range(t0s, t0s + (avail if literal else min(k, avail))):
-            if nmsg >= k and (not literal or time.perf_counter() - t0 >= 10.0):
-                break
+
+        def c_step(t, c, ref=ref):
             ref.set_odom(odom[t, 0])
-            c = int(counts[t, 0])
             ref.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
-            ncorr += int(np.count_nonzero(act[t, 0, :c] == 0))
-            nmsg += 1
-        k = nmsg
-        dt = time.perf_counter() - t0
-        out["literal" if literal else "structured"] = (ncorr / dt, ncorr, k, dt)
-    v, ncorr, k, dt = out["literal"]
-    sv, sncorr, sk, sdt = out["structured"]
-    return {"value": v, "unit": "corrections/s", "cores": cores, "kind": "port",
-            "sample": f"literal dense O(n^3) restatement of slam.cpp (fp64, OpenMP GEMM), "
-                      f"{k} message(s) = {ncorr} corrections in {dt:.2f} s",
-            "structured": {"value": sv, "sample": f"O(n^2) rank-2 restatement, {sk} messages = "
-                                                  f"{sncorr} corrections in {sdt:.2f} s"}}
+        out[literal] = timed(c_step, k_min, budget)
+    lc, lk, lt = out[True]
+    sc_, sk, st = out[False]
+    return {"value": nb / tb, "unit": "corrections/s", "cores": _blas_threads() or cores,
+            "kind": "port",
+            "sample": f"literal dense restatement of slam.cpp (numpy + OpenBLAS dgemm, fp64, "
+                      f"oracle/ekf_numpy.py): {kb} message(s) = {nb} corrections in {tb:.2f} s",
+            "c_literal": {"value": lc / lt, "cores": cores,
+                          "sample": f"C oracle, dense O(n^3) with a blocked OpenMP GEMM: {lk} "
+                                    f"message(s) = {lc} corrections in {lt:.2f} s"},
+            "structured": {"value": sc_ / st, "cores": cores,
+                           "sample": f"C oracle, O(n^2) rank-2 restatement: {sk} messages = "
+                                     f"{sc_} corrections in {st:.2f} s"}}
 
 
 def parity(args, N, gpu_poses, ws, counts, ids, act, rel, odom, t0s):
@@ -566,7 +664,7 @@ def parity(args, N, gpu_poses, ws, counts, ids, act, rel, odom, t0s):
     dth = np.arctan2(np.sin(d[:, 0]), np.cos(d[:, 0]))
     return {"pose_rmse_m": float(np.sqrt(np.mean(d[:, 1] ** 2 + d[:, 2] ** 2))),
             "heading_rmse_rad": float(np.sqrt(np.mean(dth ** 2))),
-            "messages": k, "vs": "oracle structured fp64 (CPU), same warm state"}
+            "messages": k, "vs": "oracle structured fp64 (CPU), filter 0, same warm state"}
 
 
 if __name__ == "__main__":

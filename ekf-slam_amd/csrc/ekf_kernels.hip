@@ -218,6 +218,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   const int tid = threadIdx.x;
   const int ld = A.ld;
   FilterCtl* ctl = A.ctl + f;
+  // LDS starts as whatever the CU's previous kernel left (possibly NaN bit patterns): zero it once,
+  // so padding rows / columns that feed MFMA or dot products as zeros really are zeros
+  for (int e = tid; e < static_cast<int>(sizeof(ChainShared) / 8); e += blockDim.x)
+    reinterpret_cast<double*>(&sh)[e] = 0.0;
   bool have_carry = false;
   bool pre = false;        // sdesc[ci & 1] was prefetched by the previous chunk's epilogue
   unsigned pending = 0;    // chain epoch of the previous chunk, not yet published (its record
@@ -259,7 +263,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
   if (carry && d.nnew > 0) {  // the previous chunk's Z', Y' rebuild the rows of new indices
     for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.pv.Z[0][0])[e] = (&sh.Z[0][0])[e];
-    for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x) (&sh.pv.Y[0][0])[e] = (&sh.Y[0][0])[e];
+    // Y's padding column kMaxU is never written by wave 2: zero it here (the rebuild multiplies it
+    // by C's zero row, and LDS garbage there can be a NaN: NaN·0 = NaN)
+    for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x)
+      (&sh.pv.Y[0][0])[e] = e % (kMaxU + 1) == kMaxU ? 0.0 : (&sh.Y[0][0])[e];
     if (tid < kZC) sh.pv.Z[kMaxU][tid] = 0.0;
   }
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)

@@ -4,31 +4,44 @@ This is input generation, not filter math: it plays the role of ``nusim``
 (nusim/src/nusim.cpp:211-289 wheel integration with slip, :310-349 fake landmark sensor) so the
 same odometry + marker streams can be fed to the HIP path, the CPU oracle and the benchmark.
 
-* Robot drives a circle (nuturtle_control/src/circle.cpp:85-86: v = ω·r) sampled at ``tick_hz``
-  joint-state ticks; the sensor fires every ``ticks_per_msg`` ticks (5 Hz at 200 Hz ticks,
-  nusim.cpp:72,89).
+* The robot follows a commanded (v, ω) schedule sampled at ``tick_hz`` joint-state ticks; the
+  sensor fires every ``ticks_per_msg`` ticks (5 Hz at 200 Hz ticks, nusim.cpp:72,89). The basic
+  drive is a circle (nuturtle_control/src/circle.cpp:85-86: v = ω·r).
 * True wheel angles carry multiplicative slip noise U(-slip, slip) (nusim.cpp:224-227); the encoders
   report the commanded angles, so odometry drifts from the truth and the EKF has work to do.
 * Each message carries landmark positions in the true body frame plus N(0, σ²) noise on x and y
   (nusim.cpp:317-346). ``basic_world`` reports every landmark with DELETE beyond ``max_range``
   (nusim.cpp:332-336); the large synthetic maps report the ``m`` nearest landmarks.
+* Populated maps ("one untimed warm-up pass that initializes every landmark"):
+  ``populated`` / ``swarm`` prefix the circle with a survey drive — an outward spiral with rings
+  ``ring`` m apart over the whole field — whose messages carry, of the landmarks within
+  ``max_range``, the not-yet-sighted ones first, then the nearest. Every landmark is sighted by the
+  end of the survey (asserted). Landmarks are placed at least ``clearance`` m from the true path of
+  the whole drive (range 0 is the reference's unguarded NaN, slam.cpp:241-249).
 
-Seeds are explicit; every array is deterministic for a given argument set.
+Randomness is counter-based (splitmix64 of (seed, stream, index)): every draw of filter f with seed
+``base + f`` is a pure function of its indices, so a whole swarm is generated array-at-a-time and
+any filter can be regenerated alone (``Swarm.scenario(f)`` equals ``populated(..., seed=base+f)``).
 """
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
-ADD, DELETE = 0, 2  # visualization_msgs Marker actions
+ADD, MODIFY, DELETE, DELETEALL = 0, 1, 2, 3  # visualization_msgs Marker actions
 
 # basic_world.yaml:5-10 and diff_params.yaml:3-4 of the reference
 BASIC_WORLD_LANDMARKS = np.array([[-0.5, -0.7], [0.8, -0.8], [0.4, 0.8], [-0.6, 0.65]])
 BASIC_WORLD_THETA0 = 1.28
 WHEEL_RADIUS = 0.033
 TRACK_WIDTH = 0.160
+
+# sensor modes per message
+SENSE_NEAREST, SENSE_SURVEY, SENSE_ALL = 0, 1, 2
+# RNG streams
+_S_SLIP, _S_NOISE, _S_MAP, _S_SHUFFLE, _S_DELETE = 1, 2, 3, 4, 5
 
 
 @dataclass
@@ -37,12 +50,13 @@ class Scenario:
     landmarks: np.ndarray     # [L, 2] true landmark positions, L <= N
     wheel: np.ndarray         # [T, ticks, 2] encoder wheel angles (left, right), cumulative rad
     ids: np.ndarray           # [T, M] int32 landmark ids (-1 = padding)
-    actions: np.ndarray       # [T, M] int32 ADD / DELETE
+    actions: np.ndarray       # [T, M] int32 ADD / DELETE (MODIFY / DELETEALL: corrected too)
     rel: np.ndarray           # [T, M, 2] body-frame marker positions (noisy)
     count: np.ndarray         # [T] markers per message
     truth: np.ndarray         # [T, 3] true (θ, x, y) at each sensor message
     track: float = TRACK_WIDTH
     radius: float = WHEEL_RADIUS
+    n_warm: int = 0           # leading survey messages (every landmark sighted by their end)
 
     @property
     def n_messages(self) -> int:
@@ -59,16 +73,270 @@ class Scenario:
         return c
 
 
-def _se2_step(pose, omega, vx):
-    """Exact arc integration of a body twist (same kinematics as turtlelib integrate_twist)."""
-    th, x, y = pose
-    if omega == 0.0:
-        dx, dy = vx, 0.0
+# ---- counter-based RNG ---------------------------------------------------------------------------
+_G = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(z):
+    """splitmix64's output function (uint64 arrays, wrapping arithmetic)."""
+    z = np.asarray(z, dtype=np.uint64)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def rng_u64(seed, stream: int, idx):
+    """64 random bits for draw ``idx`` of ``stream`` under ``seed`` (broadcasting arrays)."""
+    with np.errstate(over="ignore"):
+        key = _mix64(np.asarray(seed, dtype=np.uint64) * _G + np.uint64(stream))
+        return _mix64(key + (np.asarray(idx, dtype=np.uint64) + np.uint64(1)) * _G)
+
+
+def rng_uniform(seed, stream: int, idx):
+    """U[0, 1) with 53 random bits."""
+    return (rng_u64(seed, stream, idx) >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+
+
+def rng_normal(seed, stream: int, idx):
+    """N(0, 1) by Box–Muller from draws 2·idx, 2·idx + 1 of the stream."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    u1 = 1.0 - rng_uniform(seed, stream, idx * np.uint64(2))  # (0, 1]
+    u2 = rng_uniform(seed, stream, idx * np.uint64(2) + np.uint64(1))
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * math.pi * u2)
+
+
+# ---- commanded drives ----------------------------------------------------------------------------
+@dataclass
+class Drive:
+    """Per-tick commanded body twist and per-message sensor mode."""
+    v: np.ndarray              # [ticks_total] forward speed, m/s
+    w: np.ndarray              # [ticks_total] yaw rate, rad/s
+    sense: np.ndarray          # [T] SENSE_* per message
+    ticks_per_msg: int
+    tick_hz: float
+    n_warm: int = 0
+
+
+def circle_drive(n_messages: int, circle_radius=1.0, omega=0.5, tick_hz=200.0, ticks_per_msg=40,
+                 sense=SENSE_NEAREST) -> Drive:
+    nt = n_messages * ticks_per_msg
+    return Drive(np.full(nt, omega * circle_radius), np.full(nt, omega),
+                 np.full(n_messages, sense, np.int32), ticks_per_msg, tick_hz)
+
+
+def survey_drive(half: float, n_messages: int, ring=4.0, v_survey=4.0, circle_radius=1.0,
+                 omega=0.5, tick_hz=200.0, ticks_per_msg=40) -> Drive:
+    """Outward spiral from the unit circle (radius growing ``ring`` m per turn, curvature 1/r, at
+    ``v_survey`` m/s) until it covers the [-half, half]² field, then ``n_messages`` of the circle
+    (radius ``circle_radius`` at ``omega``). The spiral's messages sense in survey mode."""
+    dt = 1.0 / tick_hz
+    r, v, w = circle_radius, [], []
+    r_max = max(half * math.sqrt(2.0), circle_radius + ring)
+    while r < r_max:
+        om = v_survey / r
+        v.append(v_survey)
+        w.append(om)
+        r += ring / (2.0 * math.pi) * om * dt
+    nw = -(-len(v) // ticks_per_msg)  # whole messages
+    pad = nw * ticks_per_msg - len(v)
+    v += [v_survey] * pad
+    w += [v_survey / r] * pad
+    c = circle_drive(n_messages, circle_radius, omega, tick_hz, ticks_per_msg)
+    sense = np.concatenate([np.full(nw, SENSE_SURVEY, np.int32), c.sense])
+    return Drive(np.concatenate([np.array(v), c.v]), np.concatenate([np.array(w), c.w]), sense,
+                 ticks_per_msg, tick_hz, nw)
+
+
+# ---- simulation ----------------------------------------------------------------------------------
+def _se2_step(th, x, y, omega, vx):
+    """Exact arc integration of a body twist (the kinematics of turtlelib integrate_twist),
+    vectorised over filters."""
+    small = omega == 0.0
+    om = np.where(small, 1.0, omega)
+    dx = np.where(small, vx, vx / om * np.sin(omega))
+    dy = np.where(small, 0.0, vx / om * (1.0 - np.cos(omega)))
+    c, s = np.cos(th), np.sin(th)
+    return th + omega, x + c * dx - s * dy, y + s * dx + c * dy
+
+
+def _simulate(drive: Drive, seeds: np.ndarray, start_pose, slip: float):
+    """True poses of F filters (slip per filter) → (wheel [T, ticks, 2] encoder angles shared by
+    all filters, truth [F, T, 3] at the messages, path [F, ticks_total, 2] positions)."""
+    F = seeds.shape[0]
+    nt = drive.v.shape[0]
+    tpm = drive.ticks_per_msg
+    T = nt // tpm
+    dt = 1.0 / drive.tick_hz
+    wr = (drive.v + drive.w * TRACK_WIDTH / 2.0) / WHEEL_RADIUS * dt
+    wl = (drive.v - drive.w * TRACK_WIDTH / 2.0) / WHEEL_RADIUS * dt
+    cmd = np.stack([wl, wr], 1)                                         # [nt, 2]
+    wheel = np.cumsum(cmd, 0).reshape(T, tpm, 2)
+    k = np.arange(nt, dtype=np.uint64)
+    u = rng_uniform(seeds[:, None, None], _S_SLIP,
+                    (k[None, :, None] * np.uint64(2) + np.arange(2, dtype=np.uint64)))
+    slipped = cmd[None] * (1.0 + slip * (2.0 * u - 1.0))                # [F, nt, 2]
+    om_all = WHEEL_RADIUS / TRACK_WIDTH * (-slipped[..., 0] + slipped[..., 1])
+    vx_all = WHEEL_RADIUS / 2.0 * (slipped[..., 0] + slipped[..., 1])
+    th = np.full(F, float(start_pose[0]))
+    x = np.full(F, float(start_pose[1]))
+    y = np.full(F, float(start_pose[2]))
+    path = np.zeros((F, nt, 2))
+    truth = np.zeros((F, T, 3))
+    for i in range(nt):
+        th, x, y = _se2_step(th, x, y, om_all[:, i], vx_all[:, i])
+        path[:, i, 0] = x
+        path[:, i, 1] = y
+        if (i + 1) % tpm == 0:
+            t = (i + 1) // tpm - 1
+            truth[:, t, 0], truth[:, t, 1], truth[:, t, 2] = th, x, y
+    return wheel, truth, path
+
+
+def _place_landmarks(n: int, half: float, seeds: np.ndarray, path: np.ndarray, clearance: float):
+    """n landmarks per filter, uniform in [-half, half]², at least ``clearance`` m from that
+    filter's true path (rejection by nearest-neighbour distance to the path's tick positions,
+    ≤ 2 cm apart, with that spacing added to the clearance)."""
+    from scipy.spatial import cKDTree
+    F = seeds.shape[0]
+    out = np.zeros((F, n, 2))
+    for f in range(F):
+        tree = cKDTree(path[f])
+        k, draw = 0, 0
+        while k < n:
+            m = 2 * n
+            idx = np.arange(draw, draw + m, dtype=np.uint64)
+            p = (2.0 * rng_uniform(seeds[f], _S_MAP, idx[:, None] * np.uint64(2) +
+                                   np.arange(2, dtype=np.uint64)) - 1.0) * half
+            draw += m
+            d, _ = tree.query(p, k=1, distance_upper_bound=clearance + 0.02)
+            p = p[~np.isfinite(d)]
+            take = min(n - k, len(p))
+            out[f, k:k + take] = p[:take]
+            k += take
+    return out
+
+
+def _sense(drive: Drive, seeds, landmarks, truth, max_markers, max_range, sensor_sigma, shuffle,
+           n_delete, n_landmarks):
+    """Fake-sensor marker arrays for F filters → ids/actions [T, F, M], rel [T, F, M, 2], count."""
+    F, T = truth.shape[0], truth.shape[1]
+    L = landmarks.shape[1]
+    mall = int(np.any(drive.sense == SENSE_ALL))
+    m = min(max_markers, L)
+    M = (L if mall else m) + n_delete
+    ids = np.full((T, F, M), -1, np.int32)
+    act = np.zeros((T, F, M), np.int32)
+    rel = np.zeros((T, F, M, 2))
+    cnt = np.zeros((T, F), np.int32)
+    sighted = np.zeros((F, L), bool)
+    warm_sighted = sighted.copy()
+    ar = np.arange(L)
+    for t in range(T):
+        if t == drive.n_warm:
+            warm_sighted = sighted.copy()
+        th, x, y = truth[:, t, 0:1], truth[:, t, 1:2], truth[:, t, 2:3]
+        c, s = np.cos(th), np.sin(th)
+        dxl = landmarks[..., 0] - x
+        dyl = landmarks[..., 1] - y
+        bx = c * dxl + s * dyl            # body frame: R(θ)ᵀ (p − x)
+        by = -s * dxl + c * dyl
+        dist = np.hypot(bx, by)           # [F, L]
+        mode = drive.sense[t]
+        if mode == SENSE_ALL:
+            sel = np.broadcast_to(ar, (F, L))
+            k = np.full(F, L)
+            a = np.where(dist <= max_range, ADD, DELETE)
+        else:
+            key = np.where(dist <= max_range, dist, np.inf)
+            if mode == SENSE_SURVEY:
+                key = np.where(sighted & np.isfinite(key), key + 1e6, key)
+            sel = np.argsort(key, axis=1, kind="stable")[:, :m]
+            k = np.count_nonzero(np.isfinite(np.take_along_axis(key, sel, 1)), axis=1)
+            a = np.full((F, L), ADD)
+        W = sel.shape[1]
+        valid = np.arange(W)[None, :] < k[:, None]
+        if shuffle:  # a random order of the valid markers (invalid ones stay behind them)
+            keys = rng_u64(seeds[:, None], _S_SHUFFLE, np.uint64(t) * np.uint64(M) +
+                           np.arange(W, dtype=np.uint64))
+            keys = np.where(valid, keys >> np.uint64(1), np.uint64(2 ** 63) + np.arange(W, dtype=np.uint64))
+            sel = np.take_along_axis(sel, np.argsort(keys, axis=1, kind="stable"), 1)
+        rows = np.arange(F)[:, None]
+        ids[t, :, :W] = np.where(valid, sel, -1)
+        act[t, :, :W] = np.where(valid, a[rows, sel], 0)
+        rel[t, :, :W, 0] = np.where(valid, bx[rows, sel], 0.0)
+        rel[t, :, :W, 1] = np.where(valid, by[rows, sel], 0.0)
+        cnt[t] = k
+        sighted[np.broadcast_to(rows, sel.shape)[valid], sel[valid]] = True
+        if n_delete:
+            j = np.arange(n_delete, dtype=np.uint64)
+            far = (rng_u64(seeds[:, None], _S_DELETE, np.uint64(t) * np.uint64(n_delete) + j)
+                   % np.uint64(n_landmarks)).astype(np.int32)
+            for f in range(F):
+                kf = int(cnt[t, f])
+                ids[t, f, kf:kf + n_delete] = far[f]
+                rel[t, f, kf:kf + n_delete] = 100.0
+                act[t, f, kf:kf + n_delete] = DELETE
+                cnt[t, f] = kf + n_delete
+    # N(0, σ²) on every reported x, y (nusim.cpp:339-340; DELETE padding markers stay at 100 m)
+    idx = (np.arange(T, dtype=np.uint64)[:, None, None] * np.uint64(M) +
+           np.arange(M, dtype=np.uint64)[None, None, :]) * np.uint64(2)
+    noise = sensor_sigma * np.stack([
+        rng_normal(seeds[None, :, None], _S_NOISE, idx),
+        rng_normal(seeds[None, :, None], _S_NOISE, idx + np.uint64(1))], -1)
+    live = (np.arange(M)[None, None, :] < cnt[..., None]) & (rel[..., 0] != 100.0)
+    rel = np.where(live[..., None], rel + noise, rel)
+    if T == drive.n_warm:
+        warm_sighted = sighted.copy()
+    return ids, act, rel, cnt, warm_sighted
+
+
+@dataclass
+class Swarm:
+    """F independent seeded runs over one commanded drive, arrays indexed [T, F, ...] (the
+    ekf_replay / ekf_batch_sensor layout)."""
+    n_landmarks: int
+    seeds: np.ndarray        # [F] uint64
+    landmarks: np.ndarray    # [F, L, 2]
+    wheel: np.ndarray        # [T, ticks, 2] encoder angles (the commanded drive: every filter's)
+    ids: np.ndarray          # [T, F, M]
+    actions: np.ndarray      # [T, F, M]
+    rel: np.ndarray          # [T, F, M, 2]
+    count: np.ndarray        # [T, F]
+    truth: np.ndarray        # [T, F, 3]
+    n_warm: int = 0
+    sighted: np.ndarray = field(default=None, repr=False)  # [F, L] by the survey's end
+
+    @property
+    def n_filters(self) -> int:
+        return int(self.seeds.shape[0])
+
+    def scenario(self, f: int) -> Scenario:
+        return Scenario(self.n_landmarks, self.landmarks[f], self.wheel, self.ids[:, f],
+                        self.actions[:, f], self.rel[:, f], self.count[:, f], self.truth[:, f],
+                        n_warm=self.n_warm)
+
+    def corrections(self, start: int = 0, stop: int | None = None) -> int:
+        sl = slice(start, stop)
+        live = np.arange(self.ids.shape[2])[None, None, :] < self.count[sl][..., None]
+        return int(np.count_nonzero(live & (self.actions[sl] != DELETE)))
+
+
+def _generate(n_landmarks, drive: Drive, seeds, landmarks=None, half=None, *, max_markers=16,
+              start_pose=(0.0, 0.0, -1.0), sensor_sigma=1e-3, slip=0.02, max_range=5.0,
+              shuffle=False, n_delete=0, clearance=0.3) -> Swarm:
+    seeds = np.asarray(seeds, dtype=np.uint64).reshape(-1)
+    F = seeds.shape[0]
+    wheel, truth, path = _simulate(drive, seeds, start_pose, slip)
+    if landmarks is None:
+        landmarks = _place_landmarks(n_landmarks, half, seeds, path, clearance)
     else:
-        dx = vx / omega * math.sin(omega)
-        dy = vx / omega * (1.0 - math.cos(omega))
-    c, s = math.cos(th), math.sin(th)
-    return (th + omega, x + c * dx - s * dy, y + s * dx + c * dy)
+        landmarks = np.broadcast_to(np.asarray(landmarks, np.float64),
+                                    (F,) + np.shape(landmarks)[-2:]).copy()
+    assert landmarks.shape[1] <= n_landmarks
+    ids, act, rel, cnt, sighted = _sense(drive, seeds, landmarks, truth, max_markers, max_range,
+                                         sensor_sigma, shuffle, n_delete, n_landmarks)
+    return Swarm(n_landmarks, seeds, landmarks, wheel, ids, act, rel, cnt,
+                 np.ascontiguousarray(truth.transpose(1, 0, 2)), drive.n_warm, sighted)
 
 
 def make_scenario(n_landmarks: int, landmarks: np.ndarray, n_messages: int, *,
@@ -77,64 +345,13 @@ def make_scenario(n_landmarks: int, landmarks: np.ndarray, n_messages: int, *,
                   ticks_per_msg: int = 40, sensor_sigma: float = 1e-3, slip: float = 0.02,
                   max_range: float = 5.0, seed: int = 20240317, shuffle: bool = False,
                   n_delete: int = 0) -> Scenario:
-    """Generate a drive + sensing sequence. ``start_pose`` is (θ, x, y)."""
-    rng = np.random.default_rng(seed)
-    L = landmarks.shape[0]
-    assert L <= n_landmarks
-    v = omega * circle_radius
-    wr = (v + omega * TRACK_WIDTH / 2.0) / WHEEL_RADIUS
-    wl = (v - omega * TRACK_WIDTH / 2.0) / WHEEL_RADIUS
-    dt = 1.0 / tick_hz
-    m = L if not nearest else min(max_markers, L)
-    M = m + n_delete
-    wheel = np.zeros((n_messages, ticks_per_msg, 2))
-    ids = np.full((n_messages, M), -1, dtype=np.int32)
-    actions = np.zeros((n_messages, M), dtype=np.int32)
-    rel = np.zeros((n_messages, M, 2))
-    count = np.zeros(n_messages, dtype=np.int32)
-    truth = np.zeros((n_messages, 3))
-    enc = np.zeros(2)
-    true_w = np.zeros(2)
-    pose = tuple(float(p) for p in start_pose)
-    for t in range(n_messages):
-        for k in range(ticks_per_msg):
-            cmd = np.array([wl, wr]) * dt
-            enc = enc + cmd
-            slipped = cmd * (1.0 + rng.uniform(-slip, slip, size=2))
-            true_w = true_w + slipped
-            om = WHEEL_RADIUS / TRACK_WIDTH * (-slipped[0] + slipped[1])
-            vx = WHEEL_RADIUS / 2.0 * (slipped[0] + slipped[1])
-            pose = _se2_step(pose, om, vx)
-            wheel[t, k] = enc
-        truth[t] = pose
-        th, x, y = pose
-        c, s = math.cos(th), math.sin(th)
-        d = landmarks - np.array([x, y])
-        # body frame: R(θ)ᵀ (p − x)
-        bx = c * d[:, 0] + s * d[:, 1]
-        by = -s * d[:, 0] + c * d[:, 1]
-        dist = np.hypot(bx, by)
-        if nearest:
-            sel = np.argsort(dist, kind="stable")[:m]
-            sel = sel[dist[sel] <= max_range]
-        else:
-            sel = np.arange(L)
-        if shuffle:
-            sel = rng.permutation(sel)
-        k = len(sel)
-        noise = rng.normal(0.0, sensor_sigma, size=(k, 2))
-        ids[t, :k] = sel
-        rel[t, :k, 0] = bx[sel] + noise[:, 0]
-        rel[t, :k, 1] = by[sel] + noise[:, 1]
-        actions[t, :k] = np.where(dist[sel] <= max_range, ADD, DELETE)
-        if n_delete:
-            far = rng.integers(0, n_landmarks, size=n_delete)
-            ids[t, k:k + n_delete] = far
-            rel[t, k:k + n_delete] = 100.0
-            actions[t, k:k + n_delete] = DELETE
-            k += n_delete
-        count[t] = k
-    return Scenario(n_landmarks, landmarks, wheel, ids, actions, rel, count, truth)
+    """A circle drive + sensing sequence over a given map. ``start_pose`` is (θ, x, y)."""
+    drive = circle_drive(n_messages, circle_radius, omega, tick_hz, ticks_per_msg,
+                         SENSE_NEAREST if nearest else SENSE_ALL)
+    sw = _generate(n_landmarks, drive, [seed], landmarks, max_markers=max_markers,
+                   start_pose=start_pose, sensor_sigma=sensor_sigma, slip=slip,
+                   max_range=max_range, shuffle=shuffle, n_delete=n_delete)
+    return sw.scenario(0)
 
 
 def basic_world(n_messages: int = 100, seed: int = 20240317, **kw) -> Scenario:
@@ -165,9 +382,40 @@ def random_landmarks(n: int, seed: int = 20240317, circle_radius: float = 1.0,
 
 def synthetic(n_landmarks: int, n_messages: int, seed: int = 20240317, max_markers: int = 16,
               **kw) -> Scenario:
-    """SURVEY.md §8d synthetic map: N landmarks, unit circle at ω = 0.5, m nearest markers."""
+    """SURVEY.md §8d synthetic map: N landmarks, unit circle at ω = 0.5, m nearest markers (only
+    the landmarks near the circle are ever sighted: see ``populated`` for a full map)."""
     lm = random_landmarks(n_landmarks, seed)
     return make_scenario(n_landmarks, lm, n_messages, seed=seed, max_markers=max_markers, **kw)
+
+
+def field_half(n_landmarks: int) -> float:
+    """landmarks uniform in [-L, L]², L = 0.5·√N m."""
+    return max(0.5 * math.sqrt(n_landmarks), 2.0)
+
+
+def swarm(n_landmarks: int, n_filters: int, n_messages: int, seed: int = 20240317,
+          max_markers: int = 16, survey: bool = True, **kw) -> Swarm:
+    """SURVEY.md §8d synthetic workload for ``n_filters`` independent filters, filter f seeded
+    ``seed + f`` (its own map, slip and sensor noise): ``n_messages`` of the unit circle at
+    ω = 0.5 with the m nearest markers, prefixed (``survey``) by the spiral warm-up that sights
+    every landmark (``Swarm.n_warm`` messages)."""
+    half = field_half(n_landmarks)
+    ring = kw.pop("ring", 4.0)
+    v_survey = kw.pop("v_survey", 4.0)
+    drive = (survey_drive(half, n_messages, ring=ring, v_survey=v_survey) if survey else
+             circle_drive(n_messages))
+    seeds = np.uint64(seed) + np.arange(n_filters, dtype=np.uint64)
+    sw = _generate(n_landmarks, drive, seeds, half=half, max_markers=max_markers, **kw)
+    if survey and not sw.sighted.all():
+        raise RuntimeError(f"survey left {int((~sw.sighted).sum())} landmarks unsighted")
+    return sw
+
+
+def populated(n_landmarks: int, n_messages: int, seed: int = 20240317, max_markers: int = 16,
+              **kw) -> Scenario:
+    """One filter of ``swarm``: the survey (``n_warm`` messages, every landmark sighted), then
+    ``n_messages`` of the circle."""
+    return swarm(n_landmarks, 1, n_messages, seed=seed, max_markers=max_markers, **kw).scenario(0)
 
 
 def lidar_scans(poses, circles, arena=(10.0, 5.0), n_beams=360, sigma=0.0, seed=20240317,
