@@ -1115,6 +1115,17 @@ int ekf_profile_read(ekf_t h, int kind, long long* launches, double* total_ms) {
 
 double ekf_normalize_angle(double rad) { return normalize_angle(rad); }
 
+int ekf_debug_poison_lds(int device) {
+  if (hipSetDevice(device) != hipSuccess) return EKF_E_HIP;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return EKF_E_HIP;
+  // a quiet NaN with a payload: NaN·0 = NaN, so any product with unwritten LDS poisons the result
+  const unsigned long long nan = 0x7ff8dead0000beefull;
+  if (launch_poison_lds(nan, 12 * (cus > 0 ? cus : 256), nullptr) != hipSuccess) return EKF_E_HIP;
+  return hipDeviceSynchronize() == hipSuccess ? EKF_OK : EKF_E_HIP;
+}
+
 #ifdef EKF_DIAG_STAMPS
 int ekfslam_diag_read_stamps(unsigned long long* out, int n);  // ekf_kernels.hip
 // dev only (libekfslam_diag.so): the chain kernel's s_memtime stamps of filter 0's last chunk

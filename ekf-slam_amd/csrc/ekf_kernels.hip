@@ -1964,6 +1964,23 @@ hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
   return hipGetLastError();
 }
 
+// Diagnostics (ekf_debug_poison_lds): overwrite a workgroup's whole LDS allocation with a NaN bit
+// pattern. Launched over every CU several times, it leaves LDS the way an arbitrary previous kernel
+// may, so a kernel that reads LDS it never wrote shows it deterministically (tests/).
+__global__ __launch_bounds__(256) void k_poison_lds(unsigned long long pattern) {
+  extern __shared__ unsigned long long lds_poison[];
+  for (int e = threadIdx.x; e < kPoisonLdsBytes / 8; e += blockDim.x) lds_poison[e] = pattern;
+  __syncthreads();
+  // keep the stores: one lane publishes a word the compiler cannot prove dead
+  if (threadIdx.x == 0 && lds_poison[blockIdx.x % (kPoisonLdsBytes / 8)] == 0x1ull)
+    lds_poison[0] = 0;
+}
+
+hipError_t launch_poison_lds(unsigned long long pattern, int n_blocks, hipStream_t s) {
+  hipLaunchKernelGGL(k_poison_lds, dim3(n_blocks), dim3(256), kPoisonLdsBytes, s, pattern);
+  return hipGetLastError();
+}
+
 #define EKF_INSTANTIATE(T)                                                              \
   template hipError_t launch_chain<T>(const PassArgs<T>&, int, int, hipStream_t, hipEvent_t,        \
                                       hipEvent_t);                                                 \

@@ -81,4 +81,9 @@ hipError_t launch_resident(const PassArgs<double>& a, const PlanEntry* plan, int
 template <typename T>
 hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int nf, hipStream_t s);
 
+// Diagnostics: n_blocks workgroups each fill kPoisonLdsBytes of LDS with `pattern` (three fit a
+// CU's 160 KiB, so a grid of ≥ 3·256 blocks covers every CU's LDS).
+constexpr int kPoisonLdsBytes = 53 * 1024;
+hipError_t launch_poison_lds(unsigned long long pattern, int n_blocks, hipStream_t s);
+
 }  // namespace ekfslam

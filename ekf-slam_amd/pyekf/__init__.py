@@ -31,6 +31,7 @@ EXPORTS = [
     "ekf_set_joseph",
     "ekf_reset", "slam_reset",
     "ekf_profile_enable", "ekf_profile_read", "ekf_sigma_pass_bytes", "ekf_normalize_angle",
+    "ekf_debug_poison_lds",
     "slam_create", "slam_destroy", "slam_joint_states", "slam_markers", "slam_initial_pose",
     "slam_odom", "slam_map_odom", "slam_filter", "slam_replay", "slam_integrate_odometry",
     "lm_create", "lm_destroy", "lm_detect", "lm_fit_circles", "lm_check_circles",
@@ -91,6 +92,7 @@ def lib():
             "ekf_profile_read": (_i, [_vp, _i, C.POINTER(C.c_longlong), _dp]),
             "ekf_sigma_pass_bytes": (C.c_double, [_vp, _i]),
             "ekf_normalize_angle": (C.c_double, [_d]),
+            "ekf_debug_poison_lds": (_i, [_i]),
             "slam_create": (_i, [C.POINTER(_vp), C.POINTER(Config), _d, _d, _i]),
             "slam_destroy": (_i, [_vp]),
             "slam_joint_states": (_i, [_vp, _d, _d]),
@@ -354,6 +356,12 @@ class Slam:
         rc = lib().slam_replay(self.h, T, ticks, _ptr(wheel), M, _ptr(counts), _ptr(ids),
                                _ptr(act), _ptr(rel), _ptr(out_p), _ptr(out_t))
         return rc, out_p, out_t
+
+
+def poison_lds(device=0):
+    """ekf_debug_poison_lds: every CU's LDS filled with a NaN pattern (tests: unwritten LDS reads
+    then fail deterministically)."""
+    _check(lib().ekf_debug_poison_lds(device), "ekf_debug_poison_lds")
 
 
 def odometry(sc, track=None, radius=None):

@@ -323,12 +323,13 @@ class Swarm:
 
 def _generate(n_landmarks, drive: Drive, seeds, landmarks=None, half=None, *, max_markers=16,
               start_pose=(0.0, 0.0, -1.0), sensor_sigma=1e-3, slip=0.02, max_range=5.0,
-              shuffle=False, n_delete=0, clearance=0.3) -> Swarm:
+              shuffle=False, n_delete=0, clearance=0.3, n_map=None) -> Swarm:
     seeds = np.asarray(seeds, dtype=np.uint64).reshape(-1)
     F = seeds.shape[0]
     wheel, truth, path = _simulate(drive, seeds, start_pose, slip)
     if landmarks is None:
-        landmarks = _place_landmarks(n_landmarks, half, seeds, path, clearance)
+        landmarks = _place_landmarks(n_landmarks if n_map is None else n_map, half, seeds, path,
+                                     clearance)
     else:
         landmarks = np.broadcast_to(np.asarray(landmarks, np.float64),
                                     (F,) + np.shape(landmarks)[-2:]).copy()
@@ -399,13 +400,15 @@ def swarm(n_landmarks: int, n_filters: int, n_messages: int, seed: int = 2024031
     ``seed + f`` (its own map, slip and sensor noise): ``n_messages`` of the unit circle at
     ω = 0.5 with the m nearest markers, prefixed (``survey``) by the spiral warm-up that sights
     every landmark (``Swarm.n_warm`` messages)."""
-    half = field_half(n_landmarks)
+    n_map = kw.pop("n_map", n_landmarks)  # landmarks placed (≤ N slots; the rest stay free for
+    half = field_half(n_map)               # the association path's new landmarks)
     ring = kw.pop("ring", 4.0)
     v_survey = kw.pop("v_survey", 4.0)
     drive = (survey_drive(half, n_messages, ring=ring, v_survey=v_survey) if survey else
              circle_drive(n_messages))
     seeds = np.uint64(seed) + np.arange(n_filters, dtype=np.uint64)
-    sw = _generate(n_landmarks, drive, seeds, half=half, max_markers=max_markers, **kw)
+    sw = _generate(n_landmarks, drive, seeds, half=half, max_markers=max_markers, n_map=n_map,
+                   **kw)
     if survey and not sw.sighted.all():
         raise RuntimeError(f"survey left {int((~sw.sighted).sum())} landmarks unsighted")
     return sw

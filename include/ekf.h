@@ -158,6 +158,12 @@ int ekf_profile_read(ekf_t h, int kernel, long long* launches, double* total_ms)
 /* Bytes the Σ pass must move per launch for the current handle (2·n²·w·F). */
 double ekf_sigma_pass_bytes(ekf_t h, int filters_in_launch);
 
+/* ---- diagnostics ---- */
+/* Fill every CU's LDS on `device` with a NaN bit pattern (default stream, synchronising): LDS then
+ * holds what an arbitrary earlier kernel could have left, so a kernel that reads LDS it never
+ * wrote produces a non-finite result deterministically instead of rarely (used by tests/). */
+int ekf_debug_poison_lds(int device);
+
 #ifdef __cplusplus
 }
 #endif

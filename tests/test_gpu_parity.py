@@ -179,53 +179,6 @@ def test_set_get_state_roundtrip():
     assert np.array_equal(ekf.map_odom(), g["tmo"][-1])
 
 
-def test_n256_fp64_against_oracle():
-    """BASELINE config 2 size (N=256, fp64) over 25 messages × 16 markers, vs the C oracle."""
-    sc = synth.synthetic(256, 25)
-    rc, poses, tmo, x, S, cnt, _ = _replay_node(sc, False)
-    o = orc.run_scenario(sc, False)
-    assert rc == 0
-    assert np.abs(poses - o["poses"]).max() < 1e-7
-    assert np.abs(S - o["sigma"]).max() < 1e-7
-
-
-def test_n1024_fp32_warm_state_against_oracle():
-    """BASELINE config 3 (N=1024, fp32 Σ): warm state from an fp64 pass, then fp32 vs fp64 oracle.
-
-    fp32 cannot take a first sighting against the 1e7 prior (1e7 − (1e7 − 1e-2) in fp32 is
-    noise), so the fp32 filter starts from the state of an fp64 lap. Tolerance:
-    posterior positions within 2e-4 m and headings within 2e-4 rad of the fp64 oracle after 40
-    messages (640 corrections)."""
-    N, warm, T = 1024, 63, 40
-    sc = synth.synthetic(N, warm + T)
-    odom = pyekf.odometry(sc)
-    M = sc.ids.shape[1]
-    ekf64 = pyekf.EKF(n_landmarks=N)
-    ekf64.replay(sc.count[:warm, None], sc.rel[:warm, None], odom[:warm, None],
-                 ids=sc.ids[:warm, None], actions=sc.actions[:warm, None])
-    x, S, cnt = ekf64.state()
-    tmo = ekf64.map_odom()
-    ekf64.close()
-    ekf32 = pyekf.EKF(n_landmarks=N, dtype=pyekf.EKF_F32)
-    ekf32.set_state(x, S, tmo=tmo, counter=cnt)
-    ref = orc.OracleEKF(n_landmarks=N)
-    ref.set(x, S, tmo, x[:3], cnt)
-    poses = ekf32.replay(sc.count[warm:, None], sc.rel[warm:, None], odom[warm:, None],
-                         ids=sc.ids[warm:, None], actions=sc.actions[warm:, None], poses=True)
-    for t in range(T):
-        ref.set_odom(odom[warm + t])
-        c = int(sc.count[warm + t])
-        ref.fake_sensor_cb(sc.ids[warm + t, :c], sc.actions[warm + t, :c], sc.rel[warm + t, :c])
-        xr, _, _, _ = ref.get(sigma=False)
-        d = np.abs(poses[t, 0] - xr[:3])
-        assert d.max() < 2e-4, (t, d)
-    x32, S32, _ = ekf32.state()
-    assert ekf32.status() == 0  # no numeric skip, no epoch-poll timeout
-    seen = np.abs(np.diag(S32)) < 1e6
-    assert np.all(np.diag(S32)[seen][3:] > 0)
-    assert np.all(np.isfinite(S32))
-
-
 def _pipelined_final(sc, monkeypatch, env, dtype=pyekf.EKF_F64, F=1):
     """Replay every message in one call (one upload, chunks pipelined across the two streams)."""
     for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
@@ -245,27 +198,31 @@ def _pipelined_final(sc, monkeypatch, env, dtype=pyekf.EKF_F64, F=1):
 
 @pytest.mark.parametrize("F", [1, 4], ids=["1filter", "4filters"])
 def test_pipelined_replay_sync_modes(monkeypatch, F):
-    """Two schedules of the same replay, run without per-message synchronisation so chunks
-    really overlap: the default event-synchronised two streams and the single-stream order launch
-    the same kernels on the same data, so bit-identical; both against the oracle. (The opt-in
-    device-epoch pipeline, EKF_DEVSYNC=1, carries the |U|×|U| block across a launch's chunks — a
-    different summation order — and has an open rare non-finite result)"""
+    """Three schedules of the same replay, run without per-message synchronisation so chunks
+    really overlap. The default event-synchronised two streams and the single-stream order launch
+    the same kernels on the same data: bit-identical. The device-epoch pipeline (EKF_DEVSYNC=1)
+    carries the |U|×|U| block across a launch's chunks (another summation order): against the
+    oracle. LDS is poisoned with NaNs first, so a chain that reads LDS it never wrote fails here
+    every time (the cause of round 1's rare non-finite device-epoch results)."""
     sc = synth.synthetic(256, 30)
     evt = _pipelined_final(sc, monkeypatch, {}, F=F)  # default: event-synchronised streams
     ser = _pipelined_final(sc, monkeypatch, {"EKF_SERIAL": "1"}, F=F)
+    pyekf.poison_lds()
+    dev = _pipelined_final(sc, monkeypatch, {"EKF_DEVSYNC": "1"}, F=F)
     for (xe, Se, ce), (xs, Ss, cs) in zip(evt, ser):
         assert ce == cs
         np.testing.assert_array_equal(xe, xs)
         np.testing.assert_array_equal(Se, Ss)
     o = orc.run_scenario(sc, False)
-    x, S, _ = evt[0]
-    assert np.abs(x - o["state"]).max() < 1e-7
-    assert np.abs(S - o["sigma"]).max() < 1e-7
+    for x, S, _ in (evt[0],) + tuple(dev):
+        assert np.abs(x - o["state"]).max() < 1e-7
+        assert np.abs(S - o["sigma"]).max() < 1e-7
 
 
 def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
-    """Config 3 size, fp32 Σ, 24 messages pipelined: device-epoch (carried block) vs single
-    stream (rebuilt block) agree to fp32 rounding of the stored Σ."""
+    """Config 3 size, fp32 Σ, 24 messages pipelined: the device-epoch schedule (EKF_DEVSYNC=1,
+    carried block, LDS poisoned first) against the single stream (rebuilt block): they agree to
+    fp32 rounding of the stored Σ."""
     N, warm, T = 1024, 40, 24
     sc = synth.synthetic(N, warm + T)
     odom = pyekf.odometry(sc)
@@ -276,17 +233,19 @@ def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
     tmo0 = e64.map_odom()
     e64.close()
     res = []
-    for env in ({}, {"EKF_SERIAL": "1"}):
+    for env in ({"EKF_DEVSYNC": "1"}, {"EKF_SERIAL": "1"}):
         for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
+        pyekf.poison_lds()
         e = pyekf.EKF(n_landmarks=N, dtype=pyekf.EKF_F32)
         e.set_state(x0, S0, tmo=tmo0, counter=c0)
         sl = slice(warm, warm + T)
         e.replay(sc.count[sl, None], sc.rel[sl, None], odom[sl, None], ids=sc.ids[sl, None],
                  actions=sc.actions[sl, None])
         res.append(e.state())
+        assert e.status() == 0, env
         e.close()
     assert np.abs(res[0][0] - res[1][0]).max() < 1e-5
     S0, S1 = res[0][1], res[1][1]
@@ -296,13 +255,18 @@ def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
     assert np.abs(S0[blk] - S1[blk]).max() < 1e-5
 
 
-@pytest.mark.parametrize("F", [24, 40], ids=["24filters_xcdgrid", "40filters_nocusplit"])
-def test_many_filters_match_small_batch(F, monkeypatch):
+@pytest.mark.parametrize("F,devsync", [(24, "0"), (24, "1"), (40, "0")],
+                         ids=["24filters_xcdgrid", "24filters_devsync", "40filters_nocusplit"])
+def test_many_filters_match_small_batch(F, devsync, monkeypatch):
     """≥16 filters take the XCD-aware Σ-pass grid, > 32 filters streams without a CU split;
     filter f replays scenario f % 8, and must equal the same scenario in an 8-filter handle bit for
-    bit (the arithmetic per filter does not depend on the batch or the schedule)."""
+    bit (the arithmetic per filter does not depend on the batch). devsync: both handles run the
+    device-epoch schedule (EKF_DEVSYNC=1, LDS poisoned first)."""
     for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("EKF_DEVSYNC", devsync)
+    if devsync == "1":
+        pyekf.poison_lds()
     N, T = 64, 12
     scs = [synth.synthetic(N, T, seed=100 + k) for k in range(8)]
     odo = [pyekf.odometry(s) for s in scs]
@@ -325,12 +289,11 @@ def test_many_filters_match_small_batch(F, monkeypatch):
         e = pyekf.EKF(n_landmarks=N, n_filters=nf)
         e.replay(cnt, rel, od, ids=ids, actions=act)
         out = [e.state(f) for f in range(nf)]
+        assert [e.status(f) for f in range(nf)] == [0] * nf
         e.close()
         return out
 
     big = run(F)
-    if F > 32:
-        monkeypatch.setenv("EKF_DEVSYNC", "0")
     small = run(8)
     for f in range(F):
         xs, Ss, cs = small[f % 8]
@@ -340,12 +303,17 @@ def test_many_filters_match_small_batch(F, monkeypatch):
         np.testing.assert_array_equal(Ss, Sb)
 
 
-@pytest.mark.parametrize("F,env", [(1, {}), (4, {}), (40, {"EKF_DEVSYNC": "0"})],
-                         ids=["1filter", "4filters", "40filters_events"])
+@pytest.mark.parametrize("F,env", [(1, {}), (4, {}), (40, {}), (1, {"EKF_DEVSYNC": "1"}),
+                                   (4, {"EKF_DEVSYNC": "1"})],
+                         ids=["1filter", "4filters", "40filters", "1filter_devsync",
+                              "4filters_devsync"])
 def test_rows_handoff_is_bit_identical(monkeypatch, F, env):
     """fp64: a Σ pass hands the next chunk's factor kernel Σ_in[i, U] as contiguous rows
     (kRowsOut / kRowsIn) — the very values it stores into Σ_out, so the replay equals the strided
-    gather (EKF_ROWS=0) bit for bit, including messages longer than one chunk."""
+    gather (EKF_ROWS=0) bit for bit, including messages longer than one chunk; in the default
+    event-synchronised schedule and the device-epoch one (LDS poisoned first)."""
+    if env:
+        pyekf.poison_lds()
     sc = synth.synthetic(96, 14, max_markers=24)
     assert sc.count.max() > 16  # some messages span two chunks
     monkeypatch.delenv("EKF_ROWS", raising=False)

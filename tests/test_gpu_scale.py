@@ -1,0 +1,238 @@
+"""The BASELINE configs at their full sizes on populated maps (an untimed warm-up
+that initialises every landmark), through the C-ABI, against the C oracle.
+
+* configs[1]: N=256, fp64, one filter — survey + circle vs the oracle.
+* configs[2]: N=1024 — the fp64 survey (1 024 first sightings, the only thing fp32 cannot do
+  against the 1e7 prior, slam.cpp:130) vs the oracle; then fp32 Σ from that warm state, vs the fp64
+  oracle, in the default and the device-epoch schedule.
+* configs[3]: N=256 × 512 filters (one GPU's share of 4 096), each seeded base + f: every filter's
+  status, a strided sample vs the oracle.
+* Association at scale: unknown ids against ≥ 256 known landmarks on the pipeline
+  (slam.cpp:344-440), decisions exactly equal to the oracle's.
+
+Tolerances: fp64 poses 1e-8 and Σ 1e-8 absolute (as tests/test_gpu_parity.py); fp32 Σ: poses within
+2e-4 of the fp64 oracle. Measured errors go to gpurun_out/scale_errors.json.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import orc
+import pyekf
+from pyekf import synth
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-8
+SIGMA_TOL = 1e-8
+ERRORS = {}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _record_errors():
+    yield
+    out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "scale_errors.json"), "w") as fh:
+        json.dump(ERRORS, fh, indent=1)
+
+
+def _initialised(x):
+    """Landmark slots whose state is no longer (0, 0) (the first-sighting test, slam.cpp:213)."""
+    return int(np.count_nonzero(np.any(x[3:].reshape(-1, 2) != 0.0, 1)))
+
+
+def _oracle_from(ws, N):
+    x, S, tmo, cnt = ws
+    ref = orc.OracleEKF(n_landmarks=N)
+    ref.set(x, S, tmo, x[:3], cnt)
+    return ref
+
+
+def _replay(e, sl, sc, odom, assoc=False, poses=False):
+    return e.replay(sc.count[sl, None], sc.rel[sl, None], odom[sl, None],
+                    ids=None if assoc else sc.ids[sl, None], actions=sc.actions[sl, None],
+                    assoc=assoc, poses=poses)
+
+
+def test_n256_fp64_populated_against_oracle():
+    """configs[1]: survey (125 messages, all 256 landmarks) + 25 circle messages, fp64."""
+    sc = synth.populated(256, 25)
+    s = pyekf.Slam(n_landmarks=256, source=pyekf.SOURCE_SIM)
+    rc, poses, tmo = s.replay(sc)
+    x, S, cnt = s.filter_state()
+    s.close()
+    o = orc.run_scenario(sc, False)
+    assert rc == 0
+    assert _initialised(x) == 256
+    ERRORS["n256_fp64"] = {"pose": float(np.abs(poses - o["poses"]).max()),
+                           "sigma": float(np.abs(S - o["sigma"]).max())}
+    assert np.abs(poses - o["poses"]).max() < POSE_TOL
+    assert np.abs(x - o["state"]).max() < POSE_TOL
+    assert np.abs(S - o["sigma"]).max() < SIGMA_TOL
+
+
+@pytest.fixture(scope="module")
+def n1024():
+    """configs[2]'s map: the fp64 survey on the GPU (every landmark sighted), and its state."""
+    sc = synth.populated(1024, 40)
+    odom = pyekf.odometry(sc)
+    w = sc.n_warm
+    e = pyekf.EKF(n_landmarks=1024)
+    _replay(e, slice(0, w), sc, odom)
+    x, S, cnt = e.state()
+    ws = (x, S, e.map_odom(), cnt)
+    assert e.status() == 0
+    e.close()
+    return sc, odom, ws
+
+
+def test_n1024_fp64_survey_against_oracle(n1024):
+    """All 1 024 first sightings (the 1e7-prior cancellations) on the pipeline vs the oracle."""
+    sc, odom, (x, S, tmo, cnt) = n1024
+    w = sc.n_warm
+    ref = orc.OracleEKF(n_landmarks=1024)
+    for t in range(w):
+        ref.set_odom(odom[t])
+        c = int(sc.count[t])
+        ref.fake_sensor_cb(sc.ids[t, :c], sc.actions[t, :c], sc.rel[t, :c])
+    xr, Sr, tmr, _ = ref.get()
+    assert _initialised(x) == 1024
+    ERRORS["n1024_fp64_survey"] = {"state": float(np.abs(x - xr).max()),
+                                   "sigma": float(np.abs(S - Sr).max())}
+    assert np.abs(x - xr).max() < POSE_TOL
+    assert np.abs(tmo - tmr).max() < POSE_TOL
+    assert np.abs(S - Sr).max() < SIGMA_TOL
+
+
+@pytest.mark.parametrize("env", [{}, {"EKF_DEVSYNC": "1"}], ids=["events", "devsync"])
+def test_n1024_fp32_populated_against_oracle(n1024, env, monkeypatch):
+    """configs[2]: fp32 Σ over 40 circle messages (640 corrections of a fully correlated 1 024-
+    landmark map) from the fp64 survey's state, vs the fp64 oracle from the same state."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc, odom, ws = n1024
+    w, T = sc.n_warm, sc.n_messages - sc.n_warm
+    assert _initialised(ws[0]) == 1024
+    pyekf.poison_lds()
+    e = pyekf.EKF(n_landmarks=1024, dtype=pyekf.EKF_F32)
+    x, S, tmo, cnt = ws
+    e.set_state(x, S, tmo=tmo, counter=cnt)
+    poses = _replay(e, slice(w, w + T), sc, odom, poses=True)
+    ref = _oracle_from(ws, 1024)
+    err = 0.0
+    for t in range(T):
+        ref.set_odom(odom[w + t])
+        c = int(sc.count[w + t])
+        ref.fake_sensor_cb(sc.ids[w + t, :c], sc.actions[w + t, :c], sc.rel[w + t, :c])
+        xr = ref.get(sigma=False)[0]
+        err = max(err, float(np.abs(poses[t, 0] - xr[:3]).max()))
+    x32, S32, _ = e.state()
+    assert e.status() == 0
+    e.close()
+    xr, Sr, _, _ = ref.get()
+    ERRORS["n1024_fp32_" + ("devsync" if env else "events")] = {
+        "pose": err, "state": float(np.abs(x32 - xr).max()),
+        "sigma": float(np.abs(S32 - Sr).max())}
+    assert err < 2e-4
+    assert np.all(np.isfinite(S32))
+    assert np.abs(x32 - xr).max() < 2e-4
+
+
+def test_swarm_n256_512_filters_against_oracle():
+    """configs[3], one GPU's share: 512 filters of N=256 fp64 in one handle, filter f seeded
+    base + f (its own map, slip and noise), survey + 8 circle messages. Every filter's status is
+    clear and every landmark initialised; 8 strided filters equal their own oracle runs."""
+    F = 512
+    sw = synth.swarm(256, F, 8)
+    T = sw.count.shape[0]
+    odom = np.repeat(pyekf.odometry(sw.scenario(0))[:, None], F, 1)
+    e = pyekf.EKF(n_landmarks=256, n_filters=F)
+    e.replay(sw.count, sw.rel, odom, ids=sw.ids, actions=sw.actions)
+    assert [e.status(f) for f in range(F)] == [0] * F
+    init = [_initialised(e.state(f, sigma=False)[0]) for f in range(F)]
+    assert min(init) == 256
+    errs = []
+    for f in range(0, F, F // 8):
+        o = orc.run_scenario(sw.scenario(f), False)
+        x, S, cnt = e.state(f)
+        errs.append((float(np.abs(x - o["state"]).max()), float(np.abs(S - o["sigma"]).max())))
+        assert np.abs(x[:3] - o["poses"][-1]).max() < POSE_TOL, f
+        assert np.abs(x - o["state"]).max() < POSE_TOL, f
+        assert np.abs(S - o["sigma"]).max() < SIGMA_TOL, f
+    e.close()
+    ERRORS["swarm_n256x512"] = {"state": max(a for a, _ in errs), "sigma": max(b for _, b in errs),
+                                "messages": T}
+
+
+@pytest.fixture(scope="module")
+def known_map():
+    """512 slots, 256 landmarks surveyed with known ids (fp64 pipeline): the state the unknown-
+    association messages start from, counter = 256 (slam.cpp:351-356 numbering)."""
+    sc = synth.populated(512, 6, n_map=256, shuffle=True)
+    odom = pyekf.odometry(sc)
+    e = pyekf.EKF(n_landmarks=512)
+    _replay(e, slice(0, sc.n_warm), sc, odom)
+    x, S, _ = e.state()
+    ws = (x, S, e.map_odom(), 256)
+    e.close()
+    assert _initialised(x) == 256
+    return sc, odom, ws
+
+
+def test_association_at_scale_decisions(known_map):
+    """ekf_sensor (sensor_cb) against ≥ 256 known landmarks on the pipeline: every marker's
+    decision (landmark index, new or not) equal to the oracle's, poses 1e-8."""
+    sc, odom, ws = known_map
+    e = pyekf.EKF(n_landmarks=512)
+    x, S, tmo, cnt = ws
+    e.set_state(x, S, tmo=tmo, counter=cnt)
+    ref = _oracle_from(ws, 512)
+    n_new = n_old = 0
+    for t in range(sc.n_warm, sc.n_messages):
+        e.set_odom(odom[t])
+        ref.set_odom(odom[t])
+        c = int(sc.count[t])
+        rc, j, nw = e.sensor(sc.rel[t, :c])
+        rr, jr, nr = ref.sensor_cb(sc.rel[t, :c])
+        assert rc == rr == 0
+        assert np.array_equal(j, jr) and np.array_equal(nw, nr), t
+        n_new += int(nr.sum())
+        n_old += int(c - nr.sum())
+        assert np.abs(e.pose() - ref.get(sigma=False)[0][:3]).max() < POSE_TOL
+    xg, Sg, cg = e.state()
+    xr, Sr, _, cr = ref.get()
+    e.close()
+    ERRORS["assoc_n512_known256"] = {"new": n_new, "associated": n_old, "counter": int(cg),
+                                     "state": float(np.abs(xg - xr).max()),
+                                     "sigma": float(np.abs(Sg - Sr).max())}
+    assert cg == cr and cg >= 256
+    assert n_old > 0  # some markers really matched known landmarks
+    assert np.abs(xg - xr).max() < POSE_TOL
+    assert np.abs(Sg - Sr).max() < SIGMA_TOL
+
+
+def test_association_at_scale_batched_replay(known_map):
+    """The same messages through ekf_replay(assoc=1) (decisions on the device, no host round
+    trip), from the same state: the final state equals the oracle's."""
+    sc, odom, ws = known_map
+    e = pyekf.EKF(n_landmarks=512)
+    x, S, tmo, cnt = ws
+    e.set_state(x, S, tmo=tmo, counter=cnt)
+    w = sc.n_warm
+    _replay(e, slice(w, sc.n_messages), sc, odom, assoc=True)
+    ref = _oracle_from(ws, 512)
+    for t in range(w, sc.n_messages):
+        ref.set_odom(odom[t])
+        ref.sensor_cb(sc.rel[t, :int(sc.count[t])])
+    xg, Sg, cg = e.state()
+    xr, Sr, _, cr = ref.get()
+    assert e.status() == 0
+    e.close()
+    assert cg == cr
+    assert np.abs(xg - xr).max() < POSE_TOL
+    assert np.abs(Sg - Sr).max() < SIGMA_TOL
