@@ -91,6 +91,7 @@ struct ekf_ctx {
   int ring_next = 0;
   // scratch
   std::vector<std::vector<Marker>> msgs;
+  std::vector<char> absent;  // batch paths: counts[f] == 0, the filter gets no message this step
   // profiling
   bool prof = false;
   ProfEvents pe[5];
@@ -199,20 +200,24 @@ int join_bulk(ekf_ctx* h) {
 // Without the CU split a spinning factor grid could hold every CU the chain needs, so events are
 // used instead (the kernels' polls are then satisfied on arrival).
 // `nchunks` consecutive chunks of filters [f0, f0+nf) (descriptors dptr[i·nf + k]): ONE chain
-// launch that walks them all (carrying its block from chunk to chunk), then per chunk the factor
+// launch that walks them all (rebuilding its block from the chunk before each time), then per chunk the factor
 // kernel and the Σ pass on the bulk stream. More than one chunk only with devsync, where the bulk
 // kernels of chunk i wait on the device for the chain's epoch of chunk i.
 template <typename T>
-int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined) {
+int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined,
+                 bool nolook) {
   PassArgs<T> a = args<T>(h, dptr, f0);
   a.desc_stride = nf;
   const unsigned s0 = static_cast<unsigned>(h->seq);
   a.seq = s0;
   const bool two = pipelined && !h->serial;
   hipStream_t ms = h->stream, bs = two ? h->bulk : h->stream;
-  if (pipelined) {
+  a.polls = two && h->devsync ? 1 : 0;
+  if (pipelined && !nolook) {
+    // events: a rebuilding (kLook) chain needs the Σ pass two launches back
     if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s0 & 1], 0));
-  } else {
+  } else if (!a.polls) {
+    // a chain that gathers its own Σ_in needs the previous pass: everything on the bulk stream
     if (join_bulk(h)) return EKF_E_HIP;
   }
   int rc = timed(h, 1, ms, [&](hipEvent_t e0, hipEvent_t e1) {
@@ -248,9 +253,11 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, b
   return EKF_OK;
 }
 
-int group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined) {
-  return h->cfg.dtype == EKF_F32 ? launch_group<float>(h, dptr, f0, nf, nchunks, pipelined)
-                                 : launch_group<double>(h, dptr, f0, nf, nchunks, pipelined);
+// nolook: some active filter's first chunk gathers its own Σ_in (no kLook rebuild)
+int group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined,
+          bool nolook = true) {
+  return h->cfg.dtype == EKF_F32 ? launch_group<float>(h, dptr, f0, nf, nchunks, pipelined, nolook)
+                                 : launch_group<double>(h, dptr, f0, nf, nchunks, pipelined, nolook);
 }
 
 // The chain → factors kernels of a message are a latency-bound critical path; the Σ pass of the
@@ -275,10 +282,10 @@ int create_streams(ekf_ctx* h) {
     for (int b = 0; b < cus; ++b) (b < split * kXcd ? mmain : mbulk)[b / 32] |= 1u << (b % 32);
     if (hipExtStreamCreateWithCUMask(&h->stream, words, mmain.data()) == hipSuccess &&
         hipExtStreamCreateWithCUMask(&h->bulk, words, mbulk.data()) == hipSuccess) {
-      // device-epoch hand-offs are opt-in (EKF_DEVSYNC=1): a rare non-finite result in that mode
-      // is open (known issue); the default synchronises the streams with events
+      // device-epoch hand-offs by default; EKF_DEVSYNC=0 synchronises the streams with events
+      // (same kernels, one chain launch per chunk: bit-identical to the single-stream order)
       const char* e = std::getenv("EKF_DEVSYNC");
-      h->devsync = e && std::atoi(e) == 1;
+      h->devsync = !(e && std::atoi(e) == 0);
       return EKF_OK;
     }
     if (h->stream) hipStreamDestroy(h->stream);
@@ -310,33 +317,19 @@ int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
   });
 }
 
-// kLook descriptors: where each index of this chunk's U sits in the previous chunk's U' (the
-// chain's mapping: pose 0..2, marker c → 3+2·id, 4+2·id, a bad id → slot 0's columns 3, 4).
+// The chain's column of position a of a chunk's U (pose 0..2, marker c → 3+2·id, 4+2·id, a bad
+// id → slot 0's columns 3, 4).
 int ucol(const int* ids, int a, int N) {
   if (a < 3) return a;
   const int id = ids[(a - 3) >> 1];
   return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
 }
 
-void index_map(MsgDesc* d, int N) {
-  auto col = [N](const int* ids, int a) { return ucol(ids, a, N); };
-  const int nu = 3 + 2 * d->m, np = 3 + 2 * d->prev_m;
-  d->nnew = 0;
-  for (int a = 0; a < kMaxU + 1; ++a) {
-    int pos = -1;
-    if (a < nu) {
-      const int u = col(d->ids, a);
-      for (int k = 0; k < np && pos < 0; ++k)
-        if (col(d->prev_ids, k) == u) pos = k;
-      if (pos < 0) ++d->nnew;
-    }
-    d->cpos[a] = static_cast<signed char>(pos);
-  }
-}
-
 // Known association, one message per filter in [f0, f0+nf): msgs[k] holds filter f0+k's markers.
 // Predict + chunks of ≤ kMaxChunk corrections + posterior (slam.cpp:180-316), appended to the plan.
-void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
+// absent[k] (batch paths): filter f0+k receives no message this step — its descriptor is inactive,
+// nothing of it changes (an empty MarkerArray is rejected before anything changes, EKF_E_EMPTY).
+void plan_known(ekf_ctx* h, int f0, int nf, bool predict, const char* absent = nullptr) {
   int chunks = 1;
   for (int k = 0; k < nf; ++k)
     chunks = std::max(chunks, static_cast<int>((h->msgs[k].size() + kMaxChunk - 1) / kMaxChunk));
@@ -349,7 +342,7 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
       const auto& mk = h->msgs[k];
       const int nchunks = std::max(1, static_cast<int>((mk.size() + kMaxChunk - 1) / kMaxChunk));
       MsgDesc* d = &h->plan_d[off + k];
-      if (chunk >= nchunks) {
+      if (chunk >= nchunks || (absent && absent[k])) {
         std::memset(d, 0, sizeof(MsgDesc));
         continue;
       }
@@ -368,7 +361,6 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
         d->z[i][0] = mk[b + i].zr;
         d->z[i][1] = mk[b + i].zb;
       }
-      if (flags & kLook) index_map(d, h->cfg.n_landmarks);
       // fp64: the previous chunk's Σ pass (same plan, not uploaded yet) hands this chunk's factor
       // kernel Σ_in[i, U] as contiguous rows instead of a gather strided by ld
       if (h->rows && !h->resident && h->last_desc[f] >= 0 && m > 0) {
@@ -392,7 +384,8 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict) {
 // Unknown association (slam.cpp:318-530), markers [i0, i1) of each filter's message: per marker the
 // association kernel + a single-marker launch pair. Decisions land in FilterCtl::assoc_j/new at
 // slot i % kMaxAssoc.
-void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0, int i1) {
+void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0, int i1,
+                const char* absent = nullptr) {
   for (int i = i0; i < i1; ++i) {
     const size_t off = h->plan_d.size();
     h->plan_d.resize(off + nf);
@@ -401,7 +394,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
       const auto& mk = h->msgs[k];
       const int mf = static_cast<int>(mk.size());
       MsgDesc* d = &h->plan_d[off + k];
-      if (i >= std::max(mf, 1)) {
+      if (i >= std::max(mf, 1) || (absent && absent[k])) {
         std::memset(d, 0, sizeof(MsgDesc));
         continue;
       }
@@ -537,7 +530,12 @@ int flush(ekf_ctx* h) {
         while (lj < nl && h->plan_l[lj].kind == 0 && h->plan_l[lj].f0 == L.f0 &&
                h->plan_l[lj].nf == L.nf && h->plan_l[lj].off == h->plan_l[lj - 1].off + L.nf)
           ++lj;
-      rc = group(h, dp, L.f0, L.nf, static_cast<int>(lj - li), true);
+      bool nolook = false;
+      for (int k = 0; k < L.nf; ++k) {
+        const int fl = h->plan_d[L.off + k].flags;
+        nolook = nolook || ((fl & kActive) && !(fl & kLook));
+      }
+      rc = group(h, dp, L.f0, L.nf, static_cast<int>(lj - li), true, nolook);
       li = lj;
       continue;
     }
@@ -611,6 +609,7 @@ int load_batch(ekf_ctx* h, int assoc_mode, int m_max, const int* counts, const i
   }
   for (int f = 0; f < h->F; ++f) {
     if (odom) h->odom[f] = Pose2{odom[3 * f], odom[3 * f + 1], odom[3 * f + 2]};
+    h->absent[f] = counts[f] == 0;
     auto& mk = h->msgs[f];
     mk.clear();
     for (int i = 0; i < counts[f]; ++i) {
@@ -683,6 +682,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   h->last_desc.assign(h->F, -1L);
   h->prev_ids.assign(h->F, std::array<int, kMaxChunk>{});
   h->msgs.resize(h->F);
+  h->absent.assign(h->F, 0);
   auto fail = [&](int rc) {
     ekf_destroy(h);
     return rc;
@@ -860,9 +860,9 @@ int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, cons
   if (assoc_mode) {
     int mm = 1;
     for (int f = 0; f < h->F; ++f) mm = std::max(mm, static_cast<int>(h->msgs[f].size()));
-    plan_assoc(h, 0, h->F, true, true, 0, mm);
+    plan_assoc(h, 0, h->F, true, true, 0, mm, h->absent.data());
   } else {
-    plan_known(h, 0, h->F, true);
+    plan_known(h, 0, h->F, true, h->absent.data());
   }
   return submit(h);
 }
@@ -885,9 +885,9 @@ int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, con
     if (assoc_mode) {
       int mm = 1;
       for (size_t f = 0; f < F; ++f) mm = std::max(mm, static_cast<int>(h->msgs[f].size()));
-      plan_assoc(h, 0, h->F, true, true, 0, mm);
+      plan_assoc(h, 0, h->F, true, true, 0, mm, h->absent.data());
     } else {
-      plan_known(h, 0, h->F, true);
+      plan_known(h, 0, h->F, true, h->absent.data());
     }
     // Many filters: upload and launch every ~kFlushDesc descriptors, so planning the next
     // messages on the host overlaps the GPU's work on these (one filter keeps the whole replay in

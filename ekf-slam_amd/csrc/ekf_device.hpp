@@ -47,8 +47,6 @@ struct alignas(16) MsgDesc {
   int ids[kMaxChunk];        // landmark ids; < 0 ⇒ taken from FilterCtl::assoc_j[assoc_slot + c]
   double z[kMaxChunk][2];    // measured (range, bearing), computed on the host like slam.cpp:208-210
   int prev_ids[kMaxChunk];   // kLook: the previous chunk's ids (its index set U', known up front)
-  signed char cpos[kMaxU + 1];  // kLook: position of U[a] in U' (−1: new to this chunk)
-  int nnew;                     // kLook: count of cpos < 0
   int nxt_nu;                   // kRowsOut: |U_next|
   int pad2;
   int nxt_u[kMaxU + 1];         // kRowsOut: U_next in the next chain's order (ekf_api index_map)

@@ -63,6 +63,34 @@ extern "C" int ekfslam_diag_read_stamps(unsigned long long* out, int n) {
 namespace ekfslam {
 #endif
 
+// Diagnostic build only (tools/diag_blocks.py): filter 0's chain block Σ[U, U] and x[U] as the
+// corrections start (predict folded in), per chunk sequence number mod 64.
+#ifdef EKF_DIAG_STAMPS
+__device__ double g_blocks[64][kMaxU][kMaxU + 1];
+__device__ double g_blockx[64][kMaxU];
+}  // namespace ekfslam
+extern "C" int ekfslam_diag_read_blocks(double* blocks, double* xs) {
+  using namespace ekfslam;
+  if (hipMemcpyFromSymbol(blocks, HIP_SYMBOL(g_blocks), sizeof(g_blocks)) != hipSuccess) return -5;
+  return hipMemcpyFromSymbol(xs, HIP_SYMBOL(g_blockx), sizeof(g_blockx)) == hipSuccess ? 0 : -5;
+}
+namespace ekfslam {
+#define EKF_DUMP_BLOCK(seq)                                                         \
+  do {                                                                              \
+    __syncthreads();                                                                \
+    if (blockIdx.y == 0) {                                                          \
+      for (int e = threadIdx.x; e < kMaxU * (kMaxU + 1); e += blockDim.x)           \
+        (&g_blocks[(seq) & 63][0][0])[e] = (&sh.P[0][0][0])[e];                      \
+      if (threadIdx.x < kMaxU) g_blockx[(seq) & 63][threadIdx.x] = sh.xU[0][threadIdx.x]; \
+    }                                                                               \
+    __syncthreads();                                                                \
+  } while (0)
+#else
+#define EKF_DUMP_BLOCK(seq) \
+  do {                      \
+  } while (0)
+#endif
+
 // Diagnostic build only (tools/sigma_bench.hip): s_memrealtime (100 MHz) per Σ-pass workgroup.
 #ifdef EKF_DIAG_STAMPS
 __device__ unsigned long long g_sig_stamps[4096][5];
@@ -125,11 +153,9 @@ struct ChainShared {
     double r0U[kMaxU], c0U[kMaxU], r0P[kMaxU], c0P[kMaxU];
     double xg[kMaxU];             // x_in'[u] for this chunk's U (rows the previous chunk missed)
   } pv;
-  double Pst[kMaxU][kMaxU + 1];  // carry: the previous chunk's final Σ[U', U'] (its U' order)
   double junk[4][64];             // per-wave sink of masked-off LDS stores (no divergent branch)
   double junk2[64][2];
   double pose[3];
-  double npose[3], na1, na2;  // the next chunk's predicted pose and A entries (its prefetch)
   double xpose[3];  // x_in pose (posterior of the previous chunk)
   double tmo[3];    // t_map_odom
   double a1, a2, s00;
@@ -205,8 +231,11 @@ constexpr int kChainThreads = 256;
 
 // One workgroup per filter, persistent over the `nchunks` chunks of a launch (descriptors
 // A.desc[i·desc_stride + filter]): per chunk the m sequential corrections on the |U|×|U| block.
-// From the second chunk on, the block, x[U] and the factors of the chunk before stay in LDS
-// ("carry"): only indices new to U are gathered from HBM.
+// Every chunk of a launch after the first rebuilds its block from the chunk before (kLook): the
+// previous Σ_in (complete) and the record, the factor kernel's formulas at U. (Carrying the
+// chain's own final block into the next chunk instead was 6 % faster but let the chain's block and
+// the HBM Σ drift apart — two roundings of the 1e7-prior first sightings — until a survey replay
+// went non-finite; the rebuild keeps every schedule bit-identical)
 template <typename T>
 __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchunks) {
   __shared__ ChainShared sh;
@@ -222,7 +251,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // so padding rows / columns that feed MFMA or dot products as zeros really are zeros
   for (int e = tid; e < static_cast<int>(sizeof(ChainShared) / 8); e += blockDim.x)
     reinterpret_cast<double*>(&sh)[e] = 0.0;
-  bool have_carry = false;
   bool pre = false;        // sdesc[ci & 1] was prefetched by the previous chunk's epilogue
   unsigned pending = 0;    // chain epoch of the previous chunk, not yet published (its record
                            // stores are still in flight; see the epilogue)
@@ -235,40 +263,26 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           reinterpret_cast<const uint4*>(&gd)[threadIdx.x];
     __syncthreads();
   }
-  const bool was_pre = pre;
   pre = false;
   const MsgDesc& d = sdesc[ci & 1];
   const bool active = (d.flags & kActive) != 0;
   const bool look = (d.flags & kLook) != 0;
-  const bool carry = look && have_carry;
-  // the previous epilogue computed this chunk's predicted pose iff it prefetched the descriptor
-  // and the chunk is an active kLook one (here: carried)
-  const bool pose_pre = was_pre && carry;
   // Publish the previous chunk's record before this chunk waits on anything the bulk stream
-  // produces (its factor kernel needs that record). A carried chunk with no new index waits on
-  // nothing: it publishes just before its corrections, with the record stores long complete.
-  if (pending && !(active && carry && d.nnew == 0)) {
+  // produces (its factor kernel needs that record).
+  if (pending) {
     drain_stores();
     __syncthreads();
     if (tid == 0) epoch_store(A.sync + kSyncChain + f, pending);
     pending = 0;
   }
-  if (!active) continue;  // this filter sits the chunk out; its carry stays valid
+  if (!active) continue;  // this filter sits the chunk out
   const unsigned seq = A.seq + static_cast<unsigned>(ci);
   // Σ_in / x / records a rebuilding chain reads come from the Σ pass two launches back (bulk
-  // stream); a chunk that gathers its own Σ_in needs the pass one back. Carry waits only when it
-  // has new indices to gather (below).
+  // stream), and this record parity is free again once that pass is done (its factor kernel read
+  // it); a chunk that gathers its own Σ_in needs the pass one back.
   const unsigned need = look ? (seq >= 2 ? seq - 1 : 0u) : seq;
-  if (!carry && need && tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, need))
+  if (A.polls && need && tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, need))
     atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
-  if (carry && d.nnew > 0) {  // the previous chunk's Z', Y' rebuild the rows of new indices
-    for (int e = tid; e < kMaxU * (kZC + 1); e += blockDim.x) (&sh.pv.Z[0][0])[e] = (&sh.Z[0][0])[e];
-    // Y's padding column kMaxU is never written by wave 2: zero it here (the rebuild multiplies it
-    // by C's zero row, and LDS garbage there can be a NaN: NaN·0 = NaN)
-    for (int e = tid; e < kZC * (kMaxU + 1); e += blockDim.x)
-      (&sh.pv.Y[0][0])[e] = e % (kMaxU + 1) == kMaxU ? 0.0 : (&sh.Y[0][0])[e];
-    if (tid < kZC) sh.pv.Z[kMaxU][tid] = 0.0;
-  }
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
   if (tid == 0) sh.status = 0;
   __syncthreads();
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     sh.u[tid] = u;
   }
   if (tid == 0) sh.nu_cnt = 3 + 2 * m;
-  if (look && !carry && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0)
+  if (look && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0)
     const int pm = d.prev_m;
     int u = 0;
     if (tid < 3) {
@@ -324,212 +338,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   constexpr int kW = kMaxU + 1;  // block entries are indexed e = a·36 + b (constant divisor)
   constexpr int kPer = (kW * kW + kChainThreads - 1) / kChainThreads;  // 6
   const int wv = tid >> 6, ln = tid & 63, i16 = ln & 15, k4 = ln >> 4;
-  if (carry) {
-    // The previous chunk of this launch left, in LDS: its final Σ[U', U'] (Pst), x[U'], Z', Y',
-    // K'_c (KU, every row of U') and M'_c (MU, every column of U'). Entries of Σ_in[U, U] with both
-    // indices in U' are Pst's; an entry with an index new to U is
-    //   Σ_pred'[u_a, u_b] − Σ_c K'_c[a]·M'_c[b],  K'_c[a] = Σ_pred'[u_a, U']·Z'_c for a new row,
-    //                                              M'_c[b] = Y'_c·Σ_pred'[U', u_b] for a new column,
-    // with Σ_pred' gathered from Σ_in' (the other buffer, complete two passes back).
-    // d.cpos is the host's index map (ekf_api.cpp index_map): position of u_a in U', −1 if new.
-    const int np = sh.pv.nu, zc = 2 * sh.pv.m;
-    const bool any_new = d.nnew > 0;
-    EKF_STAMP(8);
-    if (!any_new && pose_pre) {
-      // Σ_in[U, U] = Pst permuted, x[U] = x[U'] permuted, and this chunk's predict folded in
-      // directly (the A3 fold below, same expressions): one pass, no gather, no barrier.
-      // (indices clamped, reads unconditional: all of a thread's LDS reads in flight together)
-      const double qa1 = sh.na1, qa2 = sh.na2, p00 = sh.Pst[0][0];
-      int ua[kPer], ub[kPer];
-      double vp[kPer], vr[kPer], vc[kPer];
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const int e = tid + i * kChainThreads;
-        const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
-        const int pa = max(static_cast<int>(d.cpos[a]), 0), pb = max(static_cast<int>(d.cpos[b]), 0);
-        ua[i] = sh.u[a];
-        ub[i] = sh.u[b];
-        vp[i] = sh.Pst[pa][pb];
-        vr[i] = sh.Pst[0][pb];
-        vc[i] = sh.Pst[pa][0];
-      }
-      EKF_STAMP(17);
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const int e = tid + i * kChainThreads;
-        const int a = e / kW, b = e % kW;
-        double v = vp[i];
-        if (first) {
-          const double aa = alpha_of(ua[i], qa1, qa2), ab = alpha_of(ub[i], qa1, qa2);
-          v = v + aa * vr[i];
-          v = v + (vc[i] + aa * p00) * ab;
-          if (ua[i] == ub[i] && ua[i] < 3) v += A.q;
-        }
-        if (a < nu && b < nu) sh.P[0][a][b] = v;
-      }
-      EKF_STAMP(18);
-      if (tid < nu) {
-        const int pos = d.cpos[tid];
-        sh.xU[0][tid] = tid < 3 ? sh.npose[tid] : sh.pv.xU[pos];
-        sh.alphaU[tid] = first ? alpha_of(sh.u[tid], qa1, qa2) : 0.0;
-        sh.row0raw[tid] = sh.Pst[0][pos];
-        sh.col0raw[tid] = sh.Pst[pos][0];
-      }
-      if (tid == 0) {
-        sh.s00 = sh.Pst[0][0];
-        sh.a1 = qa1;
-        sh.a2 = qa2;
-      }
-    } else {
-    if (any_new) {
-      if (tid == 0 && need && !epoch_wait_acquire(A.sync + kSyncSigma, need))
-        atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
-      drain_stores();
-      __syncthreads();
-      const T* Sp = A.sig[d.parity ^ 1] + f * A.sig_stride;
-      const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
-      double vd[kPer], vr[kPer], vc[kPer];
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const int e = tid + i * kChainThreads;
-        const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
-        const size_t ua = static_cast<size_t>(sh.u[a]) * ld, pa = static_cast<size_t>(sh.pv.u[b]);
-        vd[i] = static_cast<double>(Sp[ua + sh.u[b]]);
-        vr[i] = static_cast<double>(Sp[ua + pa]);
-        vc[i] = static_cast<double>(Sp[pa * ld + sh.u[a]]);
-      }
-      const int tc = tid < kMaxU ? tid : 0;
-      const int uu = sh.u[tc], pu = sh.pv.u[tc];
-      const double r0u = static_cast<double>(Sp[uu]);
-      const double c0u = static_cast<double>(Sp[static_cast<size_t>(uu) * ld]);
-      const double r0p = static_cast<double>(Sp[pu]);
-      const double c0p = static_cast<double>(Sp[static_cast<size_t>(pu) * ld]);
-      const double x2 = xp[uu];
-      if (tid < kMaxU) {
-        sh.pv.r0U[tid] = r0u;
-        sh.pv.c0U[tid] = c0u;
-        sh.pv.r0P[tid] = r0p;
-        sh.pv.c0P[tid] = c0p;
-        sh.pv.xg[tid] = x2;
-      }
-      __syncthreads();
-      const bool pf = sh.pv.first != 0;
-      const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const int e = tid + i * kChainThreads;
-        const int a = e / kW, b = e % kW;
-        if (a < nu && b < nu) {
-          double v = vd[i];
-          if (pf) {
-            const double ai = alpha_of(sh.u[a], qa1, qa2), aj = alpha_of(sh.u[b], qa1, qa2);
-            v = v + ai * sh.pv.r0U[b];
-            v = v + (sh.pv.c0U[a] + ai * s00) * aj;
-            if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
-          }
-          sh.P[0][a][b] = v;
-        }
-        if (a < nu && b < kW) {
-          double v = 0.0, w = 0.0;
-          if (b < np) {
-            v = vr[i];
-            w = vc[i];
-            if (pf) {
-              const double ai = alpha_of(sh.u[a], qa1, qa2), ak = alpha_of(sh.pv.u[b], qa1, qa2);
-              v = v + ai * sh.pv.r0P[b];
-              v = v + (sh.pv.c0U[a] + ai * s00) * ak;
-              w = w + ak * sh.pv.r0U[a];
-              w = w + (sh.pv.c0P[b] + ak * s00) * ai;
-              if (sh.u[a] == sh.pv.u[b] && sh.u[a] < 3) {
-                v += A.q;
-                w += A.q;
-              }
-            }
-          }
-          sh.pv.R[a][b] = v;
-          sh.pv.C[b][a] = w;
-        }
-      }
-      __syncthreads();
-      EKF_STAMP(9);
-      // K' rows and M' columns: the previous chain's K / M where U' has the index, else rebuilt
-      // (R, C, Z', Y' are zero beyond |U'| and 2m', so the sums run unguarded; columns ≥ 2m' of
-      // K' / rows of M' are written as zeros for the same reason below)
-      for (int e = tid; e < nu * kZC; e += blockDim.x) {
-        const int a = e >> 5, c = e & (kZC - 1);
-        const int pos = d.cpos[a];
-        double kk = 0.0, mm = 0.0;
-        if (c < zc) {
-          if (pos >= 0) {
-            kk = sh.KU[c >> 1][pos][c & 1];
-            mm = sh.MU[c >> 1][pos][c & 1];
-          } else {
-            double k2 = 0.0, m2 = 0.0;
-#pragma unroll
-            for (int k = 0; k < kMaxU + 1; k += 2) {
-              kk = fma(sh.pv.R[a][k], sh.pv.Z[k][c], kk);
-              mm = fma(sh.pv.Y[c][k], sh.pv.C[k][a], mm);
-              if (k + 1 < kMaxU + 1) {
-                k2 = fma(sh.pv.R[a][k + 1], sh.pv.Z[k + 1][c], k2);
-                m2 = fma(sh.pv.Y[c][k + 1], sh.pv.C[k + 1][a], m2);
-              }
-            }
-            kk += k2;
-            mm += m2;
-          }
-        }
-        sh.pv.K[a][c] = kk;
-        sh.pv.M[c][a] = mm;
-      }
-      __syncthreads();
-    }
-    EKF_STAMP(10);
-    // Σ_in[U, U] and x[U]
-    for (int e = tid; e < kW * kW; e += blockDim.x) {
-      const int a = e / kW, b = e % kW;
-      if (a >= nu || b >= nu) continue;
-      const int pa = d.cpos[a], pb = d.cpos[b];
-      if (pa >= 0 && pb >= 0) {
-        sh.P[0][a][b] = sh.Pst[pa][pb];
-      } else {
-        double v = sh.P[0][a][b], w = 0.0;
-#pragma unroll
-        for (int c = 0; c < kZC; c += 2) {
-          v = fma(-sh.pv.K[a][c], sh.pv.M[c][b], v);
-          w = fma(-sh.pv.K[a][c + 1], sh.pv.M[c + 1][b], w);
-        }
-        sh.P[0][a][b] = v + w;
-      }
-    }
-    if (tid < nu) {
-      const int pos = d.cpos[tid];
-      double xv;
-      if (pos >= 0) {
-        xv = sh.pv.xU[pos];
-      } else {
-        double acc = 0.0;
-        for (int k = 0; k < np; ++k) acc = fma(sh.pv.R[tid][k], sh.pv.Zx[k], acc);
-        xv = sh.pv.xg[tid] + acc;
-      }
-      sh.xU[0][tid] = xv;
-    }
-    if (tid < 3) sh.xpose[tid] = sh.pv.xU[tid];  // pose ∈ U' always
-    __syncthreads();
-    EKF_STAMP(11);
-    if (tid == 192) {
-      if (pose_pre) {
-        for (int k = 0; k < 3; ++k) sh.pose[k] = sh.npose[k];
-        sh.a1 = sh.na1;
-        sh.a2 = sh.na2;
-      } else {
-        double a1, a2;
-        predicted_pose(sh.tmo, d, sh.xpose, sh.pose, &a1, &a2);
-        sh.a1 = a1;
-        sh.a2 = a2;
-      }
-    }
-    }
-  } else if (look) {
+  if (look) {
     // Σ_in[U,U] = Σ_pred'[U,U] − K'·M' with Σ_pred' = A'·Σ_in'·A'ᵀ + Q̄' (the previous chunk's
     // predict, if it had one), K'[a] = Σ_pred'[u_a, U']·Z', M'[:, b] = Y'·Σ_pred'[U', u_b]: the
     // factor kernel's formulas evaluated at U only.
@@ -746,8 +555,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
   EKF_STAMP(6);
   // ---- A3: x[U] pose, α, this chunk's predict folded in: P ← A P Aᵀ + Q̄ (slam.cpp:198) --------
-  // (done in the carry pass above when the pose was ready)
-  if (!(carry && d.nnew == 0 && pose_pre)) {
   __syncthreads();
   if (tid < nu) {
     if (tid < 3) sh.xU[0][tid] = sh.pose[tid];
@@ -769,8 +576,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
   }
   __syncthreads();
-  }
   EKF_STAMP(2);
+  EKF_DUMP_BLOCK(seq);
 
   // ---- A2: the m corrections -----------------------------------------------------------------
   // The dependent chain (ẑ, H, S⁻¹, ν → K, M, x → next marker) runs on wave 0 alone, with no
@@ -1031,13 +838,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
   } else if (wave == 1) {  // Z_c and Φ (live columns)
     const int hb = lane & 31, hr = lane >> 5;
-    // The record parity this chunk writes was last written two chunks back: the bulk stream must
-    // be done with it (its factor kernel and block scatter finish before that chunk's Σ-pass
-    // epoch). A carried chunk without new indices has not polled; the others' polls covered this.
-    // Z_c goes to the record as soon as it is computed (write-through, off the chain's path).
-    if (lane == 0 && carry && d.nnew == 0 && seq >= 2 &&
-        !epoch_wait_acquire(A.sync + kSyncSigma, seq - 1))
-      atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+    // The record parity this chunk writes was last written two chunks back: the prologue's poll
+    // (that chunk's Σ-pass epoch) has made the bulk stream done with it. Z_c goes to the record as
+    // soon as it is computed (write-through, off the chain's path).
     for (int e = lane; e < kMaxU * (kMaxU + 1); e += 64) {  // Φ = I
       const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
       (&sh.Phi[0][0][0])[e] = a == b ? 1.0 : 0.0;
@@ -1046,7 +849,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const __amdgpu_buffer_rsrc_t rr =
         __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
     constexpr int oZ = static_cast<int>(offsetof(ChunkRec, Z));
-    __syncwarp();  // the lane-0 wait above orders every lane's record stores below
     {  // columns ≥ 2m of the record's Z are zero (the factor kernel and a rebuilding chain read them)
       const int zw = kZC - 2 * m;
       for (int e = lane; e < kMaxU * zw; e += 64) {
@@ -1098,15 +900,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
   } else {  // wave 2: Y_c and Ψ (live rows); Y_c to the record as soon as it is computed
     const int ha = lane & 31, hr = lane >> 5;
-    if (lane == 0 && carry && d.nnew == 0 && seq >= 2 &&
-        !epoch_wait_acquire(A.sync + kSyncSigma, seq - 1))
-      atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
     for (int e = lane; e < kMaxU * (kMaxU + 1); e += 64) {  // Ψ = I
       const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
       (&sh.Psi[0][0][0])[e] = a == b ? 1.0 : 0.0;
     }
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
-    __syncwarp();
     for (int e = lane; e < (kZC - 2 * m) * kMaxU; e += 64)  // rows ≥ 2m of the record's Y are zero
       st_wt(&(&rec->Y[2 * m][0])[e], 0.0);
     for (int c = 0; c < m; ++c) {
@@ -1152,32 +950,26 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
   }
   __syncthreads();
-  // The last step's rank-2 term on the whole block (earlier steps are applied), written to Pst:
-  // the final Σ[U, U] is what the next chunk of this launch carries.
-  // fp32 Σ: the block also goes to the record (write-through) for the Σ pass's U × U entries.
-  {
+  // fp32 Σ: the last step's rank-2 term on the whole block (earlier steps are applied), the final
+  // Σ[U, U] in fp64, to the record (write-through) for k_pend_scatter (the Σ pass's U × U entries)
+  if constexpr (sizeof(T) == 4) {
     const int c = max(m - 1, 0);
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
-    for (int e = tid; e < kMaxU * (kMaxU + 1); e += blockDim.x) {
-      const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
+    for (int e = tid; e < kMaxU * kMaxU; e += blockDim.x) {
+      const int a = e / kMaxU, b = e - a * kMaxU;
       double v = sh.P[0][a][b];
-      const bool in = a < nu && b < nu;
-      if (m > 0 && in)
+      if (m > 0)
         v = rank2_sub(v, sh.KU[c][a][0], sh.KU[c][a][1], sh.MU[c][b][0], sh.MU[c][b][1]);
-      sh.Pst[a][b] = v;
-      if constexpr (sizeof(T) == 4) {
-        if (in) st_wt(&rec->Pend[a][b], v);
-      }
+      if (a < nu && b < nu) st_wt(&rec->Pend[a][b], v);
     }
   }
   __syncthreads();
   EKF_STAMP(12);
   // ---- epilogue -----------------------------------------------------------------------------
-  // Wave 3 (one lane): the posterior t_map_odom, then the next chunk's predicted pose from its
-  // descriptor. Waves 0–2 meanwhile prefetch that descriptor, store the record write-through and
-  // keep the carry. The record's epoch is published at the next chunk's start (or the kernel's
-  // end): the stores drain behind the next prologue instead of stalling this one. The record
-  // parity's release (the bulk stream done with it) was awaited by wave 1 before its steps, or by
+  // Wave 3 (one lane): the posterior t_map_odom. Waves 0–2 meanwhile prefetch the next chunk's
+  // descriptor and store the record write-through. The record's epoch is published at the next
+  // chunk's start (or the kernel's end): the stores drain behind the next prologue instead of
+  // stalling this one. The record parity's release (the bulk stream done with it) was awaited by
   // the prologue's poll.
   const double* xfin = sh.xU[0];
   const bool pre_next = ci + 1 < nchunks;
@@ -1189,18 +981,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         ctl->tmo[0] = tmo.theta;
         ctl->tmo[1] = tmo.x;
         ctl->tmo[2] = tmo.y;
-        sh.tmo[0] = tmo.theta;
-        sh.tmo[1] = tmo.x;
-        sh.tmo[2] = tmo.y;
-      }
-      if (pre_next) {
-        const MsgDesc& gnd = A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y];
-        if ((gnd.flags & kActive) && (gnd.flags & kLook)) {
-          double a1, a2;
-          predicted_pose(sh.tmo, gnd, xfin, sh.npose, &a1, &a2);
-          sh.na1 = a1;
-          sh.na2 = a2;
-        }
       }
     }
   } else {
@@ -1224,9 +1004,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       st_wt(&rec->row0raw[tid], in ? sh.row0raw[tid] : 0.0);
       st_wt(&rec->col0raw[tid], in ? sh.col0raw[tid] : 0.0);
       st_wt(&rec->xU[tid], in ? xfin[tid] : 0.0);
-      sh.pv.u[tid] = sh.u[tid];
-      sh.pv.xU[tid] = xfin[tid];
-      sh.pv.Zx[tid] = zx;
     }
     if (tid == 0) {
       st_wt(&rec->m, m);
@@ -1235,16 +1012,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       st_wt(&rec->a1, sh.a1);
       st_wt(&rec->a2, sh.a2);
       st_wt(&rec->s00, sh.s00);
-      sh.pv.nu = nu;
-      sh.pv.m = m;
-      sh.pv.first = first ? 1 : 0;
-      sh.pv.a1 = sh.a1;
-      sh.pv.a2 = sh.a2;
     }
     EKF_STAMP(16);
   }
   pending = seq + 1u;
-  have_carry = true;
   pre = pre_next;
   __syncthreads();
   EKF_STAMP(40);
@@ -1288,7 +1059,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
   const bool first = (d.flags & kFirst) != 0;
   // the chain of this chunk runs on the other stream: wait for its record
   if (tid < 64) sh.pos64[tid] = kMaxU;
-  if (tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
+  if (A.polls && tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
     atomicOr(&A.ctl[f].status, EKF_FLAG_TIMEOUT_D);
   drain_stores();
   __syncthreads();
@@ -1941,7 +1712,7 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, hipStre
   if constexpr (sizeof(T) == 4)
     hipLaunchKernelGGL(k_pend_scatter, dim3(nf), dim3(256), 0, s, a);
   // the pass's epoch (otherwise published by the next chunk's factor kernel, PassArgs::pub_sigma)
-  if (publish) hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
+  if (publish && a.polls) hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();
 }
 

@@ -30,6 +30,8 @@ struct PassArgs {
   unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
   unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
   unsigned pub_sigma;   // factors: publish this Σ-pass epoch first (the previous chunk's pass, 0 = none)
+  int polls;            // 1: the streams hand off through device epochs (kernels poll them);
+                        // 0: stream order / events order everything, no poll and no epoch kernel
   const MsgDesc* desc;
   int desc_stride;      // descriptors between consecutive chunks of a chain launch
   int n, ld, N, f0;

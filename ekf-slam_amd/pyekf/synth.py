@@ -13,9 +13,11 @@ same odometry + marker streams can be fed to the HIP path, the CPU oracle and th
   (nusim.cpp:317-346). ``basic_world`` reports every landmark with DELETE beyond ``max_range``
   (nusim.cpp:332-336); the large synthetic maps report the ``m`` nearest landmarks.
 * Populated maps ("one untimed warm-up pass that initializes every landmark"):
-  ``populated`` / ``swarm`` prefix the circle with a survey drive — an outward spiral with rings
-  ``ring`` m apart over the whole field — whose messages carry, of the landmarks within
-  ``max_range``, the not-yet-sighted ones first, then the nearest. Every landmark is sighted by the
+  ``populated`` / ``swarm`` prefix the circle with a survey drive — an inward spiral with rings
+  ``ring`` m apart over the whole field, ending on the unit circle at the field's centre — whose
+  messages carry, of the landmarks within
+  twice ``max_range`` (slip drifts the true path off the commanded spiral), the not-yet-sighted
+  ones first, then the nearest; never none (the nearest, if nothing is in range). Every landmark is sighted by the
   end of the survey (asserted). Landmarks are placed at least ``clearance`` m from the true path of
   the whole drive (range 0 is the reference's unguarded NaN, slam.cpp:241-249).
 
@@ -40,6 +42,7 @@ TRACK_WIDTH = 0.160
 
 # sensor modes per message
 SENSE_NEAREST, SENSE_SURVEY, SENSE_ALL = 0, 1, 2
+SURVEY_RANGE = 2.0  # survey messages sense out to this multiple of max_range
 # RNG streams
 _S_SLIP, _S_NOISE, _S_MAP, _S_SHUFFLE, _S_DELETE = 1, 2, 3, 4, 5
 
@@ -115,6 +118,7 @@ class Drive:
     ticks_per_msg: int
     tick_hz: float
     n_warm: int = 0
+    start_pose: tuple | None = None  # true (θ, x, y) at the first tick (None: the caller's)
 
 
 def circle_drive(n_messages: int, circle_radius=1.0, omega=0.5, tick_hz=200.0, ticks_per_msg=40,
@@ -124,27 +128,32 @@ def circle_drive(n_messages: int, circle_radius=1.0, omega=0.5, tick_hz=200.0, t
                  np.full(n_messages, sense, np.int32), ticks_per_msg, tick_hz)
 
 
-def survey_drive(half: float, n_messages: int, ring=4.0, v_survey=4.0, circle_radius=1.0,
-                 omega=0.5, tick_hz=200.0, ticks_per_msg=40) -> Drive:
-    """Outward spiral from the unit circle (radius growing ``ring`` m per turn, curvature 1/r, at
-    ``v_survey`` m/s) until it covers the [-half, half]² field, then ``n_messages`` of the circle
-    (radius ``circle_radius`` at ``omega``). The spiral's messages sense in survey mode."""
+def survey_drive(half: float, n_messages: int, ring=3.0, v_survey=4.0, circle_radius=1.0,
+                 omega=0.5, tick_hz=200.0, ticks_per_msg=40, max_range=5.0) -> Drive:
+    """Inward spiral over the [-half, half]² field (radius shrinking ``ring`` m per turn, curvature
+    1/r, at ``v_survey`` m/s) from the outer ring down to the unit circle, then ``n_messages`` of the
+    circle (radius ``circle_radius`` at ``omega``) around the field's centre. The robot starts on
+    the outer ring towards a corner, heading counter-clockwise (``Drive.start_pose``); the ring
+    passes each corner within ``max_range`` − 1 m while it shrinks over the first turn. The spiral's
+    messages sense in survey mode."""
     dt = 1.0 / tick_hz
-    r, v, w = circle_radius, [], []
-    r_max = max(half * math.sqrt(2.0), circle_radius + ring)
-    while r < r_max:
+    r_max = max(half * math.sqrt(2.0) - 0.5, circle_radius + ring)
+    phi0 = 0.25 * math.pi
+    r, v, w = r_max, [], []
+    while r > circle_radius:
         om = v_survey / r
         v.append(v_survey)
         w.append(om)
-        r += ring / (2.0 * math.pi) * om * dt
-    nw = -(-len(v) // ticks_per_msg)  # whole messages
+        r -= ring / (2.0 * math.pi) * om * dt
+    nw = -(-len(v) // ticks_per_msg)  # whole messages: pad with the unit circle at survey speed
     pad = nw * ticks_per_msg - len(v)
     v += [v_survey] * pad
-    w += [v_survey / r] * pad
+    w += [v_survey / circle_radius] * pad
     c = circle_drive(n_messages, circle_radius, omega, tick_hz, ticks_per_msg)
     sense = np.concatenate([np.full(nw, SENSE_SURVEY, np.int32), c.sense])
     return Drive(np.concatenate([np.array(v), c.v]), np.concatenate([np.array(w), c.w]), sense,
-                 ticks_per_msg, tick_hz, nw)
+                 ticks_per_msg, tick_hz, nw,
+                 start_pose=(phi0 + 0.5 * math.pi, r_max * math.cos(phi0), r_max * math.sin(phi0)))
 
 
 # ---- simulation ----------------------------------------------------------------------------------
@@ -247,9 +256,15 @@ def _sense(drive: Drive, seeds, landmarks, truth, max_markers, max_range, sensor
             k = np.full(F, L)
             a = np.where(dist <= max_range, ADD, DELETE)
         else:
-            key = np.where(dist <= max_range, dist, np.inf)
+            # the survey senses out to twice the range: slip drifts the true path off the
+            # commanded spiral by metres over a survey, and every landmark must still be sighted
+            rng = SURVEY_RANGE * max_range if mode == SENSE_SURVEY else max_range
+            key = np.where(dist <= rng, dist, np.inf)
             if mode == SENSE_SURVEY:
                 key = np.where(sighted & np.isfinite(key), key + 1e6, key)
+            if mode == SENSE_SURVEY:  # a survey message is never empty: the nearest, out of range
+                key = np.where(np.isfinite(key).any(1, keepdims=True), key,
+                               np.where(dist == dist.min(1, keepdims=True), dist, np.inf))
             sel = np.argsort(key, axis=1, kind="stable")[:, :m]
             k = np.count_nonzero(np.isfinite(np.take_along_axis(key, sel, 1)), axis=1)
             a = np.full((F, L), ADD)
@@ -326,6 +341,8 @@ def _generate(n_landmarks, drive: Drive, seeds, landmarks=None, half=None, *, ma
               shuffle=False, n_delete=0, clearance=0.3, n_map=None) -> Swarm:
     seeds = np.asarray(seeds, dtype=np.uint64).reshape(-1)
     F = seeds.shape[0]
+    if drive.start_pose is not None:
+        start_pose = drive.start_pose
     wheel, truth, path = _simulate(drive, seeds, start_pose, slip)
     if landmarks is None:
         landmarks = _place_landmarks(n_landmarks if n_map is None else n_map, half, seeds, path,
@@ -402,9 +419,10 @@ def swarm(n_landmarks: int, n_filters: int, n_messages: int, seed: int = 2024031
     every landmark (``Swarm.n_warm`` messages)."""
     n_map = kw.pop("n_map", n_landmarks)  # landmarks placed (≤ N slots; the rest stay free for
     half = field_half(n_map)               # the association path's new landmarks)
-    ring = kw.pop("ring", 4.0)
+    ring = kw.pop("ring", 3.0)
     v_survey = kw.pop("v_survey", 4.0)
-    drive = (survey_drive(half, n_messages, ring=ring, v_survey=v_survey) if survey else
+    drive = (survey_drive(half, n_messages, ring=ring, v_survey=v_survey,
+                          max_range=kw.get("max_range", 5.0)) if survey else
              circle_drive(n_messages))
     seeds = np.uint64(seed) + np.arange(n_filters, dtype=np.uint64)
     sw = _generate(n_landmarks, drive, seeds, half=half, max_markers=max_markers, n_map=n_map,

@@ -94,7 +94,10 @@ int ekf_sensor(ekf_t h, int filter, int m, const double* rel_xy, int* assoc_out,
 
 /* All filters of the handle at once, one message per filter (the swarm / replay path).
  * counts[F], ids/actions[F][m_max], rel_xy[F][m_max][2], odom[F][3] (t_odom_robot per filter,
- * NULL = keep). ids may be NULL with assoc=1 (unknown association). Asynchronous. */
+ * NULL = keep). ids may be NULL with assoc=1 (unknown association). Asynchronous.
+ * counts[f] == 0: filter f gets no message this step and nothing of it changes (as ekf_fake_sensor
+ * rejects an empty array, EKF_E_EMPTY: the reference throws at msg.markers.at(0), slam.cpp:281);
+ * a message whose markers are all DELETE is a predict + posterior (slam.cpp:205). */
 int ekf_batch_sensor(ekf_t h, int assoc, int m_max, const int* counts, const int* ids,
                      const int* actions, const double* rel_xy, const double* odom);
 

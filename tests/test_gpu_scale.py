@@ -10,8 +10,13 @@ that initialises every landmark), through the C-ABI, against the C oracle.
 * Association at scale: unknown ids against ≥ 256 known landmarks on the pipeline
   (slam.cpp:344-440), decisions exactly equal to the oracle's.
 
-Tolerances: fp64 poses 1e-8 and Σ 1e-8 absolute (as tests/test_gpu_parity.py); fp32 Σ: poses within
-2e-4 of the fp64 oracle. Measured errors go to gpurun_out/scale_errors.json.
+Tolerances: fp64 poses and state 1e-8; Σ 1e-7 absolute on populated maps (1e-14 of the 1e7 prior,
+slam.cpp:130). Every first sighting computes a landmark's variance as 1e7 − (1e7 − δ), so two
+faithful fp64 evaluation orders differ there by ~1e7·ε per sighting: the two CPU restatements
+(oracle/ekf_oracle.c literal dense (I − KH)Σ vs structured rank-2) already differ by 1.8e-8 in Σ
+on the N=256 populated drive (152 survey + 25 circle messages, 256 first sightings), so 1e-7 is
+5× that floor. fp32 Σ: poses within 2e-4 of the fp64 oracle. Measured errors go to
+gpurun_out/scale_errors.json.
 """
 import json
 import os
@@ -26,7 +31,7 @@ from pyekf import synth
 pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-8
-SIGMA_TOL = 1e-8
+SIGMA_TOL = 1e-7
 ERRORS = {}
 
 
@@ -89,6 +94,30 @@ def n1024():
     return sc, odom, ws
 
 
+def test_n1024_survey_schedules_bit_identical(n1024, monkeypatch):
+    """The first 160 survey messages (many first sightings against the 1e7 prior, heavy index
+    overlap between consecutive messages) in one persistent device-epoch replay, in the
+    event-synchronised schedule and on one stream: bit-identical states (a chain that carried its
+    own block from chunk to chunk instead of rebuilding it drifted from the HBM Σ here and went
+    non-finite)."""
+    sc, odom, _ = n1024
+    sl = slice(0, 160)
+    out = []
+    for env in ({"EKF_DEVSYNC": "1"}, {"EKF_DEVSYNC": "0"}, {"EKF_SERIAL": "1"}):
+        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        e = pyekf.EKF(n_landmarks=1024)
+        _replay(e, sl, sc, odom)
+        out.append(e.state())
+        assert e.status() == 0, env
+        e.close()
+    for x, S, c in out[1:]:
+        np.testing.assert_array_equal(x, out[0][0])
+        np.testing.assert_array_equal(S, out[0][1])
+
+
 def test_n1024_fp64_survey_against_oracle(n1024):
     """All 1 024 first sightings (the 1e7-prior cancellations) on the pipeline vs the oracle."""
     sc, odom, (x, S, tmo, cnt) = n1024
@@ -107,7 +136,8 @@ def test_n1024_fp64_survey_against_oracle(n1024):
     assert np.abs(S - Sr).max() < SIGMA_TOL
 
 
-@pytest.mark.parametrize("env", [{}, {"EKF_DEVSYNC": "1"}], ids=["events", "devsync"])
+@pytest.mark.parametrize("env", [{"EKF_DEVSYNC": "0"}, {"EKF_DEVSYNC": "1"}],
+                         ids=["events", "devsync"])
 def test_n1024_fp32_populated_against_oracle(n1024, env, monkeypatch):
     """configs[2]: fp32 Σ over 40 circle messages (640 corrections of a fully correlated 1 024-
     landmark map) from the fp64 survey's state, vs the fp64 oracle from the same state."""
@@ -135,7 +165,7 @@ def test_n1024_fp32_populated_against_oracle(n1024, env, monkeypatch):
     assert e.status() == 0
     e.close()
     xr, Sr, _, _ = ref.get()
-    ERRORS["n1024_fp32_" + ("devsync" if env else "events")] = {
+    ERRORS["n1024_fp32_" + ("devsync" if env["EKF_DEVSYNC"] == "1" else "events")] = {
         "pose": err, "state": float(np.abs(x32 - xr).max()),
         "sigma": float(np.abs(S32 - Sr).max())}
     assert err < 2e-4
