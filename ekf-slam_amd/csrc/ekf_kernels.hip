@@ -394,6 +394,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
     if (tid < 3) sh.tmo[tid] = tq;
     __syncthreads();
+    EKF_STAMP(21);
     // the previous predict on the gathered values: v + α_i·Σ[0][j] + (Σ[i][0] + α_i·Σ00)·α_j + Q̄;
     // R / C columns k ≥ |U'| up to 36 are zeroed (MFMA k padding)
     const bool pf = sh.pv.first != 0;

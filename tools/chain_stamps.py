@@ -14,7 +14,7 @@ from pyekf import synth  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 T = 40
-sc = synth.synthetic(N, T)
+sc = synth.synthetic(N, T) if os.environ.get("STAMPS_MAP") != "populated" else synth.populated(N, T)
 odom = pyekf.odometry(sc)
 e = pyekf.EKF(n_landmarks=N)
 e.replay(sc.count[:, None], sc.rel[:, None], odom[:, None], ids=sc.ids[:, None],
@@ -26,9 +26,11 @@ L.ekf_diag_stamps.argtypes = [C.c_void_p, C.c_int]
 assert L.ekf_diag_stamps(st, 256) == 0
 s = np.array(st[:], dtype=np.int64)
 t0 = s[0]
-names = {1: "A0", 8: "carry:pos", 9: "carry:gather", 10: "carry:K'M'", 11: "carry:P,x", 17: "fused: reads", 18: "fused: compute", 6: "A1 done",
-         2: "predict (steps start)", 12: "steps+final pass", 16: "epi: rec stores issued", 40: "carry copies"}
-for k in (1, 8, 9, 10, 11, 17, 18, 6, 2, 12, 16, 40):
+names = {1: "A0", 21: "kLook: gathers landed", 3: "kLook: R, C, D (prev predict)",
+         7: "kLook: K', M' tiles", 5: "kLook: x[U]", 6: "A1 done (P tiles)",
+         2: "predict (steps start)", 12: "steps+final pass", 16: "epi: rec stores issued",
+         40: "chunk end"}
+for k in (1, 21, 3, 7, 5, 6, 2, 12, 16, 40):
     print(f"{names[k]:24s} {s[k] - t0:8d}")
 m = int(sc.count[-1])
 steps = [s[64 + 8 * c] - t0 for c in range(m)]
