@@ -63,6 +63,11 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=20240317,
                    help="filter g (global index over ranks) uses seed + g (SURVEY.md §8d)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and parity legs")
+    p.add_argument("--inputs", choices=["auto", "host", "device"], default="auto",
+                   help="device: odometry, slip and the fake sensor simulated on the GPU inside the "
+                        "timed region, descriptors written there too (include/ekf_sim.h); host: "
+                        "marker arrays from pyekf.synth replayed through ekf_replay; auto: device "
+                        "for the fp64 swarm workloads, host otherwise")
     p.add_argument("--parity-messages", type=int, default=10)
     p.add_argument("--traffic", choices=["auto", "off"], default="auto",
                    help="auto: measure the Σ pass's HBM bytes with two rocprofv3 --pmc child runs")
@@ -328,23 +333,21 @@ def build_inputs(N, F, T, seed, m, rank):
     """SURVEY.md §8d inputs for this rank's F filters: global filter g = rank·F + f is seeded
     seed + g (its own map, slip and sensor noise); the survey warm-up (every landmark sighted)
     precedes T messages of the circle drive. N = 50 is configs[0]'s basic_world (4 landmarks,
-    every one in view, no survey needed)."""
+    every one in view, no survey needed). Returns the synth.Swarm (its drive, maps and the host
+    restatement of every marker) and the odometry."""
     from pyekf import synth
     import pyekf
     if N == 50:
-        scs = [synth.basic_world(T, seed=seed + rank * F + f) for f in range(F)]
-        M = max(s.ids.shape[1] for s in scs)
-        counts = np.stack([s.count for s in scs], 1)
-        ids = np.full((T, F, M), -1, np.int32)
-        act = np.zeros((T, F, M), np.int32)
-        rel = np.zeros((T, F, M, 2))
-        for f, s in enumerate(scs):
-            ids[:, f], act[:, f], rel[:, f] = s.ids, s.actions, s.rel
-        odo = pyekf.odometry(scs[0])
-        return 0, counts, ids, act, rel, np.repeat(odo[:, None], F, 1), 4
-    sw = synth.swarm(N, F, T, seed=seed + rank * F, max_markers=m)
+        drive = synth.circle_drive(T, 0.3, sense=synth.SENSE_ALL)
+        sw = synth._generate(50, drive, np.uint64(seed + rank * F) + np.arange(F, dtype=np.uint64),
+                             synth.BASIC_WORLD_LANDMARKS,
+                             start_pose=(synth.BASIC_WORLD_THETA0, 0.0, 0.0))
+        n_target = 4
+    else:
+        sw = synth.swarm(N, F, T, seed=seed + rank * F, max_markers=m)
+        n_target = N
     odo = pyekf.odometry(sw.scenario(0))  # encoders report the commanded drive: every filter's
-    return sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel, np.repeat(odo[:, None], F, 1), N
+    return sw, np.repeat(odo[:, None], F, 1), n_target
 
 
 def main(argv=None, backend=None):
@@ -383,15 +386,31 @@ def run(args, rank, world, local, backend=None):
     dtype = be.F32 if dt == "f32" else be.F64
     W, K = args.warmup, args.steps
     t_gen = time.perf_counter()
-    n_warm, counts, ids, act, rel, odom, n_init_target = build_inputs(
-        N, F, W + 2 * K, args.seed, m, rank)
+    sw, odom, n_init_target = build_inputs(N, F, W + 2 * K, args.seed, m, rank)
+    n_warm, counts, ids, act, rel = sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel
     t_gen = time.perf_counter() - t_gen
+    inputs = args.inputs
+    if inputs == "auto":
+        inputs = "device" if (F > 1 and dt == "f64" and backend is None) else "host"
+    if inputs == "device" and dt != "f64":
+        raise SystemExit("--inputs device: fp64 workloads (fp32 takes its survey on an fp64 handle)")
+    ekf = be.EKF(n_landmarks=N, n_filters=F, dtype=dtype, device=local)
+    sim = None
+    if inputs == "device":
+        import pyekf
+        tpm = sw.wheel.shape[1]
+        sim = pyekf.Sim(ekf, sw.landmarks, seed=int(args.seed), f0=rank * F, ticks_per_msg=tpm,
+                        max_markers=min(m, sw.landmarks.shape[1]), marker_stride=ids.shape[2],
+                        start_theta=sw.start_pose[0], start_x=sw.start_pose[1],
+                        start_y=sw.start_pose[2])
 
     def msgs(a, b, e=None):
+        if sim is not None and e is None:  # the GPU simulates, senses and plans these messages
+            sim.run(sw.cmd[a * tpm:b * tpm], sw.sense[a:b])
+            return
         sl = slice(a, b)
         (e or ekf).replay(counts[sl], rel[sl], odom[sl], ids=ids[sl], actions=act[sl])
 
-    ekf = be.EKF(n_landmarks=N, n_filters=F, dtype=dtype, device=local)
     # ---- untimed warm-up: the survey (every landmark initialised), then W messages ----
     # fp32 cannot take first sightings against the 1e7 prior (slam.cpp:130): the survey runs on an
     # fp64 handle whose state seeds the fp32 one
@@ -478,7 +497,10 @@ def run(args, rank, world, local, backend=None):
             "vs_baseline": None,
             "dtype": "f32" if dt == "f32" else "f64",
             "data": "synthetic (seeded map per filter, survey warm-up sighting every landmark, "
-                    "then the circle drive with a nusim-style fake sensor)",
+                    "then the circle drive with a nusim-style fake sensor)" + (
+                        "; odometry, slip and sensing simulated on the GPU inside the timed "
+                        "region (ekf_sim)" if inputs == "device" else
+                        "; host-generated markers replayed through ekf_replay"),
             "config": {"workload": args.workload, "baseline_config": cfgname,
                        "n_landmarks": N, "state_dim": n, "filters_per_gpu": F,
                        "filters_total": F * world, "markers_per_message": m,
@@ -488,6 +510,7 @@ def run(args, rank, world, local, backend=None):
                        "landmarks_initialised_target": n_init_target,
                        "status_flags_rank0": sorted(set(status)),
                        "host_input_generation_s": t_gen,
+                       "inputs": inputs,
                        "parallelism": f"independent filters x{world} ranks"},
             "roofline": {
                 "kernel": "k_sigma_pass", "bound": "hbm", "achieved": achieved,
@@ -539,6 +562,8 @@ def run(args, rank, world, local, backend=None):
             result["cpu_baseline"] = cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if sim is not None:
+        sim.close()
     ekf.close()
     if world > 1:
         dist.barrier()

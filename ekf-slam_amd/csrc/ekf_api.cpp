@@ -14,6 +14,7 @@
 
 #include "ekf.h"
 #include "ekf_device.hpp"
+#include "ekf_internal.hpp"
 #include "ekf_launch.hpp"
 #include "geom.hpp"
 
@@ -627,6 +628,65 @@ int load_batch(ekf_ctx* h, int assoc_mode, int m_max, const int* counts, const i
 bool valid(ekf_ctx* h, int f) { return h && f >= 0 && f < h->F; }
 
 }  // namespace
+
+namespace ekfslam {
+
+int handle_info(ekf_t h, HandleInfo* out) {
+  if (!h || !out) return EKF_E_ARG;
+  if (int rc = flush(h)) return rc;
+  hipSetDevice(h->cfg.device);
+  if (join_bulk(h)) return EKF_E_HIP;  // work enqueued on the main stream next sees the bulk's done
+  out->F = h->F;
+  out->N = h->cfg.n_landmarks;
+  out->n = h->n;
+  out->dtype = h->cfg.dtype;
+  out->device = h->cfg.device;
+  out->resident = h->resident;
+  out->rows = h->rows != nullptr && !h->resident;
+  out->stream = h->stream;
+  return EKF_OK;
+}
+
+int handle_parity(ekf_t h, int* parity) {
+  if (!h || !parity) return EKF_E_ARG;
+  for (int f = 0; f < h->F; ++f) parity[f] = h->parity[f];
+  return EKF_OK;
+}
+
+int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
+                    const int* parity_after) {
+  if (!h || T < 0 || !dd || !parity_after) return EKF_E_ARG;
+  hipSetDevice(h->cfg.device);
+  int rc = EKF_OK;
+  if (T > 0) {
+    if (h->resident) {
+      const PassArgs<double> a = args<double>(h, dd, 0);
+      rc = timed(h, 4, h->stream, [&](hipEvent_t e0, hipEvent_t e1) {
+        return launch_resident(a, dplan, T, 0, h->F, h->stream, e0, e1);
+      });
+    } else {
+      // the bulk stream reads these descriptors too (written on the main stream)
+      HIPCHK(hipEventRecord(h->ev_chain, h->stream));
+      HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
+      const size_t F = static_cast<size_t>(h->F);
+      if (h->devsync && !h->serial) {
+        rc = group(h, dd, 0, h->F, T, true, true);
+      } else {
+        for (int t = 0; t < T && !rc; ++t) rc = group(h, dd + t * F, 0, h->F, 1, true, t == 0);
+      }
+    }
+  }
+  for (int f = 0; f < h->F; ++f) {
+    h->parity[f] = parity_after[f];
+    h->pending[f] = 0;
+    h->prev_m[f] = -1;
+    h->last_desc[f] = -1;
+  }
+  return rc;
+}
+
+}  // namespace ekfslam
+
 
 extern "C" {
 

@@ -59,7 +59,7 @@ typedef unsigned u2 __attribute__((ext_vector_type(2)));
 // a voffset past the descriptor's num_records: the access is dropped (loads return 0); the range
 // check is on voffset, so rows past n (the SGPR offset) must use it too
 constexpr int kOOB = 0x7ffffff0;
-constexpr int kRW = 8;  // waves per workgroup (512 threads: 256 VGPRs per lane for the resident Σ)
+
 
 // The prefix of a MsgDesc the kernel reads (m … z), staged in LDS a block of plan entries at a time.
 struct alignas(16) ResMsg {
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
     __syncthreads();
     posterior_from(sh.gx[b][0], sh.gx[b][1], sh.gx[b][2]);
   };
-  int ncorr = 0;  // corrections so far (diagnostic stamps)
+  [[maybe_unused]] int ncorr = 0;  // corrections so far (diagnostic stamps)
   auto correct = [&](int j, double z0, double z1, bool noinit) __attribute__((always_inline)) {
     RS_STAMP(ncorr, 1);
     asm volatile("" : "+s"(wq));

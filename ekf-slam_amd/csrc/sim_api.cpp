@@ -1,0 +1,302 @@
+// Host side of include/ekf_sim.h: device buffers of the simulator, one run = one simulator launch
+// (which also writes the filter's descriptors) + the filter's launches over the run's messages.
+// The simulator runs on a stream of its own with double-buffered run buffers, so run r's
+// simulation overlaps run r−1's filter work; the host waits only for the simulation (it needs
+// each filter's final parity for the handle's host mirror).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "ekf.h"
+#include "ekf_device.hpp"
+#include "ekf_internal.hpp"
+#include "ekf_launch.hpp"
+#include "ekf_sim.h"
+#include "sim_launch.hpp"
+
+using namespace ekfslam;
+
+struct ekf_sim {
+  ekf_t h = nullptr;
+  ekf_sim_config cfg{};
+  HandleInfo info{};
+  int L = 0, m = 0;
+  long long tick = 0, msg = 0;  // global tick / message index of the next run
+  double* lm = nullptr;
+  unsigned* sighted = nullptr;
+  SimState* st = nullptr;
+  int* par = nullptr;
+  hipStream_t sst = nullptr;        // the simulator's stream
+  hipEvent_t ev_sim = nullptr;      // simulation of the current run done
+  hipEvent_t ev_done[2] = {nullptr, nullptr};  // filter work of the run that used buffer b done
+  int* host_par_pinned = nullptr;
+  int buf = 0;                      // run buffer of the next run
+  double* cmd[2] = {nullptr, nullptr};
+  int* sense[2] = {nullptr, nullptr};
+  size_t cap_ticks = 0, cap_msgs = 0;
+  MsgDesc* desc[2] = {nullptr, nullptr};
+  PlanEntry* plan = nullptr;
+  // record
+  int* ids = nullptr;
+  int* act = nullptr;
+  double* rel = nullptr;
+  int* cnt = nullptr;
+  double* truth = nullptr;
+  double* odom = nullptr;
+  int last_T = 0;
+  std::vector<int> host_par;
+};
+
+namespace {
+
+void free_run(ekf_sim* s) {
+  for (void* p : {static_cast<void*>(s->cmd[0]), static_cast<void*>(s->sense[0]),
+                  static_cast<void*>(s->desc[0]), static_cast<void*>(s->cmd[1]),
+                  static_cast<void*>(s->sense[1]), static_cast<void*>(s->desc[1]),
+                  static_cast<void*>(s->plan), static_cast<void*>(s->ids),
+                  static_cast<void*>(s->act), static_cast<void*>(s->rel),
+                  static_cast<void*>(s->cnt), static_cast<void*>(s->truth),
+                  static_cast<void*>(s->odom)})
+    if (p) hipFree(p);
+  for (int b = 0; b < 2; ++b) {
+    s->cmd[b] = nullptr;
+    s->sense[b] = nullptr;
+    s->desc[b] = nullptr;
+  }
+  s->plan = nullptr;
+  s->ids = s->act = s->cnt = nullptr;
+  s->rel = s->truth = s->odom = nullptr;
+  s->cap_ticks = s->cap_msgs = 0;
+}
+
+// run buffers for T messages (grown, never shrunk)
+int reserve(ekf_sim* s, int T) {
+  const size_t F = static_cast<size_t>(s->info.F), M = static_cast<size_t>(s->cfg.marker_stride);
+  const size_t ticks = static_cast<size_t>(T) * s->cfg.ticks_per_msg;
+  if (static_cast<size_t>(T) <= s->cap_msgs && ticks <= s->cap_ticks) return EKF_OK;
+  if (hipStreamSynchronize(s->info.stream) != hipSuccess ||
+      hipStreamSynchronize(s->sst) != hipSuccess)
+    return EKF_E_HIP;
+  free_run(s);
+  const size_t Tn = std::max<size_t>(T, 1);
+  const size_t tk = Tn * s->cfg.ticks_per_msg;
+  bool ok = hipMalloc(&s->plan, Tn * sizeof(PlanEntry)) == hipSuccess;
+  for (int b = 0; b < 2 && ok; ++b)
+    ok = hipMalloc(&s->cmd[b], tk * 2 * sizeof(double)) == hipSuccess &&
+         hipMalloc(&s->sense[b], Tn * sizeof(int)) == hipSuccess &&
+         hipMalloc(&s->desc[b], Tn * F * sizeof(MsgDesc)) == hipSuccess;
+  if (ok && s->cfg.record)
+    ok = hipMalloc(&s->ids, Tn * F * M * sizeof(int)) == hipSuccess &&
+         hipMalloc(&s->act, Tn * F * M * sizeof(int)) == hipSuccess &&
+         hipMalloc(&s->rel, Tn * F * M * 2 * sizeof(double)) == hipSuccess &&
+         hipMalloc(&s->cnt, Tn * F * sizeof(int)) == hipSuccess &&
+         hipMalloc(&s->truth, Tn * F * 3 * sizeof(double)) == hipSuccess &&
+         hipMalloc(&s->odom, Tn * 3 * sizeof(double)) == hipSuccess;
+  if (!ok) {
+    free_run(s);
+    return EKF_E_NOMEM;
+  }
+  s->cap_msgs = Tn;
+  s->cap_ticks = tk;
+  // the resident plan: one entry per message, every filter (off = t·F)
+  std::vector<PlanEntry> pe(Tn);
+  for (size_t t = 0; t < Tn; ++t) pe[t] = PlanEntry{static_cast<int>(t * F), 0, static_cast<int>(F), 0};
+  if (hipMemcpy(s->plan, pe.data(), Tn * sizeof(PlanEntry), hipMemcpyHostToDevice) != hipSuccess)
+    return EKF_E_HIP;
+  return EKF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void ekf_sim_config_default(ekf_sim_config* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->seed = 20240317ull;
+  c->ticks_per_msg = 40;
+  c->slip = 0.02;
+  c->sensor_sigma = 1e-3;
+  c->max_range = 5.0;
+  c->max_markers = 16;
+  c->marker_stride = 16;
+  c->wheel_radius = 0.033;
+  c->track_width = 0.160;
+  c->start_theta = -1.0;
+}
+
+int ekf_sim_create(ekf_sim_t* out, ekf_t filter, const ekf_sim_config* cfg, int n_map,
+                   const double* landmarks) {
+  if (!out || !filter || !cfg || n_map <= 0 || n_map > kSimMaxMap || !landmarks) return EKF_E_ARG;
+  *out = nullptr;
+  ekf_sim* s = new ekf_sim;
+  s->h = filter;
+  s->cfg = *cfg;
+  if (int rc = handle_info(filter, &s->info)) {
+    delete s;
+    return rc;
+  }
+  s->L = n_map;
+  s->m = std::min(cfg->max_markers, n_map);
+  if (n_map > s->info.N || cfg->ticks_per_msg <= 0 || s->m <= 0 || s->m > kMaxChunk ||
+      cfg->marker_stride < s->m || cfg->wheel_radius <= 0.0 || cfg->track_width <= 0.0 ||
+      cfg->ticks_per_msg > 64) {
+    delete s;
+    return EKF_E_ARG;
+  }
+  const size_t F = static_cast<size_t>(s->info.F), words = (n_map + 31) / 32;
+  hipSetDevice(s->info.device);
+  bool ok = hipMalloc(&s->lm, F * n_map * 2 * sizeof(double)) == hipSuccess &&
+            hipMalloc(&s->sighted, F * words * sizeof(unsigned)) == hipSuccess &&
+            hipMalloc(&s->st, F * sizeof(SimState)) == hipSuccess &&
+            hipMalloc(&s->par, F * sizeof(int)) == hipSuccess;
+  std::vector<SimState> st(F);
+  for (auto& v : st) {
+    std::memset(&v, 0, sizeof(v));
+    v.truth[0] = cfg->start_theta;
+    v.truth[1] = cfg->start_x;
+    v.truth[2] = cfg->start_y;
+  }
+  ok = ok && hipStreamCreateWithFlags(&s->sst, hipStreamNonBlocking) == hipSuccess &&
+       hipEventCreateWithFlags(&s->ev_sim, hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&s->ev_done[0], hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&s->ev_done[1], hipEventDisableTiming) == hipSuccess &&
+       hipHostMalloc(reinterpret_cast<void**>(&s->host_par_pinned), F * sizeof(int),
+                     hipHostMallocDefault) == hipSuccess &&
+       hipEventRecord(s->ev_done[0], s->info.stream) == hipSuccess &&
+       hipEventRecord(s->ev_done[1], s->info.stream) == hipSuccess &&
+       hipMemcpy(s->lm, landmarks, F * n_map * 2 * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+       hipMemset(s->sighted, 0, F * words * sizeof(unsigned)) == hipSuccess &&
+       hipMemcpy(s->st, st.data(), F * sizeof(SimState), hipMemcpyHostToDevice) == hipSuccess;
+  if (!ok) {
+    ekf_sim_destroy(s);
+    return EKF_E_NOMEM;
+  }
+  s->host_par.assign(F, 0);
+  *out = s;
+  return EKF_OK;
+}
+
+int ekf_sim_destroy(ekf_sim_t s) {
+  if (!s) return EKF_E_ARG;
+  if (s->info.stream) hipStreamSynchronize(s->info.stream);
+  if (s->sst) hipStreamSynchronize(s->sst);
+  free_run(s);
+  for (void* p : {static_cast<void*>(s->lm), static_cast<void*>(s->sighted),
+                  static_cast<void*>(s->st), static_cast<void*>(s->par)})
+    if (p) hipFree(p);
+  if (s->host_par_pinned) hipHostFree(s->host_par_pinned);
+  for (hipEvent_t e : {s->ev_sim, s->ev_done[0], s->ev_done[1]})
+    if (e) hipEventDestroy(e);
+  if (s->sst) hipStreamDestroy(s->sst);
+  delete s;
+  return EKF_OK;
+}
+
+int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
+  if (!s || T < 0 || (T > 0 && !wheel_cmd)) return EKF_E_ARG;
+  if (T == 0) return EKF_OK;
+  if (sense)
+    for (int t = 0; t < T; ++t) {
+      if (sense[t] < EKF_SENSE_NEAREST || sense[t] > EKF_SENSE_ALL) return EKF_E_ARG;
+      if (sense[t] == EKF_SENSE_ALL && (s->L > kMaxChunk || s->cfg.marker_stride < s->L))
+        return EKF_E_ARG;
+    }
+  if (int rc = handle_info(s->h, &s->info)) return rc;  // host-planned work first, bulk joined
+  hipSetDevice(s->info.device);
+  if (int rc = reserve(s, T)) return rc;
+  const int b = s->buf;
+  s->buf ^= 1;
+  const hipStream_t st = s->sst;
+  const size_t F = static_cast<size_t>(s->info.F);
+  const size_t ticks = static_cast<size_t>(T) * s->cfg.ticks_per_msg;
+  // the handle's host mirror is authoritative (host-planned calls between runs flip parities)
+  if (int rc = handle_parity(s->h, s->host_par.data())) return rc;
+  std::memcpy(s->host_par_pinned, s->host_par.data(), F * sizeof(int));
+  if (hipMemcpyAsync(s->par, s->host_par_pinned, F * sizeof(int), hipMemcpyHostToDevice, st) !=
+      hipSuccess)
+    return EKF_E_HIP;
+  // buffer b was last read by the filter work of the run before the previous one
+  if (hipStreamWaitEvent(st, s->ev_done[b], 0) != hipSuccess) return EKF_E_HIP;
+  if (hipMemcpyAsync(s->cmd[b], wheel_cmd, ticks * 2 * sizeof(double), hipMemcpyHostToDevice, st) !=
+      hipSuccess)
+    return EKF_E_HIP;
+  if (sense && hipMemcpyAsync(s->sense[b], sense, T * sizeof(int), hipMemcpyHostToDevice, st) !=
+                   hipSuccess)
+    return EKF_E_HIP;
+  SimArgs a{};
+  a.cmd = s->cmd[b];
+  a.sense = sense ? s->sense[b] : nullptr;
+  a.lm = s->lm;
+  a.sighted = s->sighted;
+  a.st = s->st;
+  a.par = s->par;
+  a.desc = s->desc[b];
+  if (s->cfg.record) {
+    a.out_ids = s->ids;
+    a.out_act = s->act;
+    a.out_rel = s->rel;
+    a.out_cnt = s->cnt;
+    a.out_truth = s->truth;
+    a.out_odom = s->odom;
+  }
+  a.seed = s->cfg.seed;
+  a.tick0 = s->tick;
+  a.msg0 = s->msg;
+  a.f0 = s->cfg.f0;
+  a.F = s->info.F;
+  a.L = s->L;
+  a.T = T;
+  a.tpm = s->cfg.ticks_per_msg;
+  a.m = s->m;
+  a.M = s->cfg.marker_stride;
+  a.N = s->info.N;
+  a.rows = s->info.rows ? 1 : 0;
+  a.slip = s->cfg.slip;
+  a.sigma = s->cfg.sensor_sigma;
+  a.range = s->cfg.max_range;
+  a.radius = s->cfg.wheel_radius;
+  a.track = s->cfg.track_width;
+  if (launch_sim(a, st) != hipSuccess) return EKF_E_HIP;
+  // each filter's final parity (its inactive messages do not flip it): the host mirror
+  if (hipMemcpyAsync(s->host_par_pinned, s->par, F * sizeof(int), hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipEventRecord(s->ev_sim, st) != hipSuccess || hipEventSynchronize(s->ev_sim) != hipSuccess)
+    return EKF_E_HIP;
+  std::memcpy(s->host_par.data(), s->host_par_pinned, F * sizeof(int));
+  s->tick += static_cast<long long>(ticks);
+  s->msg += T;
+  s->last_T = T;
+  // the filter's kernels behind the simulation (their descriptors), then release buffer b
+  if (hipStreamWaitEvent(s->info.stream, s->ev_sim, 0) != hipSuccess) return EKF_E_HIP;
+  const int rc = run_device_plan(s->h, s->desc[b], s->plan, T, s->host_par.data());
+  if (rc) return rc;
+  if (int r2 = handle_info(s->h, &s->info)) return r2;  // joins the bulk stream into main
+  return hipEventRecord(s->ev_done[b], s->info.stream) == hipSuccess ? EKF_OK : EKF_E_HIP;
+}
+
+int ekf_sim_markers(ekf_sim_t s, int* counts, int* ids, int* actions, double* rel_xy) {
+  if (!s || !s->cfg.record) return EKF_E_ARG;
+  const size_t n = static_cast<size_t>(s->last_T) * s->info.F, M = s->cfg.marker_stride;
+  if (hipStreamSynchronize(s->info.stream) != hipSuccess) return EKF_E_HIP;
+  if ((counts && hipMemcpy(counts, s->cnt, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (ids && hipMemcpy(ids, s->ids, n * M * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (actions && hipMemcpy(actions, s->act, n * M * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (rel_xy && hipMemcpy(rel_xy, s->rel, n * M * 2 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
+    return EKF_E_HIP;
+  return EKF_OK;
+}
+
+int ekf_sim_poses(ekf_sim_t s, double* odom, double* truth) {
+  if (!s || !s->cfg.record) return EKF_E_ARG;
+  const size_t T = static_cast<size_t>(s->last_T);
+  if (hipStreamSynchronize(s->info.stream) != hipSuccess) return EKF_E_HIP;
+  if ((odom && hipMemcpy(odom, s->odom, T * 3 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (truth && hipMemcpy(truth, s->truth, T * s->info.F * 3 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
+    return EKF_E_HIP;
+  return EKF_OK;
+}
+
+}  // extern "C"

@@ -1,4 +1,5 @@
-"""ctypes binding of libekfslam.so (include/ekf.h, include/slam_core.h, include/landmarks.h).
+"""ctypes binding of libekfslam.so (include/ekf.h, include/slam_core.h, include/landmarks.h,
+include/ekf_sim.h).
 
 The binding is plumbing for tests and bench.py; the product is the C-ABI library. Loading fails
 loudly when the HIP library has not been built — there is no CPU fallback anywhere in this package.
@@ -36,13 +37,25 @@ EXPORTS = [
     "slam_odom", "slam_map_odom", "slam_filter", "slam_replay", "slam_integrate_odometry",
     "lm_create", "lm_destroy", "lm_detect", "lm_fit_circles", "lm_check_circles",
     "lm_last_kernel_us",
+    "ekf_sim_config_default", "ekf_sim_create", "ekf_sim_destroy", "ekf_sim_run",
+    "ekf_sim_markers", "ekf_sim_poses",
 ]
+SENSE_NEAREST, SENSE_SURVEY, SENSE_ALL = 0, 1, 2
 
 
 class EkfError(RuntimeError):
     def __init__(self, rc: int, what: str = ""):
         self.rc = rc
         super().__init__(f"{what}: {lib().ekf_strerror(rc).decode()} ({rc})")
+
+
+class SimConfig(C.Structure):
+    _fields_ = [("seed", C.c_ulonglong), ("f0", C.c_int), ("ticks_per_msg", C.c_int),
+                ("slip", C.c_double), ("sensor_sigma", C.c_double), ("max_range", C.c_double),
+                ("max_markers", C.c_int), ("marker_stride", C.c_int),
+                ("wheel_radius", C.c_double), ("track_width", C.c_double),
+                ("start_theta", C.c_double), ("start_x", C.c_double), ("start_y", C.c_double),
+                ("record", C.c_int)]
 
 
 class Config(C.Structure):
@@ -109,6 +122,12 @@ def lib():
             "lm_fit_circles": (_i, [_vp, _i, _vp, _vp, _vp]),
             "lm_check_circles": (_i, [_vp, _i, _vp, _vp, _vp]),
             "lm_last_kernel_us": (_i, [_vp, _dp]),
+            "ekf_sim_config_default": (None, [C.POINTER(SimConfig)]),
+            "ekf_sim_create": (_i, [C.POINTER(_vp), _vp, C.POINTER(SimConfig), _i, _vp]),
+            "ekf_sim_destroy": (_i, [_vp]),
+            "ekf_sim_run": (_i, [_vp, _i, _vp, _vp]),
+            "ekf_sim_markers": (_i, [_vp, _vp, _vp, _vp, _vp]),
+            "ekf_sim_poses": (_i, [_vp, _vp, _vp]),
         }
         for name, (res, argt) in sig.items():
             fn = getattr(L, name)
@@ -356,6 +375,63 @@ class Slam:
         rc = lib().slam_replay(self.h, T, ticks, _ptr(wheel), M, _ptr(counts), _ptr(ids),
                                _ptr(act), _ptr(rel), _ptr(out_p), _ptr(out_t))
         return rc, out_p, out_t
+
+
+class Sim:
+    """ekf_sim_t: on-device Monte-Carlo inputs for an EKF handle (include/ekf_sim.h)."""
+
+    def __init__(self, ekf, landmarks, **cfg):
+        c = SimConfig()
+        lib().ekf_sim_config_default(C.byref(c))
+        for k, v in cfg.items():
+            setattr(c, k, v)
+        self.cfg = c
+        self.F = ekf.F
+        lm = _f64(np.broadcast_to(np.asarray(landmarks, np.float64),
+                                  (ekf.F,) + np.shape(landmarks)[-2:]))
+        self.L = lm.shape[1]
+        self.h = C.c_void_p()
+        _check(lib().ekf_sim_create(C.byref(self.h), ekf.h, C.byref(c), self.L, _ptr(lm)),
+               "ekf_sim_create")
+        self.T = 0
+
+    def run(self, wheel_cmd, sense=None):
+        """wheel_cmd[T·ticks][2] commanded wheel increments per tick; sense[T] or None."""
+        cmd = _f64(wheel_cmd).reshape(-1, 2)
+        T = cmd.shape[0] // self.cfg.ticks_per_msg
+        sn = None if sense is None else _i32(sense)
+        _check(lib().ekf_sim_run(self.h, T, _ptr(cmd), _ptr(sn)), "ekf_sim_run")
+        self.T = T
+
+    def markers(self):
+        """The last run's inputs as ekf_replay takes them: counts [T,F], ids/actions [T,F,M],
+        rel [T,F,M,2]."""
+        T, F, M = self.T, self.F, self.cfg.marker_stride
+        cnt = np.zeros((T, F), np.int32)
+        ids = np.zeros((T, F, M), np.int32)
+        act = np.zeros((T, F, M), np.int32)
+        rel = np.zeros((T, F, M, 2))
+        _check(lib().ekf_sim_markers(self.h, _ptr(cnt), _ptr(ids), _ptr(act), _ptr(rel)),
+               "ekf_sim_markers")
+        return cnt, ids, act, rel
+
+    def poses(self):
+        """(odom [T, 3], truth [T, F, 3]) of the last run."""
+        odom = np.zeros((self.T, 3))
+        truth = np.zeros((self.T, self.F, 3))
+        _check(lib().ekf_sim_poses(self.h, _ptr(odom), _ptr(truth)), "ekf_sim_poses")
+        return odom, truth
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().ekf_sim_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def poison_lds(device=0):

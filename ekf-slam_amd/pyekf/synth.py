@@ -7,8 +7,9 @@ same odometry + marker streams can be fed to the HIP path, the CPU oracle and th
 * The robot follows a commanded (v, ω) schedule sampled at ``tick_hz`` joint-state ticks; the
   sensor fires every ``ticks_per_msg`` ticks (5 Hz at 200 Hz ticks, nusim.cpp:72,89). The basic
   drive is a circle (nuturtle_control/src/circle.cpp:85-86: v = ω·r).
-* True wheel angles carry multiplicative slip noise U(-slip, slip) (nusim.cpp:224-227); the encoders
-  report the commanded angles, so odometry drifts from the truth and the EKF has work to do.
+* True wheel angles carry multiplicative slip noise U(-slip, slip) (nusim.cpp:224-227) and the true
+  pose is DiffDrive::FKin of them (nusim.cpp:230); the encoders report the commanded angles, so
+  odometry drifts from the truth and the EKF has work to do.
 * Each message carries landmark positions in the true body frame plus N(0, σ²) noise on x and y
   (nusim.cpp:317-346). ``basic_world`` reports every landmark with DELETE beyond ``max_range``
   (nusim.cpp:332-336); the large synthetic maps report the ``m`` nearest landmarks.
@@ -157,20 +158,39 @@ def survey_drive(half: float, n_messages: int, ring=3.0, v_survey=4.0, circle_ra
 
 
 # ---- simulation ----------------------------------------------------------------------------------
-def _se2_step(th, x, y, omega, vx):
-    """Exact arc integration of a body twist (the kinematics of turtlelib integrate_twist),
-    vectorised over filters."""
-    small = omega == 0.0
-    om = np.where(small, 1.0, omega)
-    dx = np.where(small, vx, vx / om * np.sin(omega))
-    dy = np.where(small, 0.0, vx / om * (1.0 - np.cos(omega)))
-    c, s = np.cos(th), np.sin(th)
-    return th + omega, x + c * dx - s * dy, y + s * dx + c * dy
+def _compose(a, b):
+    """geom.hpp compose (turtlelib Transform2D ``*``, se2d.cpp:57-75), vectorised; a, b = (θ, x, y)."""
+    c, s = np.cos(a[0]), np.sin(a[0])
+    return a[0] + b[0], c * b[1] - s * b[2] + a[1], s * b[1] + c * b[2] + a[2]
+
+
+def _inverse(t):
+    c, s = np.cos(t[0]), np.sin(t[0])
+    return -t[0], -t[1] * c - t[2] * s, -t[2] * c + t[1] * s
+
+
+def _fkin_step(config, dl, dr, radius=WHEEL_RADIUS, track=TRACK_WIDTH):
+    """One DiffDrive::FKin update (diff_drive.cpp:10-28, geom.hpp DiffDrive::fkin) for wheel-angle
+    increments (dl, dr): body twist → integrate_twist (se2d.cpp:127-138) → config · Δ."""
+    om = radius / track * (-dl + dr)
+    vx = radius / 2.0 * (dl + dr)
+    zero = om == 0.0
+    w = np.where(zero, 1.0, om)
+    tsb = (np.zeros_like(om), 0.0 / w, -vx / w)
+    d = _compose(_compose(_inverse(tsb), (w, np.zeros_like(om), np.zeros_like(om))), tsb)
+    d = (np.where(zero, 0.0, d[0]), np.where(zero, vx, d[1]), np.where(zero, 0.0, d[2]))
+    return _compose(config, d)
 
 
 def _simulate(drive: Drive, seeds: np.ndarray, start_pose, slip: float):
-    """True poses of F filters (slip per filter) → (wheel [T, ticks, 2] encoder angles shared by
-    all filters, truth [F, T, 3] at the messages, path [F, ticks_total, 2] positions)."""
+    """True poses of F filters → (wheel [T, ticks, 2] encoder angles shared by all filters,
+    truth [F, T, 3] at the messages, path [F, ticks_total, 2] positions).
+
+    nusim's timer (nusim.cpp:222-230): each tick a wheel turns by its commanded increment ×
+    (1 + U(−slip, slip)), and the true pose is DiffDrive::FKin of the accumulated true wheel angles
+    from the start pose. The encoders here report the commanded angles (nusim reports the slipped
+    ones), so odometry drifts from the truth and the filter has work to do. The device simulator
+    (ekf-slam_amd/csrc/sim_kernels.hip) runs the same arithmetic, draw for draw."""
     F = seeds.shape[0]
     nt = drive.v.shape[0]
     tpm = drive.ticks_per_msg
@@ -184,20 +204,22 @@ def _simulate(drive: Drive, seeds: np.ndarray, start_pose, slip: float):
     u = rng_uniform(seeds[:, None, None], _S_SLIP,
                     (k[None, :, None] * np.uint64(2) + np.arange(2, dtype=np.uint64)))
     slipped = cmd[None] * (1.0 + slip * (2.0 * u - 1.0))                # [F, nt, 2]
-    om_all = WHEEL_RADIUS / TRACK_WIDTH * (-slipped[..., 0] + slipped[..., 1])
-    vx_all = WHEEL_RADIUS / 2.0 * (slipped[..., 0] + slipped[..., 1])
-    th = np.full(F, float(start_pose[0]))
-    x = np.full(F, float(start_pose[1]))
-    y = np.full(F, float(start_pose[2]))
+    config = (np.full(F, float(start_pose[0])), np.full(F, float(start_pose[1])),
+              np.full(F, float(start_pose[2])))
+    phi_l = np.zeros(F)
+    phi_r = np.zeros(F)
     path = np.zeros((F, nt, 2))
     truth = np.zeros((F, T, 3))
     for i in range(nt):
-        th, x, y = _se2_step(th, x, y, om_all[:, i], vx_all[:, i])
-        path[:, i, 0] = x
-        path[:, i, 1] = y
+        nl = phi_l + slipped[:, i, 0]
+        nr = phi_r + slipped[:, i, 1]
+        config = _fkin_step(config, nl - phi_l, nr - phi_r)
+        phi_l, phi_r = nl, nr
+        path[:, i, 0] = config[1]
+        path[:, i, 1] = config[2]
         if (i + 1) % tpm == 0:
             t = (i + 1) // tpm - 1
-            truth[:, t, 0], truth[:, t, 1], truth[:, t, 2] = th, x, y
+            truth[:, t, 0], truth[:, t, 1], truth[:, t, 2] = config
     return wheel, truth, path
 
 
@@ -320,6 +342,9 @@ class Swarm:
     truth: np.ndarray        # [T, F, 3]
     n_warm: int = 0
     sighted: np.ndarray = field(default=None, repr=False)  # [F, L] by the survey's end
+    cmd: np.ndarray = field(default=None, repr=False)      # [T·ticks, 2] commanded wheel increments
+    sense: np.ndarray = field(default=None, repr=False)    # [T] SENSE_* per message
+    start_pose: tuple = (0.0, 0.0, -1.0)                   # true (θ, x, y) at the first tick
 
     @property
     def n_filters(self) -> int:
@@ -344,6 +369,11 @@ def _generate(n_landmarks, drive: Drive, seeds, landmarks=None, half=None, *, ma
     if drive.start_pose is not None:
         start_pose = drive.start_pose
     wheel, truth, path = _simulate(drive, seeds, start_pose, slip)
+    tpm = drive.ticks_per_msg
+    dt = 1.0 / drive.tick_hz
+    cmd = np.stack([(drive.v - drive.w * TRACK_WIDTH / 2.0) / WHEEL_RADIUS * dt,
+                    (drive.v + drive.w * TRACK_WIDTH / 2.0) / WHEEL_RADIUS * dt], 1)
+    cmd = cmd[:(drive.v.shape[0] // tpm) * tpm]
     if landmarks is None:
         landmarks = _place_landmarks(n_landmarks if n_map is None else n_map, half, seeds, path,
                                      clearance)
@@ -354,7 +384,8 @@ def _generate(n_landmarks, drive: Drive, seeds, landmarks=None, half=None, *, ma
     ids, act, rel, cnt, sighted = _sense(drive, seeds, landmarks, truth, max_markers, max_range,
                                          sensor_sigma, shuffle, n_delete, n_landmarks)
     return Swarm(n_landmarks, seeds, landmarks, wheel, ids, act, rel, cnt,
-                 np.ascontiguousarray(truth.transpose(1, 0, 2)), drive.n_warm, sighted)
+                 np.ascontiguousarray(truth.transpose(1, 0, 2)), drive.n_warm, sighted, cmd,
+                 drive.sense.copy(), tuple(float(v) for v in start_pose))
 
 
 def make_scenario(n_landmarks: int, landmarks: np.ndarray, n_messages: int, *,

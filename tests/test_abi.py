@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared():
     names = set()
-    for h in ("ekf.h", "slam_core.h", "landmarks.h"):
+    for h in ("ekf.h", "slam_core.h", "landmarks.h", "ekf_sim.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b((?:ekf|slam|lm)_\w+)\s*\(",

@@ -122,8 +122,8 @@ def test_bench_run_gloo_world2():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import bench
     N, _, F, m, _ = TINY
-    n_warm, counts, ids, act, rel, odom, _ = bench.build_inputs(N, 2 * F, 2 + 2 * 3, 20240317,
-                                                                m, 0)
+    sw, odom, _ = bench.build_inputs(N, 2 * F, 2 + 2 * 3, 20240317, m, 0)
+    n_warm, counts, ids, act, rel = sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel
     ref = OracleSwarm(N, 2 * F)
     ref.replay(counts[:n_warm + 2 + 3], rel[:n_warm + 5], odom[:n_warm + 5], ids=ids[:n_warm + 5],
                actions=act[:n_warm + 5])
