@@ -59,7 +59,7 @@ struct ekf_ctx {
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
   bool defer = false;            // ekf_defer: plan now, upload and launch later
-  bool joseph = false;           // ekf_set_joseph (resident path)
+  bool joseph = false;           // ekf_set_joseph (resident: its own kernel; pipeline: kJoseph chunks)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
   hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
   bool devsync = false;                   // streams synchronise through device epochs
@@ -331,9 +331,13 @@ int ucol(const int* ids, int a, int N) {
 // absent[k] (batch paths): filter f0+k receives no message this step — its descriptor is inactive,
 // nothing of it changes (an empty MarkerArray is rejected before anything changes, EKF_E_EMPTY).
 void plan_known(ekf_ctx* h, int f0, int nf, bool predict, const char* absent = nullptr) {
+  // Joseph form on the pipeline: one marker per chunk (the factors then need no column recursion
+  // of the (ΣHᵀ − K·S)·Kᵀ term, k_chain)
+  const bool jos = h->joseph && !h->resident;
+  const int cm = jos ? 1 : kMaxChunk;
   int chunks = 1;
   for (int k = 0; k < nf; ++k)
-    chunks = std::max(chunks, static_cast<int>((h->msgs[k].size() + kMaxChunk - 1) / kMaxChunk));
+    chunks = std::max(chunks, static_cast<int>((h->msgs[k].size() + cm - 1) / cm));
   for (int chunk = 0; chunk < chunks; ++chunk) {
     const size_t off = h->plan_d.size();
     h->plan_d.resize(off + nf);
@@ -341,15 +345,15 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict, const char* absent = n
     for (int k = 0; k < nf; ++k) {
       const int f = f0 + k;
       const auto& mk = h->msgs[k];
-      const int nchunks = std::max(1, static_cast<int>((mk.size() + kMaxChunk - 1) / kMaxChunk));
+      const int nchunks = std::max(1, static_cast<int>((mk.size() + cm - 1) / cm));
       MsgDesc* d = &h->plan_d[off + k];
       if (chunk >= nchunks || (absent && absent[k])) {
         std::memset(d, 0, sizeof(MsgDesc));
         continue;
       }
-      const int b = chunk * kMaxChunk;
-      const int m = std::max(0, std::min(kMaxChunk, static_cast<int>(mk.size()) - b));
-      int flags = kActive;
+      const int b = chunk * cm;
+      const int m = std::max(0, std::min(cm, static_cast<int>(mk.size()) - b));
+      int flags = kActive | (jos ? kJoseph : 0);
       if (chunk == 0 && (predict || h->pending[f])) flags |= kFirst;
       if (chunk == nchunks - 1 && predict) flags |= kLast;
       // rebuild from the chunk before (its Σ pass may run); the resident kernel carries Σ itself
@@ -375,7 +379,7 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict, const char* absent = n
       h->prev_m[f] = m;
       for (int i = 0; i < m; ++i) h->prev_ids[f][i] = mk[b + i].id;
       h->parity[f] ^= 1;
-      kw = std::max(kw, ((2 + 2 * m + 3) / 4) * 4);
+      kw = std::max(kw, ((2 + (jos ? 4 : 2) * m + 3) / 4) * 4);
       if (chunk == 0) h->pending[f] = 0;
     }
     h->plan_l.push_back(Launch{0, off, f0, nf, kw});
@@ -399,7 +403,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
         std::memset(d, 0, sizeof(MsgDesc));
         continue;
       }
-      int flags = kActive | kNoInit;
+      int flags = kActive | kNoInit | (h->joseph && !h->resident ? kJoseph : 0);
       h->prev_m[f] = -1;  // association chunks run unpipelined
       h->last_desc[f] = -1;
       if (i == 0 && (predict || h->pending[f])) flags |= kFirst;
@@ -1025,8 +1029,7 @@ int ekf_sync(ekf_t h) {
 
 int ekf_set_joseph(ekf_t h, int on) {
   if (!h) return EKF_E_ARG;
-  if (on && !h->resident) return EKF_E_ARG;  // the pipeline's low-rank factors: simple form only
-  if (int rc = flush(h)) return rc;           // what is planned runs with the form it was planned in
+  if (int rc = flush(h)) return rc;  // what is planned runs with the form it was planned in
   h->joseph = on != 0;
   return EKF_OK;
 }

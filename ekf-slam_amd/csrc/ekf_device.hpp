@@ -34,6 +34,8 @@ constexpr int kRowsOut = 32; // Σ pass (fp64): also write Σ_out[i, U_next] to 
 constexpr int kRowsIn = 64;  // factor kernel: r(i) = Σ_in[i, U] from the rows buffer (written
                              // by the previous chunk's Σ pass) instead of a strided gather
 constexpr int kRowW = kMaxU + 1;  // rows buffer: kRowW × ldk per filter (position-major)
+constexpr int kJoseph = 128; // Joseph-form Σ update (ekf_set_joseph): one marker per chunk, the
+                             // factor rank 2 + 4 (K·M and (ΣHᵀ − K·S)·Kᵀ, see k_chain)
 
 // One chunk of one message for one filter (uploaded by the host, read by every kernel of the pair).
 struct alignas(16) MsgDesc {

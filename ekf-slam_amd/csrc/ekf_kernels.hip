@@ -137,10 +137,12 @@ struct ChainShared {
   double nu[kMaxChunk][2];
   double Hs[kMaxChunk][2][5];    // H_c over pA (published for waves 1–2)
   double Sis[kMaxChunk][4];      // S_c⁻¹
+  double GU[kMaxU][2];           // Joseph (one marker per chunk): (Σ·Hᵀ)[U] of the step
+  double Ss[4];                  // Joseph: S of the step
   // kLook: the previous chunk's record and the blocks rebuilt from it
   struct {
     int u[kMaxU];
-    int nu, m, first;
+    int nu, m, first, joseph;
     double a1, a2, s00;
     double xU[kMaxU], Zx[kMaxU];
     // k (over U') padded to kMaxU + 1 = 36 with zeros, so MFMA operand reads need no predicate
@@ -291,6 +293,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   const double* xin = A.x[d.parity] + f * A.x_stride;
   const int m = d.m;
   const bool first = (d.flags & kFirst) != 0;
+  // Joseph (one marker per chunk): Σ ← Σ − K·M − (ΣHᵀ − K·S)·Kᵀ, i.e. (I−KH)Σ(I−KH)ᵀ + K·R·Kᵀ
+  // expanded (slam.cpp:264-265's update in Joseph form). Row factor V = G − K·S beside K, column
+  // factor Kᵀ beside M: the record's Z carries V in columns 2..3, the chain's block gets the term.
+  const bool joseph = (d.flags & kJoseph) != 0;
 
   // kLook: this chunk's Σ_in is still being written by the previous chunk's Σ pass. Rebuild what
   // the chain needs from the chunk before: Σ_in' (the other buffer, complete) and its record.
@@ -389,6 +395,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
     if (tid == 0) {
       sh.pv.first = (pflags & kFirst) != 0;
+      sh.pv.joseph = (pflags & kJoseph) != 0;
       sh.pv.a1 = pa1;
       sh.pv.a2 = pa2;
     }
@@ -491,6 +498,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     if (tid < 3) sh.xpose[tid] = sh.pv.xU[tid];  // pose ∈ U' always
     __syncthreads();
     EKF_STAMP(5);
+    // a Joseph chunk before: its V'·K'ᵀ term as rank 2..3 (K' columns 2..3 are V' = R·Z'[:, 2..3];
+    // M' rows 2..3 become K'ᵀ, the column factor)
+    const bool pj = sh.pv.joseph != 0;
+    if (pj) {
+      for (int e = tid; e < 2 * kW; e += blockDim.x) {
+        const int k = e / kW, b = e - k * kW;
+        sh.pv.M[2 + k][b] = b < kMaxU ? sh.pv.K[b][k] : 0.0;
+      }
+      __syncthreads();
+    }
     if (tid == 192) {  // wave 3 has one P tile fewer: the predicted pose (slam.cpp:184-196) here
       double a1, a2;
       predicted_pose(sh.tmo, d, sh.xpose, sh.pose, &a1, &a2);
@@ -498,8 +515,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       sh.a2 = a2;
     }
     // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
-    // ≥ 2m' are zero because Z' / Y' are)
-    const int zc = 2 * sh.pv.m;
+    // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4)
+    const int zc = pj ? 4 : 2 * sh.pv.m;
     for (int tt = wv; tt < 9; tt += 4) {
       const int ti = tt / 3, tj = tt % 3;
       const int col = 16 * tj + i16, ar = min(16 * ti + i16, kMaxU - 1), cc = min(col, kMaxU - 1);
@@ -653,7 +670,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       EKF_STAMP(64 + 8 * c);
       const double z0 = d.z[c][0], z1 = d.z[c][1];
       bool sk = sh.skip[c] != 0;
-      double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0;
+      double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0, Sm_keep[4];
       if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
       EKF_STAMP(65 + 8 * c);
       // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]
@@ -678,6 +695,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
         Sm[0] += A.r;
         Sm[3] += A.r;
+        for (int k = 0; k < 4; ++k) Sm_keep[k] = Sm[k];
         if (!sk && inv2(Sm, Si)) {
           nv0 = z0 - zhat[0];
           bool nok;
@@ -754,6 +772,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         kd[1] = in ? K1 : 0.0;
         md[0] = in ? mm0 : 0.0;
         md[1] = in ? mm1 : 0.0;
+        if (joseph) {  // G = Σ·Hᵀ and S for the (ΣHᵀ − K·S)·Kᵀ term (chunks of one marker)
+          double* gd = st ? &sh.GU[lane][0] : &sh.junk2[lane][0];
+          gd[0] = in ? ka : 0.0;
+          gd[1] = in ? kb : 0.0;
+          if (lane == 0)
+            for (int k = 0; k < 4; ++k) sh.Ss[k] = sk ? 0.0 : Sm_keep[k];
+        }
       }
       if (lane == 0) {
 #pragma unroll
@@ -850,10 +875,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const __amdgpu_buffer_rsrc_t rr =
         __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
     constexpr int oZ = static_cast<int>(offsetof(ChunkRec, Z));
-    {  // columns ≥ 2m of the record's Z are zero (the factor kernel and a rebuilding chain read them)
-      const int zw = kZC - 2 * m;
+    {  // columns ≥ 2m of the record's Z are zero (the factor kernel and a rebuilding chain read
+       // them); Joseph keeps columns 2..3 for V
+      const int z0c = joseph ? 2 * m + 2 : 2 * m;
+      const int zw = kZC - z0c;
       for (int e = lane; e < kMaxU * zw; e += 64) {
-        const int b = e / zw, k = 2 * m + (e - b * zw);
+        const int b = e / zw, k = z0c + (e - b * zw);
         st_wt(&rec->Z[b][k], 0.0);
       }
     }
@@ -862,7 +889,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       const int pj = 3 + 2 * c;
       const int pA[5] = {0, 1, 2, pj, pj + 1};
       if (lane < kMaxU) {
-        double Z0 = 0.0, Z1 = 0.0;
+        double Z0 = 0.0, Z1 = 0.0, V0 = 0.0, V1 = 0.0;
         if (lane < nu) {
           double pa = 0.0, pb = 0.0;
 #pragma unroll
@@ -873,10 +900,19 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           }
           Z0 = pa * sh.Sis[c][0] + pb * sh.Sis[c][2];
           Z1 = pa * sh.Sis[c][1] + pb * sh.Sis[c][3];
+          if (joseph) {  // V = W − Z·S with W = Φ[:, pA]·Hᵀ: r₀(i)·V = (ΣHᵀ − K·S)[i]
+            V0 = pa - (Z0 * sh.Ss[0] + Z1 * sh.Ss[2]);
+            V1 = pb - (Z0 * sh.Ss[1] + Z1 * sh.Ss[3]);
+          }
         }
         sh.Z[lane][2 * c] = Z0;
         sh.Z[lane][2 * c + 1] = Z1;
         st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
+        if (joseph) {
+          sh.Z[lane][2] = V0;
+          sh.Z[lane][3] = V1;
+          st_wt2(rr, oZ + 8 * (kZC * lane + 2), V0, V1);
+        }
       }
       if (c + 1 < m) {
         const int live = 3 + (nu - pj - 2);
@@ -961,6 +997,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       double v = sh.P[0][a][b];
       if (m > 0)
         v = rank2_sub(v, sh.KU[c][a][0], sh.KU[c][a][1], sh.MU[c][b][0], sh.MU[c][b][1]);
+      if (m > 0 && joseph) {  // − (G − K·S)[a]·K[b]ᵀ
+        const double k0 = sh.KU[c][a][0], k1 = sh.KU[c][a][1];
+        const double v0 = sh.GU[a][0] - (k0 * sh.Ss[0] + k1 * sh.Ss[2]);
+        const double v1 = sh.GU[a][1] - (k0 * sh.Ss[1] + k1 * sh.Ss[3]);
+        v = rank2_sub(v, v0, v1, sh.KU[c][b][0], sh.KU[c][b][1]);
+      }
       if (a < nu && b < nu) st_wt(&rec->Pend[a][b], v);
     }
   }
@@ -1058,6 +1100,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
   T* mc = A.mcat + f * A.km_stride;
   const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
   const bool first = (d.flags & kFirst) != 0;
+  const bool joseph = (d.flags & kJoseph) != 0;
   // the chain of this chunk runs on the other stream: wait for its record
   if (tid < 64) sh.pos64[tid] = kMaxU;
   if (A.polls && tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
@@ -1165,6 +1208,8 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
       if (row < n) {
         kc[(2 + l16) * ldk + row] = static_cast<T>(acc0[r]);
         kc[(18 + l16) * ldk + row] = static_cast<T>(acc1[r]);
+        // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
+        if (joseph && l16 < 2) mc[(4 + l16) * ldk + row] = static_cast<T>(acc0[r]);
         if (l16 == 0) {  // rows of U take the chain's x (first position of the row in U)
           const int pos = sh.pos64[row - rbase];
           xout[row] = pos < nu ? xfin[pos] : xin[row] + acc2[r];
@@ -1212,7 +1257,8 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kr = ks + 4 * r;
-        mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
+        if (!(joseph && (kr == 2 || kr == 3)))  // (Joseph: the row waves write K there)
+          mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
         mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
       }
     }
@@ -1430,7 +1476,8 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
   if ((d.flags & kActive) && t < trows * tcols) {
     SIG_STAMP(1);
     const int f = A.f0 + fb;
-    const int kw = ((2 + 2 * d.m + 3) / 4) * 4;  // this filter's rank; rows beyond are stale
+    // this filter's rank (Joseph: K·M and V·Kᵀ per marker); rows beyond are stale
+    const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
     const int tr = t / tcols, tc = t - tr * tcols;
     T* rows = (d.flags & kRowsOut) ? A.rows + f * A.rows_stride : nullptr;
     Tile::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,

@@ -120,8 +120,9 @@ int ekf_posterior(ekf_t h, int filter);
 
 /* Joseph-form covariance update, opt-in (off by default, like the reference, which applies
  * Σ ← (I − KH)Σ at slam.cpp:264-265): Σ ← (I − KH)Σ(I − KH)ᵀ + KRKᵀ for every later correction.
- * Equal in exact arithmetic with the optimal gain; it differs only in rounding. Resident path only
- * (EKF_E_ARG on the pipeline, whose rank-(2+2m) factors carry the simple form). */
+ * Equal in exact arithmetic with the optimal gain; it differs only in rounding. Resident path: its
+ * own kernel instantiation. HBM pipeline (fp32 and fp64): one marker per chunk, the factor pair of
+ * rank 2 + 4 (K·M and (ΣHᵀ − K·S)·Kᵀ), so one Σ pass per correction instead of per message. */
 int ekf_set_joseph(ekf_t h, int on);
 
 /* Deferred submission. While on, the callbacks above only plan their work on the host; the plan

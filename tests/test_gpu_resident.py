@@ -252,14 +252,16 @@ def test_deferred_submission_and_reset(resident, monkeypatch):
     assert np.abs(S1 - g["sigma"]).max() < TOL
 
 
+@pytest.mark.parametrize("resident", [True, False], ids=["resident", "pipeline"])
 @pytest.mark.parametrize("name", ["basic_world_known", "basic_world_assoc", "synth16_known",
                                   "crowded_assoc"])
-def test_joseph_form_matches_oracle(name, monkeypatch):
+def test_joseph_form_matches_oracle(name, resident, monkeypatch):
     """Opt-in Joseph-form update (BASELINE.json north_star; off by default like slam.cpp:264-265)
-    against the C oracle's Joseph mode on the same drive. Same tolerance as the swarm test: the
+    against the C oracle's Joseph mode on the same drive, on the resident path and on the HBM
+    pipeline (one marker per chunk, factor rank 2 + 4). Same tolerance as the swarm test: the
     Joseph expansion adds two rank-2 terms whose rounding meets the 1e7 first-sighting
     cancellation (the oracle's literal and structured Joseph modes differ by up to 4e-9)."""
-    _env(monkeypatch, True)
+    _env(monkeypatch, resident)
     sc, g = load_golden(name)
     assoc = bool(g["assoc"])
     s = pyekf.Slam(n_landmarks=sc.n_landmarks,
@@ -279,9 +281,38 @@ def test_joseph_form_matches_oracle(name, monkeypatch):
     assert np.abs(poses - g["poses"]).max() < 1e-7
 
 
-def test_joseph_form_rejected_on_pipeline(monkeypatch):
+def test_joseph_pipeline_multi_filter_and_toggle(monkeypatch):
+    """Pipeline Joseph with 4 filters (filter f replays scenario f), switched on mid-replay: the
+    messages before the switch equal the simple form, the ones after the oracle's Joseph mode from
+    that state."""
     _env(monkeypatch, False)
-    e = pyekf.EKF(n_landmarks=50)
+    scs = [synth.synthetic(40, 16, seed=300 + k) for k in range(4)]
+    odo = [pyekf.odometry(s) for s in scs]
+    T, M = 16, max(s.ids.shape[1] for s in scs)
+    cnt = np.stack([s.count for s in scs], 1)
+    ids = np.full((T, 4, M), -1, np.int32)
+    act = np.zeros((T, 4, M), np.int32)
+    rel = np.zeros((T, 4, M, 2))
+    for k, s in enumerate(scs):
+        ids[:, k, :s.ids.shape[1]], act[:, k, :s.ids.shape[1]] = s.ids, s.actions
+        rel[:, k, :s.ids.shape[1]] = s.rel
+    od = np.stack(odo, 1)
+    e = pyekf.EKF(n_landmarks=40, n_filters=4)
     assert e.path == pyekf.EKF_PATH_PIPELINE
-    assert e.set_joseph(True) == pyekf.EKF_E_ARG
-    assert e.set_joseph(False) == pyekf.EKF_OK
+    e.replay(cnt[:8], rel[:8], od[:8], ids=ids[:8], actions=act[:8])
+    assert e.set_joseph(True) == pyekf.EKF_OK
+    e.replay(cnt[8:], rel[8:], od[8:], ids=ids[8:], actions=act[8:])
+    for k in range(4):
+        ref = orc.OracleEKF(n_landmarks=40)
+        for t in range(T):
+            if t == 8:  # the switch point
+                orc.lib().orc_ekf_set_joseph(ref.h, 1)
+            ref.set_odom(od[t, k])
+            c = int(cnt[t, k])
+            ref.fake_sensor_cb(ids[t, k, :c], act[t, k, :c], rel[t, k, :c])
+        x, S, c = e.state(k)
+        xr, Sr, _, cr = ref.get()
+        assert e.status(k) == 0 and c == cr
+        assert np.abs(x - xr).max() < SWARM_TOL, k
+        assert np.abs(S - Sr).max() < SWARM_TOL, k
+    e.close()

@@ -177,6 +177,42 @@ def test_n1024_fp32_populated_against_oracle(n1024, env, monkeypatch):
     assert np.abs(x32 - xr).max() < 2e-4
 
 
+@pytest.mark.parametrize("dtype", [pyekf.EKF_F32, pyekf.EKF_F64], ids=["f32", "f64"])
+def test_n1024_joseph_populated_against_oracle(n1024, dtype):
+    """configs[2]'s populated map with the Joseph form (BASELINE.json north_star; ekf_set_joseph)
+    on the HBM pipeline: 6 circle messages (96 corrections, one Σ pass each) from the fp64 survey's
+    state against the oracle's Joseph mode. fp32 poses within 2e-4 (as the simple form), fp64 state
+    5e-8 and Σ 1e-7 (the populated-map tolerances above)."""
+    sc, odom, ws = n1024
+    w, T = sc.n_warm, 6
+    e = pyekf.EKF(n_landmarks=1024, dtype=dtype)
+    x, S, tmo, cnt = ws
+    e.set_state(x, S, tmo=tmo, counter=cnt)
+    assert e.set_joseph(True) == pyekf.EKF_OK
+    poses = _replay(e, slice(w, w + T), sc, odom, poses=True)
+    ref = orc.OracleEKF(n_landmarks=1024, joseph=True)
+    ref.set(x, S, tmo, x[:3], cnt)
+    err = 0.0
+    for t in range(T):
+        ref.set_odom(odom[w + t])
+        c = int(sc.count[w + t])
+        ref.fake_sensor_cb(sc.ids[w + t, :c], sc.actions[w + t, :c], sc.rel[w + t, :c])
+        err = max(err, float(np.abs(poses[t, 0] - ref.get(sigma=False)[0][:3]).max()))
+    xg, Sg, _ = e.state()
+    assert e.status() == 0
+    e.close()
+    xr, Sr, _, _ = ref.get()
+    ERRORS["n1024_joseph_" + ("f32" if dtype == pyekf.EKF_F32 else "f64")] = {
+        "pose": err, "state": float(np.abs(xg - xr).max()), "sigma": float(np.abs(Sg - Sr).max())}
+    if dtype == pyekf.EKF_F32:
+        assert err < 2e-4
+        assert np.all(np.isfinite(Sg))
+    else:
+        assert err < POSE_TOL
+        assert np.abs(xg - xr).max() < STATE_TOL
+        assert np.abs(Sg - Sr).max() < SIGMA_TOL
+
+
 def test_swarm_n256_512_filters_against_oracle():
     """configs[3], one GPU's share: 512 filters of N=256 fp64 in one handle, filter f seeded
     base + f (its own map, slip and noise), survey + 8 circle messages. Every filter's status is
