@@ -73,6 +73,7 @@ struct ekf_ctx {
   FilterCtl* ctl = nullptr;
   ChunkRec* rec = nullptr;
   void* rows = nullptr;  // fp64: Σ_in[i, U] from a Σ pass to the next chunk's factor kernel
+  void* stage = nullptr; // StageRec<T>[2][F]: a kLook chain's rebuild operands (kStageIn)
   MsgDesc* ddesc = nullptr;
   size_t sig_stride = 0, x_stride = 0, km_stride = 0;
   // host mirror
@@ -83,6 +84,8 @@ struct ekf_ctx {
   std::vector<std::array<int, kMaxChunk>> prev_ids;  // that chunk's landmark ids
   std::vector<long> last_desc;   // plan_d index of the filter's last known-association chunk in
                                  // the current (not yet uploaded) plan, −1: none
+  std::vector<std::array<long, 2>> stg_desc;  // plan_d indices of its last two pipelined chunks
+                                              // ([0] the last), −1: none (kStageOut planning)
   // launch plan: descriptors for a whole call (or a whole replay) uploaded with ONE copy
   std::vector<MsgDesc> plan_d;
   std::vector<Launch> plan_l;
@@ -125,6 +128,7 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.ctl = h->ctl;
   a.rec = h->rec;
   a.rec_stride = static_cast<size_t>(h->F);
+  a.stage = static_cast<StageRec<T>*>(h->stage);
   a.rows = static_cast<T*>(h->rows);
   a.rows_stride = static_cast<size_t>(h->ldk) * kRowW;
   a.sync = h->sync;
@@ -179,6 +183,13 @@ void fill_desc(MsgDesc* d, int m, int flags, int parity, const Pose2& odom) {
   d->odom[2] = odom.y;
 }
 
+// The filter's next chunk has no planned predecessor in this plan (upload, association, posterior,
+// reset, device plan): no row hand-off, no staged rebuild operands.
+void forget_desc(ekf_ctx* h, int f) {
+  h->last_desc[f] = -1;
+  h->stg_desc[f] = {-1L, -1L};
+}
+
 // slam.cpp:208-210 (host, glibc, as the reference)
 inline void measure(double rx, double ry, double* zr, double* zb) {
   *zr = std::sqrt(std::pow(rx, 2) + std::pow(ry, 2));
@@ -204,9 +215,10 @@ int join_bulk(ekf_ctx* h) {
 // launch that walks them all (rebuilding its block from the chunk before each time), then per chunk the factor
 // kernel and the Σ pass on the bulk stream. More than one chunk only with devsync, where the bulk
 // kernels of chunk i wait on the device for the chain's epoch of chunk i.
+// hd: the host copy of the group's descriptors (nullptr: written on the device, no kStageOut).
 template <typename T>
-int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined,
-                 bool nolook) {
+int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
+                 bool pipelined, bool nolook) {
   PassArgs<T> a = args<T>(h, dptr, f0);
   a.desc_stride = nf;
   const unsigned s0 = static_cast<unsigned>(h->seq);
@@ -244,8 +256,13 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, b
       return launch_factors<T>(ai, nf, bs, e0, e1);
     });
     if (rc) return rc;
+    bool stage = false;  // some filter stages the rebuild operands of its chunk after next
+    for (int k = 0; hd && k < nf; ++k) {
+      const int fl = hd[static_cast<size_t>(i) * nf + k].flags;
+      stage = stage || ((fl & kActive) && (fl & kStageOut));
+    }
     rc = timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
-      return launch_sigma_pass<T>(ai, nf, !(in_group && i + 1 < nchunks), bs, e0, e1);
+      return launch_sigma_pass<T>(ai, nf, !(in_group && i + 1 < nchunks), stage, bs, e0, e1);
     });
     if (rc) return rc;
     if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[(s0 + i) & 1], bs));
@@ -255,10 +272,11 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, b
 }
 
 // nolook: some active filter's first chunk gathers its own Σ_in (no kLook rebuild)
-int group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, int nchunks, bool pipelined,
-          bool nolook = true) {
-  return h->cfg.dtype == EKF_F32 ? launch_group<float>(h, dptr, f0, nf, nchunks, pipelined, nolook)
-                                 : launch_group<double>(h, dptr, f0, nf, nchunks, pipelined, nolook);
+int group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
+          bool pipelined, bool nolook = true) {
+  return h->cfg.dtype == EKF_F32
+             ? launch_group<float>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook)
+             : launch_group<double>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook);
 }
 
 // The chain → factors kernels of a message are a latency-bound critical path; the Σ pass of the
@@ -376,6 +394,20 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict, const char* absent = n
         d->flags |= kRowsIn;
       }
       h->last_desc[f] = m > 0 ? static_cast<long>(off + k) : -1;
+      // the k_patch_stage behind the Σ pass two chunks back gathers this chain's rebuild operands
+      // (the Σ_in' it reads is that pass's output)
+      if ((flags & kLook) && h->stage && h->stg_desc[f][1] >= 0) {
+        MsgDesc* sd = &h->plan_d[h->stg_desc[f][1]];
+        sd->flags |= kStageOut;
+        sd->stg_m = m;
+        sd->stg_pm = h->prev_m[f];
+        for (int i = 0; i < kMaxChunk; ++i) {
+          sd->stg_ids[i] = d->ids[i];
+          sd->stg_pids[i] = h->prev_ids[f][i];
+        }
+        d->flags |= kStageIn;
+      }
+      h->stg_desc[f] = {static_cast<long>(off + k), h->stg_desc[f][0]};
       h->prev_m[f] = m;
       for (int i = 0; i < m; ++i) h->prev_ids[f][i] = mk[b + i].id;
       h->parity[f] ^= 1;
@@ -405,7 +437,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
       }
       int flags = kActive | kNoInit | (h->joseph && !h->resident ? kJoseph : 0);
       h->prev_m[f] = -1;  // association chunks run unpipelined
-      h->last_desc[f] = -1;
+      forget_desc(h, f);
       if (i == 0 && (predict || h->pending[f])) flags |= kFirst;
       if (i == std::max(mf, 1) - 1 && posterior) flags |= kLast;
       const int m = mf > 0 ? 1 : 0;
@@ -425,7 +457,7 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
 
 void plan_posterior(ekf_ctx* h, int f) {
   h->prev_m[f] = -1;
-  h->last_desc[f] = -1;
+  forget_desc(h, f);
   const size_t off = h->plan_d.size();
   h->plan_d.resize(off + 1);
   fill_desc(&h->plan_d[off], 0, kActive, h->parity[f], h->odom[f]);
@@ -486,7 +518,7 @@ int flush_resident(ekf_ctx* h) {
   });
   h->plan_d.clear();
   h->plan_l.clear();
-  std::fill(h->last_desc.begin(), h->last_desc.end(), -1L);
+  for (int f = 0; f < h->F; ++f) forget_desc(h, f);
   std::fill(h->prev_m.begin(), h->prev_m.end(), -1);
   return rc;
 }
@@ -540,14 +572,15 @@ int flush(ekf_ctx* h) {
         const int fl = h->plan_d[L.off + k].flags;
         nolook = nolook || ((fl & kActive) && !(fl & kLook));
       }
-      rc = group(h, dp, L.f0, L.nf, static_cast<int>(lj - li), true, nolook);
+      rc = group(h, dp, h->plan_d.data() + L.off, L.f0, L.nf, static_cast<int>(lj - li), true,
+                 nolook);
       li = lj;
       continue;
     }
     if (L.kind == 1) {
       if (join_bulk(h)) return EKF_E_HIP;
       rc = assoc(h, dp, L.f0, L.nf);
-      if (!rc) rc = group(h, dp, L.f0, L.nf, 1, false);
+      if (!rc) rc = group(h, dp, h->plan_d.data() + L.off, L.f0, L.nf, 1, false);
     }
     if (!rc && L.kind == 2) {
       if (join_bulk(h)) return EKF_E_HIP;
@@ -557,7 +590,7 @@ int flush(ekf_ctx* h) {
   }
   h->plan_d.clear();
   h->plan_l.clear();
-  std::fill(h->last_desc.begin(), h->last_desc.end(), -1L);
+  for (int f = 0; f < h->F; ++f) forget_desc(h, f);
   return rc;
 }
 
@@ -674,9 +707,10 @@ int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
       HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
       const size_t F = static_cast<size_t>(h->F);
       if (h->devsync && !h->serial) {
-        rc = group(h, dd, 0, h->F, T, true, true);
+        rc = group(h, dd, nullptr, 0, h->F, T, true, true);
       } else {
-        for (int t = 0; t < T && !rc; ++t) rc = group(h, dd + t * F, 0, h->F, 1, true, t == 0);
+        for (int t = 0; t < T && !rc; ++t)
+          rc = group(h, dd + t * F, nullptr, 0, h->F, 1, true, t == 0);
       }
     }
   }
@@ -684,7 +718,7 @@ int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
     h->parity[f] = parity_after[f];
     h->pending[f] = 0;
     h->prev_m[f] = -1;
-    h->last_desc[f] = -1;
+    forget_desc(h, f);
   }
   return rc;
 }
@@ -744,6 +778,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   h->pending.assign(h->F, 0);
   h->prev_m.assign(h->F, -1);
   h->last_desc.assign(h->F, -1L);
+  h->stg_desc.assign(h->F, std::array<long, 2>{-1L, -1L});
   h->prev_ids.assign(h->F, std::array<int, kMaxChunk>{});
   h->msgs.resize(h->F);
   h->absent.assign(h->F, 0);
@@ -776,9 +811,17 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipMalloc(&h->rec, 2 * sizeof(ChunkRec) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
   const char* rows_env = std::getenv("EKF_ROWS");  // EKF_ROWS=0: always gather (tests)
   if (cfg.dtype == EKF_F64 && !(rows_env && std::atoi(rows_env) == 0) &&
-      // fp32's U block is rewritten after its pass (k_pend_scatter): gathered there
+      // fp32's U block is rewritten after its pass (k_patch_stage): gathered there
       hipMalloc(&h->rows, sizeof(double) * kRowW * h->ldk * h->F) != hipSuccess)
     return fail(EKF_E_NOMEM);
+  // staged rebuild operands (EKF_STAGE=0: every kLook chain gathers its own, tests compare the two)
+  const char* stage_env = std::getenv("EKF_STAGE");
+  const size_t stage_bytes = 2 * h->F *
+      (cfg.dtype == EKF_F32 ? sizeof(StageRec<float>) : sizeof(StageRec<double>));
+  if (!(stage_env && std::atoi(stage_env) == 0)) {
+    if (hipMalloc(&h->stage, stage_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
+    if (hipMemset(h->stage, 0, stage_bytes) != hipSuccess) return fail(EKF_E_HIP);
+  }
   const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + h->F);
   if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
@@ -827,6 +870,7 @@ int ekf_destroy(ekf_t h) {
   if (h->ctl) hipFree(h->ctl);
   if (h->rec) hipFree(h->rec);
   if (h->rows) hipFree(h->rows);
+  if (h->stage) hipFree(h->stage);
   if (h->ddesc) hipFree(h->ddesc);
   for (int i = 0; i < kRing; ++i) {
     if (h->ring[i].p) hipHostFree(h->ring[i].p);
@@ -1051,7 +1095,7 @@ int ekf_reset(ekf_t h, int f) {
     h->parity[k] = 0;
     h->pending[k] = 0;
     h->prev_m[k] = -1;
-    h->last_desc[k] = -1;
+    forget_desc(h, k);
   }
   const size_t sb = h->sig_stride * h->w;
   char* sig0 = static_cast<char*>(h->sig[0]) + f0 * sb;
@@ -1112,7 +1156,7 @@ int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, cons
   if (!valid(h, f)) return EKF_E_ARG;
   if (int rc = settle(h)) return rc;
   h->prev_m[f] = -1;
-  h->last_desc[f] = -1;
+  forget_desc(h, f);
   const int p = h->parity[f];
   if (state)
     HIPCHK(hipMemcpy(h->x[p] + f * h->x_stride, state, h->n * sizeof(double),

@@ -36,6 +36,11 @@ constexpr int kRowsIn = 64;  // factor kernel: r(i) = Σ_in[i, U] from the rows 
 constexpr int kRowW = kMaxU + 1;  // rows buffer: kRowW × ldk per filter (position-major)
 constexpr int kJoseph = 128; // Joseph-form Σ update (ekf_set_joseph): one marker per chunk, the
                              // factor rank 2 + 4 (K·M and (ΣHᵀ − K·S)·Kᵀ, see k_chain)
+constexpr int kStageOut = 256;  // behind this chunk's Σ pass (k_patch_stage): gather the rebuild
+                                // operands of the filter's chunk after next (stg_*) into StageRec
+constexpr int kStageIn = 512;   // kLook chain: read its rebuild operands from StageRec (contiguous)
+                                // instead of gathering them from Σ_in' at the chunk's start
+constexpr int kStW = kMaxU + 1;  // chain block stride (entry e = a·kStW + b)
 
 // One chunk of one message for one filter (uploaded by the host, read by every kernel of the pair).
 struct alignas(16) MsgDesc {
@@ -52,6 +57,10 @@ struct alignas(16) MsgDesc {
   int nxt_nu;                   // kRowsOut: |U_next|
   int pad2;
   int nxt_u[kMaxU + 1];         // kRowsOut: U_next in the next chain's order (ekf_api index_map)
+  int stg_m, stg_pm;            // kStageOut: markers of the filter's chunk after next / next chunk
+  int pad3[2];
+  int stg_ids[kMaxChunk];       // kStageOut: the chunk after next's ids (its U)
+  int stg_pids[kMaxChunk];      // kStageOut: the next chunk's ids (U' of the chunk after next)
 };
 
 struct alignas(16) FilterCtl {
@@ -83,5 +92,18 @@ struct alignas(16) ChunkRec {
 static_assert(offsetof(ChunkRec, Z) % 16 == 0 && offsetof(ChunkRec, Y) % 16 == 0 &&
                   offsetof(ChunkRec, Pend) % 16 == 0 && sizeof(ChunkRec) % 16 == 0,
               "ChunkRec payload 16-byte aligned");
+
+// The rebuild operands of a kLook chain (k_chain's prologue), gathered off the chain's path by the
+// k_patch_stage of the chunk two back, right behind the Σ pass that wrote them: with U this chunk's
+// index set and U' the previous chunk's, Σ = Σ_in' (the previous chunk's Σ_in), x = x_in',
+//   v[0][e] = Σ[u_a][u_b], v[1][e] = Σ[u_a][u'_b], v[2][e] = Σ[u'_b][u_a]   (a, b clamped to kMaxU−1)
+//   r0u[t] = Σ[0][u_t], c0u[t] = Σ[u_t][0], r0p[t] = Σ[0][u'_t], c0p[t] = Σ[u'_t][0], xg[t] = x[u_t]
+// — the very values the chain would gather (the fp32 block patch included), stored contiguously.
+// [2][F] by the chain's Σ parity.
+template <typename T>
+struct alignas(16) StageRec {
+  double r0u[kStW], c0u[kStW], r0p[kStW], c0p[kStW], xg[kStW];
+  T v[3][kStW * kStW];
+};
 
 }  // namespace ekfslam

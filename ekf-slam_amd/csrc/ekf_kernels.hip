@@ -33,18 +33,19 @@
 
 namespace ekfslam {
 
-// Diagnostic build only (tools/gain_bench.hip): s_memtime stamps of block (0,0), thread 0.
+// Diagnostic build only (tools/chain_stamps.py): s_memtime stamps of k_chain's block (0,0), thread
+// 0, in a ring of the last four chunks (by seq & 3).
 #ifdef EKF_DIAG_STAMPS
-__device__ unsigned long long g_stamps[256];
+__device__ unsigned long long g_stamps[4 * 512];
 #define EKF_STAMP(i)                                                              \
   do {                                                                            \
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                   \
-      g_stamps[i] = __builtin_amdgcn_s_memtime();                                 \
+      g_stamps[512 * (seq & 3) + (i)] = __builtin_amdgcn_s_memtime();             \
   } while (0)
 #define EKF_STAMPT(i, t)                                                          \
   do {                                                                            \
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == (t))                 \
-      g_stamps[i] = __builtin_amdgcn_s_memtime();                                 \
+      g_stamps[512 * (seq & 3) + (i)] = __builtin_amdgcn_s_memtime();             \
   } while (0)
 #else
 #define EKF_STAMPT(i, t) \
@@ -58,7 +59,7 @@ __device__ unsigned long long g_stamps[256];
 }  // namespace ekfslam
 extern "C" int ekfslam_diag_read_stamps(unsigned long long* out, int n) {
   using ekfslam::g_stamps;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < 256 ? n : 256)) == hipSuccess ? 0 : -5;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < 2048 ? n : 2048)) == hipSuccess ? 0 : -5;
 }
 namespace ekfslam {
 #endif
@@ -352,25 +353,49 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
     const int np = sh.pv.nu;
     double vz[kPer], vy[kPer], vd[kPer], vr[kPer], vc[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = tid + i * kChainThreads;
-      vz[i] = (&rp->Z[0][0])[e < kMaxU * kZC ? e : 0];
-      vy[i] = (&rp->Y[0][0])[e < kZC * kMaxU ? e : 0];
-      const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);  // clamped: in bounds
-      const size_t ua = static_cast<size_t>(sh.u[a]) * ld, pa = static_cast<size_t>(sh.pv.u[b]);
-      vd[i] = static_cast<double>(Sp[ua + sh.u[b]]);
-      vr[i] = static_cast<double>(Sp[ua + pa]);
-      vc[i] = static_cast<double>(Sp[pa * ld + sh.u[a]]);
-    }
-    // raw row 0 / column 0 of Σ_in' at U and U' (for the previous predict), x', record scalars
+    double r0u, c0u, r0p, c0p, x2;
     const int tc = tid < kMaxU ? tid : 0;
-    const int uu = sh.u[tc], pu = sh.pv.u[tc];
-    const double r0u = static_cast<double>(Sp[uu]);
-    const double c0u = static_cast<double>(Sp[static_cast<size_t>(uu) * ld]);
-    const double r0p = static_cast<double>(Sp[pu]);
-    const double c0p = static_cast<double>(Sp[static_cast<size_t>(pu) * ld]);
-    const double x0 = rp->xU[tc], x1 = rp->Zx[tc], x2 = xp[uu];
+    if (d.flags & kStageIn) {
+      // staged by the k_patch_stage two chunks back, right behind the Σ pass that wrote Σ_in':
+      // the same values as the gather below, contiguous (≈ 5 000 cycles less than the ≈ 1 900
+      // scattered lines of the gather through one CU)
+      const StageRec<T>* sg = A.stage + static_cast<size_t>(d.parity) * A.rec_stride + f;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + i * kChainThreads, es = min(e, kW * kW - 1);
+        vz[i] = (&rp->Z[0][0])[e < kMaxU * kZC ? e : 0];
+        vy[i] = (&rp->Y[0][0])[e < kZC * kMaxU ? e : 0];
+        vd[i] = static_cast<double>(sg->v[0][es]);
+        vr[i] = static_cast<double>(sg->v[1][es]);
+        vc[i] = static_cast<double>(sg->v[2][es]);
+      }
+      r0u = sg->r0u[tc];
+      c0u = sg->c0u[tc];
+      r0p = sg->r0p[tc];
+      c0p = sg->c0p[tc];
+      x2 = sg->xg[tc];
+    } else {
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + i * kChainThreads;
+        vz[i] = (&rp->Z[0][0])[e < kMaxU * kZC ? e : 0];
+        vy[i] = (&rp->Y[0][0])[e < kZC * kMaxU ? e : 0];
+        const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);  // clamped: in bounds
+        const size_t ua = static_cast<size_t>(sh.u[a]) * ld, pa = static_cast<size_t>(sh.pv.u[b]);
+        vd[i] = static_cast<double>(Sp[ua + sh.u[b]]);
+        vr[i] = static_cast<double>(Sp[ua + pa]);
+        vc[i] = static_cast<double>(Sp[pa * ld + sh.u[a]]);
+      }
+      // raw row 0 / column 0 of Σ_in' at U and U' (for the previous predict), x'
+      const int uu = sh.u[tc], pu = sh.pv.u[tc];
+      r0u = static_cast<double>(Sp[uu]);
+      c0u = static_cast<double>(Sp[static_cast<size_t>(uu) * ld]);
+      r0p = static_cast<double>(Sp[pu]);
+      c0p = static_cast<double>(Sp[static_cast<size_t>(pu) * ld]);
+      x2 = xp[uu];
+    }
+    // record scalars
+    const double x0 = rp->xU[tc], x1 = rp->Zx[tc];
     const int pflags = rp->flags;
     const double pa1 = rp->a1, pa2 = rp->a2;
     const double tq = ctl->tmo[tid < 3 ? tid : 0];
@@ -988,7 +1013,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
   __syncthreads();
   // fp32 Σ: the last step's rank-2 term on the whole block (earlier steps are applied), the final
-  // Σ[U, U] in fp64, to the record (write-through) for k_pend_scatter (the Σ pass's U × U entries)
+  // Σ[U, U] in fp64, to the record (write-through) for k_patch_stage (the Σ pass's U × U entries)
   if constexpr (sizeof(T) == 4) {
     const int c = max(m - 1, 0);
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
@@ -1494,37 +1519,127 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
 // reference's prior, slam.cpp:130) loses δ in fp32; the chain computed it in fp64. Other entries
 // carry no such cancellation (the prior has no cross terms). A repeated index takes the entry of
 // its first position in U. One workgroup per filter, ≤ 35 × 35 stores.
-__global__ __launch_bounds__(256) void k_pend_scatter(PassArgs<float> A) {
+//
+// kStageOut (either dtype): then the rebuild operands of the filter's chunk after next (StageRec),
+// gathered from the Σ_out / x_out just completed — off the chain's critical path, where the same
+// gather at the chain's start cost ≈ 10 µs of a 47 µs message (≈ 1 900 scattered lines through one
+// CU). Patched entries take the patch's value (the loads would race the scatter's stores).
+template <typename T>
+__global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
+  constexpr bool kPatch = sizeof(T) == 4;
   const MsgDesc& d = A.desc[blockIdx.x];
-  if (!(d.flags & kActive)) return;
+  const int flags = d.flags;
+  if (!(flags & kActive)) return;
+  const bool stage = (flags & kStageOut) != 0;
+  if (!kPatch && !stage) return;
   const int f = A.f0 + blockIdx.x;
+  const int tid = threadIdx.x;
   const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
   __shared__ int su[kMaxU];
-  __shared__ int firstpos[kMaxU];
-  // every global load issued up front: entry e ↔ (e / kMaxU, e % kMaxU) of the padded block
+  __shared__ int sfirst[kMaxU];           // position is its index's first in this chunk's U
+  __shared__ double spend[kMaxU][kMaxU + 1];
+  __shared__ int sgu[kStW], sgp[kStW];    // staged chain's U and U' (columns)
+  __shared__ int sgfu[kStW], sgfp[kStW];  // their first positions in this chunk's U (patched), −1
+  // ---- one global round trip: the record's block and U, the staged chunks' ids ----
   constexpr int kPer = (kMaxU * kMaxU + 255) / 256;
-  const int tid = threadIdx.x;
   double pv[kPer];
+  if (kPatch) {
 #pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const int e = min(tid + 256 * i, kMaxU * kMaxU - 1);
-    pv[i] = rec->Pend[e / kMaxU][e % kMaxU];
+    for (int i = 0; i < kPer; ++i) {
+      const int e = min(tid + 256 * i, kMaxU * kMaxU - 1);
+      pv[i] = rec->Pend[e / kMaxU][e % kMaxU];
+    }
   }
   const int nu = rec->nu;
-  if (tid < kMaxU) su[tid] = rec->u[tid];
-  __syncthreads();
-  if (tid < kMaxU) {
-    int fp = tid < nu;
-    for (int k = 0; k < tid; ++k) fp = fp && su[k] != su[tid];
-    firstpos[tid] = fp;
+  const int myu = rec->u[min(tid, kMaxU - 1)];
+  // stage threads: a = tid (U of the chunk after next) or tid − 64 (U', the next chunk's)
+  const bool isp = tid >= 64;
+  const int sa = isp ? tid - 64 : tid;
+  const int sm = isp ? d.stg_pm : d.stg_m;
+  const int sid = (isp ? d.stg_pids : d.stg_ids)[min(max(sa - 3, 0) >> 1, kMaxChunk - 1)];
+  if (tid < kMaxU) su[tid] = myu;
+  if (kPatch) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i;
+      if (e < kMaxU * kMaxU) spend[e / kMaxU][e % kMaxU] = pv[i];
+    }
   }
   __syncthreads();
-  float* S = A.sig[d.parity ^ 1] + f * A.sig_stride;
+  // ---- first positions: every lane takes all of U into registers (one LDS wait) ----
+  int uall[kMaxU];
 #pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const int e = tid + 256 * i, a = e / kMaxU, b = e % kMaxU;
-    if (e < kMaxU * kMaxU && firstpos[a] && firstpos[b])
-      S[static_cast<size_t>(su[a]) * A.ld + su[b]] = static_cast<float>(pv[i]);
+  for (int k = 0; k < kMaxU; ++k) uall[k] = su[k];
+  if (tid < kMaxU) {
+    bool fp = tid < nu;
+#pragma unroll
+    for (int k = 0; k < kMaxU; ++k) fp = fp && !(k < tid && uall[k] == myu);
+    sfirst[tid] = fp;
+  }
+  if (stage && sa < kStW && (tid < kStW || (isp && tid < 64 + kStW))) {
+    int col = 0;
+    if (sa < 3) col = sa;
+    else if (sa < 3 + 2 * sm && sa < kMaxU)
+      // k_chain's A0 mapping: marker c → 3 + 2·id (+1), a bad id → slot 0's, padding → 0
+      col = (sid < 0 || sid >= A.N ? 3 : 3 + 2 * sid) + ((sa - 3) & 1);
+    int fpos = -1;  // the first position of col in this chunk's U = its patched entry
+    if (kPatch) {
+#pragma unroll
+      for (int k = kMaxU - 1; k >= 0; --k) fpos = (k < nu && uall[k] == col) ? k : fpos;
+    }
+    (isp ? sgp : sgu)[sa] = col;
+    (isp ? sgfp : sgfu)[sa] = fpos;
+  }
+  __syncthreads();
+  T* S = A.sig[d.parity ^ 1] + f * A.sig_stride;
+  if (kPatch) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i, a = e / kMaxU, b = e % kMaxU;
+      if (e < kMaxU * kMaxU && sfirst[a] && sfirst[b])
+        S[static_cast<size_t>(su[a]) * A.ld + su[b]] = static_cast<T>(pv[i]);
+    }
+  }
+  if (!stage) return;
+  // ---- stage: the chunk after next's rebuild operands (the second global round trip) ----
+  const double* xo = A.x[d.parity ^ 1] + f * A.x_stride;
+  StageRec<T>* sg = A.stage + static_cast<size_t>(d.parity) * A.rec_stride + f;
+  // Σ_out[r][c] as the chain would read it after the patch (the load of a patched entry races
+  // the scatter above and is discarded)
+  auto val = [&](int r, int fr, int c, int fc) -> T {
+    const T g = S[static_cast<size_t>(r) * A.ld + c];
+    return (kPatch && fr >= 0 && fc >= 0) ? static_cast<T>(spend[fr][fc]) : g;
+  };
+  constexpr int kSPer = (kStW * kStW + 255) / 256;  // 6
+  T od[kSPer], orr[kSPer], oc[kSPer];
+#pragma unroll
+  for (int i = 0; i < kSPer; ++i) {
+    const int e = min(tid + 256 * i, kStW * kStW - 1);
+    const int a = min(e / kStW, kMaxU - 1), b = min(e % kStW, kMaxU - 1);
+    od[i] = val(sgu[a], sgfu[a], sgu[b], sgfu[b]);
+    orr[i] = val(sgu[a], sgfu[a], sgp[b], sgfp[b]);
+    oc[i] = val(sgp[b], sgfp[b], sgu[a], sgfu[a]);
+  }
+  const int t = min(tid, kMaxU - 1);
+  const int z = sgfu[0];  // position 0 of U is the pose θ column
+  const T r0u = val(0, z, sgu[t], sgfu[t]), c0u = val(sgu[t], sgfu[t], 0, z);
+  const T r0p = val(0, z, sgp[t], sgfp[t]), c0p = val(sgp[t], sgfp[t], 0, z);
+  const double xg = xo[sgu[t]];
+  if (tid < kStW) {
+    sg->r0u[tid] = static_cast<double>(r0u);
+    sg->c0u[tid] = static_cast<double>(c0u);
+    sg->r0p[tid] = static_cast<double>(r0p);
+    sg->c0p[tid] = static_cast<double>(c0p);
+    sg->xg[tid] = xg;
+  }
+#pragma unroll
+  for (int i = 0; i < kSPer; ++i) {
+    const int e = tid + 256 * i;
+    if (e < kStW * kStW) {
+      sg->v[0][e] = od[i];
+      sg->v[1][e] = orr[i];
+      sg->v[2][e] = oc[i];
+    }
   }
 }
 
@@ -1739,7 +1854,7 @@ hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_
 }
 
 template <typename T>
-hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, hipStream_t s,
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool stage, hipStream_t s,
                              hipEvent_t e0, hipEvent_t e1) {
   constexpr int wpb = 4;  // waves per workgroup
   if (nf >= 16) {  // XCD-aware 1-D grid (see k_sigma_pass), wide fp64 tiles
@@ -1757,8 +1872,7 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, hipStre
     const dim3 grid(per_filter, nf);
     launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
   }
-  if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL(k_pend_scatter, dim3(nf), dim3(256), 0, s, a);
+  if (sizeof(T) == 4 || stage) hipLaunchKernelGGL(k_patch_stage<T>, dim3(nf), dim3(256), 0, s, a);
   // the pass's epoch (otherwise published by the next chunk's factor kernel, PassArgs::pub_sigma)
   if (publish && a.polls) hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();
@@ -1805,7 +1919,7 @@ hipError_t launch_poison_lds(unsigned long long pattern, int n_blocks, hipStream
                                       hipEvent_t);                                                 \
   template hipError_t launch_factors<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t,          \
                                         hipEvent_t);                                               \
-  template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, bool, hipStream_t, hipEvent_t, \
+  template hipError_t launch_sigma_pass<T>(const PassArgs<T>&, int, bool, bool, hipStream_t, hipEvent_t, \
                                            hipEvent_t);                                            \
   template hipError_t launch_assoc<T>(const PassArgs<T>&, int, hipStream_t, hipEvent_t, hipEvent_t); \
   template hipError_t launch_posterior<T>(const PassArgs<T>&, int, hipStream_t);              \

@@ -26,6 +26,7 @@ struct PassArgs {
   FilterCtl* ctl;
   ChunkRec* rec;        // [2][rec_stride]: chunk records by Σ parity (chain → factors, next chain)
   size_t rec_stride;
+  StageRec<T>* stage;   // [2][rec_stride]: rebuild operands staged for a kLook chain (kStageIn)
   unsigned* sync;       // device epochs (ekf_device.hpp kSync*)
   unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
   unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
@@ -51,11 +52,12 @@ template <typename T>
 hipError_t launch_factors(const PassArgs<T>& a, int n_filters, hipStream_t s,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
-// Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, one tile per wave (fp32: then the chain's fp64
-// Σ[U,U] scattered over its block by k_pend_scatter). publish: launch the Σ-pass epoch kernel behind it; otherwise
-// the next chunk's factor kernel publishes it (PassArgs::pub_sigma).
+// Σ pass: Σ_out = Σ_in + Q − Kcatᵀ·Mcat on MFMA, one tile per wave, then k_patch_stage (fp32: the
+// chain's fp64 Σ[U,U] over its block; stage: some filter's descriptor has kStageOut, fp32 checks
+// on the device). publish: launch the Σ-pass epoch kernel behind it; otherwise the next chunk's
+// factor kernel publishes it (PassArgs::pub_sigma).
 template <typename T>
-hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, bool publish, hipStream_t s,
+hipError_t launch_sigma_pass(const PassArgs<T>& a, int n_filters, bool publish, bool stage, hipStream_t s,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 // Mahalanobis nearest-neighbour association for one marker per filter (one workgroup each).

@@ -101,14 +101,16 @@ def n1024():
 def test_n1024_survey_schedules_bit_identical(n1024, monkeypatch):
     """The first 160 survey messages (many first sightings against the 1e7 prior, heavy index
     overlap between consecutive messages) in one persistent device-epoch replay, in the
-    event-synchronised schedule and on one stream: bit-identical states (a chain that carried its
-    own block from chunk to chunk instead of rebuilding it drifted from the HBM Σ here and went
-    non-finite)."""
+    event-synchronised schedule and on one stream, with the chains' rebuild operands staged behind
+    the Σ passes (default) and gathered by the chains themselves (EKF_STAGE=0): bit-identical
+    states (a chain that carried its own block from chunk to chunk instead of rebuilding it drifted
+    from the HBM Σ here and went non-finite)."""
     sc, odom, _ = n1024
     sl = slice(0, 160)
     out = []
-    for env in ({"EKF_DEVSYNC": "1"}, {"EKF_DEVSYNC": "0"}, {"EKF_SERIAL": "1"}):
-        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+    for env in ({"EKF_DEVSYNC": "1"}, {"EKF_DEVSYNC": "0"}, {"EKF_SERIAL": "1"},
+                {"EKF_DEVSYNC": "1", "EKF_STAGE": "0"}):
+        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -175,6 +177,30 @@ def test_n1024_fp32_populated_against_oracle(n1024, env, monkeypatch):
     assert err < 2e-4
     assert np.all(np.isfinite(S32))
     assert np.abs(x32 - xr).max() < 2e-4
+
+
+@pytest.mark.parametrize("devsync", ["1", "0"], ids=["devsync", "events"])
+def test_n1024_fp32_staged_rebuild_bit_identical(n1024, devsync, monkeypatch):
+    """configs[2] fp32 (the block patch k_patch_stage writes over the Σ pass's U × U entries, and
+    the stage must see it): 12 circle messages from the survey's state with the rebuild operands
+    staged behind the Σ passes and gathered by the chains (EKF_STAGE=0): bit-identical."""
+    sc, odom, ws = n1024
+    w = sc.n_warm
+    out = []
+    for stage in ("1", "0"):
+        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
+            monkeypatch.delenv(k, raising=False)
+        monkeypatch.setenv("EKF_DEVSYNC", devsync)
+        monkeypatch.setenv("EKF_STAGE", stage)
+        e = pyekf.EKF(n_landmarks=1024, dtype=pyekf.EKF_F32)
+        x, S, tmo, cnt = ws
+        e.set_state(x, S, tmo=tmo, counter=cnt)
+        _replay(e, slice(w, w + 12), sc, odom)
+        out.append(e.state())
+        assert e.status() == 0
+        e.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
 
 
 @pytest.mark.parametrize("dtype", [pyekf.EKF_F32, pyekf.EKF_F64], ids=["f32", "f64"])

@@ -1,5 +1,8 @@
 """Dev tool: phase stamps (s_memtime cycles) of the chain kernel's last chunk, filter 0, in the
-pipelined replay (libekfslam_diag.so; build: make -C ekf-slam_amd diag)."""
+pipelined replay (libekfslam_diag.so; build: make -C ekf-slam_amd diag).
+
+  python tools/chain_stamps.py [N] [f32|f64]   (default 1024 f32: configs[2]'s headline shape —
+  the fp64 survey lap, then fp32 circle messages from its state, as bench.py runs it)"""
 import ctypes as C
 import os
 import sys
@@ -13,28 +16,54 @@ import pyekf  # noqa: E402
 from pyekf import synth  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+DT = sys.argv[2] if len(sys.argv) > 2 else "f32"
 T = 40
-sc = synth.synthetic(N, T) if os.environ.get("STAMPS_MAP") != "populated" else synth.populated(N, T)
+sw = synth.swarm(N, 1, T, seed=20240317, max_markers=16)
+sc = sw.scenario(0)
 odom = pyekf.odometry(sc)
-e = pyekf.EKF(n_landmarks=N)
-e.replay(sc.count[:, None], sc.rel[:, None], odom[:, None], ids=sc.ids[:, None],
-         actions=sc.actions[:, None])
+w = sc.n_warm
+
+
+def replay(e, sl):
+    e.replay(sc.count[sl, None], sc.rel[sl, None], odom[sl, None], ids=sc.ids[sl, None],
+             actions=sc.actions[sl, None])
+
+
+e64 = pyekf.EKF(n_landmarks=N)
+replay(e64, slice(0, w))
+if DT == "f32":
+    x, S, cnt = e64.state()
+    tmo = e64.map_odom()
+    e64.close()
+    e = pyekf.EKF(n_landmarks=N, dtype=pyekf.EKF_F32)
+    e.set_state(x, S, tmo=tmo, counter=cnt)
+else:
+    e = e64
+replay(e, slice(w, w + T))
 e.sync()
+assert e.status() == 0
 L = pyekf.lib()
-st = (C.c_ulonglong * 256)()
+st = (C.c_ulonglong * 2048)()
 L.ekf_diag_stamps.argtypes = [C.c_void_p, C.c_int]
-assert L.ekf_diag_stamps(st, 256) == 0
-s = np.array(st[:], dtype=np.int64)
+assert L.ekf_diag_stamps(st, 2048) == 0
+ring = np.array(st[:], dtype=np.int64).reshape(4, 512)
+# the ring holds the last four chunks; WHICH=1 (default) the one before the last (it rebuilt the
+# last chunk's block: the steady state), 0 the last
+order = np.argsort(ring[:, 0])[::-1]
+s = ring[order[int(os.environ.get("WHICH", "1"))]]
 t0 = s[0]
-names = {1: "A0", 21: "kLook: gathers landed", 3: "kLook: R, C, D (prev predict)",
+names = {1: "A0", 21: "kLook: loads landed", 3: "kLook: R, C, D (prev predict)",
          7: "kLook: K', M' tiles", 5: "kLook: x[U]", 6: "A1 done (P tiles)",
          2: "predict (steps start)", 12: "steps+final pass", 16: "epi: rec stores issued",
          40: "chunk end"}
+print(f"N={N} {DT}, chunk {-1 - int(os.environ.get('WHICH', '1'))} of {T} messages (cycles from "
+      f"the chunk's stamp 0); chunk starts of the ring, relative: {sorted(ring[:, 0] - ring[:, 0].min())}")
 for k in (1, 21, 3, 7, 5, 6, 2, 12, 16, 40):
     print(f"{names[k]:24s} {s[k] - t0:8d}")
-m = int(sc.count[-1])
-steps = [s[64 + 8 * c] - t0 for c in range(m)]
+m = int(sc.count[w + T - 1 - int(os.environ.get("WHICH", "1"))])
+steps = [int(s[64 + 8 * c] - t0) for c in range(m)]
 print("step starts:", steps)
+print("mean step:", (steps[-1] - steps[0]) / max(m - 1, 1))
 for c in (0, 1, m // 2, m - 2):
     b = 64 + 8 * c
     d = [s[b + k + 1] - s[b + k] for k in range(6)]
