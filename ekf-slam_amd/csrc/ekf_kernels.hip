@@ -750,15 +750,18 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         xr[k] = pk[k];
         xq[k] = pm[k];
       }
-      {
-        const int l0 = more ? nx : 0;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const double mq0 = readlane_f64(mp0, l0 + j), mq1 = readlane_f64(mp1, l0 + j);
-          const double kq0 = readlane_f64(kp0, l0 + j), kq1 = readlane_f64(kp1, l0 + j);
-          xr[3 + j] = rank2_sub(rn[j], kp0, kp1, mq0, mq1);
-          xq[3 + j] = rank2_sub(qn[j], kq0, kq1, mp0, mp1);
-        }
+      {  // K_{c−1} and M_{c−1} of the nx rows / columns: broadcast LDS reads of what step c−1
+         // stored (the stored values are the registers' values; two reads instead of 8 readlanes)
+        const int l0 = more ? nx : 0, cp = c > 0 ? c - 1 : 0;
+        const double2 mq = *reinterpret_cast<const double2*>(&sh.MU[cp][l0][0]);
+        const double2 mq2 = *reinterpret_cast<const double2*>(&sh.MU[cp][l0 + 1][0]);
+        const double2 kq = *reinterpret_cast<const double2*>(&sh.KU[cp][l0][0]);
+        const double2 kq2 = *reinterpret_cast<const double2*>(&sh.KU[cp][l0 + 1][0]);
+        const bool p0 = c > 0;  // step 0: kp = mp = 0, rank2_sub(v, 0, 0, 0, 0) = v
+        xr[3] = rank2_sub(rn[0], kp0, kp1, p0 ? mq.x : 0.0, p0 ? mq.y : 0.0);
+        xr[4] = rank2_sub(rn[1], kp0, kp1, p0 ? mq2.x : 0.0, p0 ? mq2.y : 0.0);
+        xq[3] = rank2_sub(qn[0], p0 ? kq.x : 0.0, p0 ? kq.y : 0.0, mp0, mp1);
+        xq[4] = rank2_sub(qn[1], p0 ? kq2.x : 0.0, p0 ? kq2.y : 0.0, mp0, mp1);
       }
       EKF_STAMP(66 + 8 * c);
       // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's
@@ -819,20 +822,23 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       lds_publish(&sh.pub, c + 1);
       EKF_STAMP(68 + 8 * c);
       if (more) {
-        geometry(c + 1);
-        // wave 3's step c−1 writes outside this step's cross must land before this cross update
-        // overwrites the nx columns / rows (waited for above already when c + 2 < m)
-        if (c + 2 >= m) lds_wait_ge(&sh.pdone, c);
-        // K and M of the five Bx rows / columns, from their lanes
+        // K and M of the five Bx rows / columns: broadcast LDS reads of what this step stored
+        // above (issued before geometry(c + 1), so its latency hides; ds_read_b128 each)
         double kx0[5], kx1[5], mx0[5], mx1[5];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
           const int l = k < 3 ? k : nx + k - 3;
-          kx0[k] = readlane_f64(K0, l);
-          kx1[k] = readlane_f64(K1, l);
-          mx0[k] = readlane_f64(mm0, l);
-          mx1[k] = readlane_f64(mm1, l);
+          const double2 kk = *reinterpret_cast<const double2*>(&sh.KU[c][l][0]);
+          const double2 mk = *reinterpret_cast<const double2*>(&sh.MU[c][l][0]);
+          kx0[k] = kk.x;
+          kx1[k] = kk.y;
+          mx0[k] = mk.x;
+          mx1[k] = mk.y;
         }
+        geometry(c + 1);
+        // wave 3's step c−1 writes outside this step's cross must land before this cross update
+        // overwrites the nx columns / rows (waited for above already when c + 2 < m)
+        if (c + 2 >= m) lds_wait_ge(&sh.pdone, c);
         // all rows × Bx columns: next step's pk
 #pragma unroll
         for (int k = 0; k < 5; ++k) {

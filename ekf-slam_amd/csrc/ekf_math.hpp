@@ -92,10 +92,10 @@ __device__ __forceinline__ bool inv2(const double* A, double* o) {
   return isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
 }
 
-// v − (k0·m0 + k1·m1) with one fixed evaluation order, so a value rebuilt on the fly from the
-// previous buffer is bit-identical to the one the block update stores.
+// v − k0·m0 − k1·m1 with one fixed evaluation order (two FMAs), so a value rebuilt on the fly
+// from the previous buffer is bit-identical to the one the block update stores.
 __device__ __forceinline__ double rank2_sub(double v, double k0, double k1, double m0, double m1) {
-  return v - fma(k0, m0, k1 * m1);
+  return fma(-k1, m1, fma(-k0, m0, v));
 }
 
 // geom.hpp's compose / inverse with one sincos (one argument reduction for both) — the same
