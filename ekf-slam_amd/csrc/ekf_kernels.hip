@@ -128,8 +128,8 @@ struct ChainShared {
   double col0raw[kMaxU];  // Σ_in[u_a][0]
   double xU[1][kMaxU];    // x[U], owned by wave 0 during the corrections
   double P[1][kMaxU][kMaxU + 1];    // Σ[U,U] (rows all, columns live)
-  double Phi[1][kMaxU][kMaxU + 1];  // row map: r_c[U] = r_0[U]·Φ_c   (identity at c = 0)
-  double Psi[1][kMaxU][kMaxU + 1];  // column map: c_c[U] = Ψ_c·c_0[U] (identity at c = 0)
+  double Cz[kMaxChunk][4];  // wave 1, step c: C_k = M_k[:, pA_c]·Hᵀ·S⁻¹ (2×2) for k < c
+  double Dy[kMaxChunk][4];  // wave 2, step c: D_k = H·K_k[pA_c] (2×2) for k < c
   double KU[kMaxChunk][kMaxU][2];
   double MU[kMaxChunk][kMaxU][2];
   double Z[kMaxU][kZC + 1];      // K_c[i] = r_0(i)[U] · Z[:, 2c..2c+1]
@@ -228,6 +228,251 @@ __device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
   while (__builtin_amdgcn_readfirstlane(
              __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < v)
     __builtin_amdgcn_s_sleep(1);
+}
+
+// Wave 0's corrections (see k_chain, A2): a function of its own, so that its register allocation
+// is not the one of the kernel's four wave programs together (the shared allocation spilled
+// SGPRs, and their reloads sat in this loop). LDS through address-space-3 references.
+typedef __attribute__((address_space(3))) ChainShared LdsChain;
+typedef __attribute__((address_space(3))) const MsgDesc LdsDesc;
+typedef __attribute__((address_space(3))) double ldsd;
+__device__ __forceinline__ void lds_publish3(__attribute__((address_space(3))) int* flag, int v) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait_ge3(const __attribute__((address_space(3))) int* flag,
+                                             int v) {
+  while (__builtin_amdgcn_readfirstlane(
+             __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < v)
+    __builtin_amdgcn_s_sleep(1);
+}
+
+__device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int nu, bool joseph,
+                                         double r_noise, unsigned seq) {
+  LdsChain& sh = *shp;
+  LdsDesc& d = *dp;
+  const int lane = threadIdx.x & 63;
+  (void)seq;  // (diagnostic stamps)
+  // Lane ℓ carries row ℓ of the step's block columns (pk = Σ[ℓ, pA]) and column ℓ of its block
+  // rows (pm = Σ[pA, ℓ]) in registers from one step to the next: the cross update of step c
+  // produces exactly step c+1's pk (and pm for the later columns). S needs no block read:
+  // (Σ·Hᵀ)[ℓ] is the first half of K anyway, and S = H·(Σ·Hᵀ)[pA] takes five lanes' values by
+  // v_readlane. The pose / landmark x of a step come by v_readlane from the lane that updated
+  // them. Lanes ≥ |U| carry a clamped row and never store.
+  const int lr = lane < kMaxU ? lane : kMaxU - 1;
+  const int ul = sh.u[lr];
+  double pk[5], pm[5];
+  double xl = sh.xU[0][lr];
+#pragma unroll
+  for (int a = 0; a < 5; ++a) {
+    const int col = a < 3 ? a : 3 + a - 3;  // pA of step 0 = {0, 1, 2, 3, 4}
+    pk[a] = sh.P[0][lr][col];
+    pm[a] = sh.P[0][col][lr];
+  }
+  // Look-ahead operands of the next marker's cross (see the step): rn = Σ[ℓ, nx..nx+1] and
+  // qn = Σ[nx..nx+1, ℓ] one step old, and the previous step's K (kp) and M (mp) of this lane.
+  double rn[2], qn[2], kp0 = 0.0, kp1 = 0.0, mp0 = 0.0, mp1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = min(5 + j, kMaxU - 1);
+    rn[j] = sh.P[0][lr][col];
+    qn[j] = sh.P[0][col][lr];
+  }
+  // A step's geometry (first sighting, ẑ, H) needs only x after the step before. It is computed
+  // right after that step's state update, ahead of the step's cross update, so the two
+  // independent chains (f64 ALU vs LDS round trips) interleave in one basic block.
+  double lx = 0.0, ly = 0.0, H0[5], H1[5], zhat[2], braw = 0.0;
+  bool init = false, bok = true;
+  auto geometry = [&](int c) {
+    const int pj = 3 + 2 * c;
+    const double pose[3] = {readlane_f64(xl, 0), readlane_f64(xl, 1), readlane_f64(xl, 2)};
+    lx = readlane_f64(xl, pj);
+    ly = readlane_f64(xl, pj + 1);
+    init = false;
+    if (!sh.skip[c] && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
+      init = true;
+      const double z0 = d.z[c][0], z1 = d.z[c][1];
+      lx = pose[1] + z0 * cos(z1 + pose[0]);
+      ly = pose[2] + z0 * sin(z1 + pose[0]);
+    }
+    range_bearing(pose, lx, ly, zhat, H0, H1, &braw, &bok);
+  };
+  if (m > 0) geometry(0);
+  for (int c = 0; c < m; ++c) {
+    const int pj = 3 + 2 * c, nx = pj + 2;
+    const bool more = c + 1 < m;
+    EKF_STAMP(64 + 8 * c);
+    const double z0 = d.z[c][0], z1 = d.z[c][1];
+    bool sk = sh.skip[c] != 0;
+    double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0, Sm_keep[4];
+    if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
+    EKF_STAMP(65 + 8 * c);
+    // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]
+    double ka = 0.0, kb = 0.0, mm0 = 0.0, mm1 = 0.0;
+#pragma unroll
+    for (int a = 0; a < 5; ++a) {
+      ka += pk[a] * H0[a];
+      kb += pk[a] * H1[a];
+      mm0 += H0[a] * pm[a];
+      mm1 += H1[a] * pm[a];
+    }
+    {
+      double Sm[4] = {0.0, 0.0, 0.0, 0.0};  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:252)
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        const int l = a < 3 ? a : pj + a - 3;
+        const double ta = readlane_f64(ka, l), tb = readlane_f64(kb, l);
+        Sm[0] += H0[a] * ta;
+        Sm[1] += H0[a] * tb;
+        Sm[2] += H1[a] * ta;
+        Sm[3] += H1[a] * tb;
+      }
+      Sm[0] += r_noise;
+      Sm[3] += r_noise;
+      for (int k = 0; k < 4; ++k) Sm_keep[k] = Sm[k];
+      if (!sk && inv2(Sm, Si)) {
+        nv0 = z0 - zhat[0];
+        bool nok;
+        const double nn = normalize_angle_near(z1 - zhat[1], &nok);
+        nv1 = nok ? nn : normalize_angle(z1 - zhat[1]);
+      } else {
+        if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every lane
+        sk = true;
+      }
+    }
+    if (sk) {
+#pragma unroll
+      for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
+      Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
+      nv0 = nv1 = 0.0;
+      ka = kb = mm0 = mm1 = 0.0;
+    }
+    // The next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}) after step c−1. Pose columns /
+    // rows: pk / pm (pA ⊃ pose). The nx columns / rows were read one step back (rn / qn, after
+    // step c−2) and get step c−1's rank-2 term here from registers: K_{c−1} of this lane (kp)
+    // and of the nx rows (v_readlane), M_{c−1} of this column (mp) and of the nx columns
+    // (v_readlane) — the writers' expression, operands and order (wave 3's, or this wave's cross
+    // update), so the same bits. Step 0 has kp = mp = 0: rank2_sub(v, 0, 0, 0, 0) = v.
+    double xr[5], xq[5];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      xr[k] = pk[k];
+      xq[k] = pm[k];
+    }
+    {  // K_{c−1} and M_{c−1} of the nx rows / columns: broadcast LDS reads of what step c−1
+       // stored (the stored values are the registers' values; two reads instead of 8 readlanes)
+      const int l0 = more ? nx : 0, cp = c > 0 ? c - 1 : 0;
+      const double mqx = sh.MU[cp][l0][0], mqy = sh.MU[cp][l0][1];
+      const double mq2x = sh.MU[cp][l0 + 1][0], mq2y = sh.MU[cp][l0 + 1][1];
+      const double kqx = sh.KU[cp][l0][0], kqy = sh.KU[cp][l0][1];
+      const double kq2x = sh.KU[cp][l0 + 1][0], kq2y = sh.KU[cp][l0 + 1][1];
+      const bool p0 = c > 0;  // step 0: kp = mp = 0, rank2_sub(v, 0, 0, 0, 0) = v
+      xr[3] = rank2_sub(rn[0], kp0, kp1, p0 ? mqx : 0.0, p0 ? mqy : 0.0);
+      xr[4] = rank2_sub(rn[1], kp0, kp1, p0 ? mq2x : 0.0, p0 ? mq2y : 0.0);
+      xq[3] = rank2_sub(qn[0], p0 ? kqx : 0.0, p0 ? kqy : 0.0, mp0, mp1);
+      xq[4] = rank2_sub(qn[1], p0 ? kq2x : 0.0, p0 ? kq2y : 0.0, mp0, mp1);
+    }
+    EKF_STAMP(66 + 8 * c);
+    // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's
+    // cross, before this step's cross update writes its Bx rows (wave 3 writes these entries for
+    // step c only after the publish below, whose release waits for the reads)
+    if (c + 2 < m) {
+      lds_wait_ge3(&sh.pdone, c);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        rn[j] = sh.P[0][lr][nx + 2 + j];
+        qn[j] = sh.P[0][nx + 2 + j][lr];
+      }
+    }
+    const int jx = sh.u[pj];
+    EKF_STAMP(67 + 8 * c);
+    const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
+    const double K1 = ka * Si[1] + kb * Si[3];
+    {
+      double xt = xl;
+      if (init) {
+        if (ul == jx) xt = lx;
+        else if (ul == jx + 1) xt = ly;
+      }
+      xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
+      bool tok;                                     // slam.cpp:267 on lane 0, branch-free
+      const double tn = normalize_angle_near(xt, &tok);
+      if (lane == 0) xt = tok ? tn : normalize_angle(xt);
+      xl = xt;
+      *(lane < nu ? &sh.xU[0][lane] : &sh.junk[0][lane]) = xt;
+    }
+    {
+      const bool in = lane < nu, st = lane < kMaxU;
+      ldsd* kd = st ? &sh.KU[c][lane][0] : &sh.junk2[lane][0];
+      ldsd* md = st ? &sh.MU[c][lane][0] : &sh.junk2[lane][0];
+      kd[0] = in ? K0 : 0.0;
+      kd[1] = in ? K1 : 0.0;
+      md[0] = in ? mm0 : 0.0;
+      md[1] = in ? mm1 : 0.0;
+      if (joseph) {  // G = Σ·Hᵀ and S for the (ΣHᵀ − K·S)·Kᵀ term (chunks of one marker)
+        ldsd* gd = st ? &sh.GU[lane][0] : &sh.junk2[lane][0];
+        gd[0] = in ? ka : 0.0;
+        gd[1] = in ? kb : 0.0;
+        if (lane == 0)
+          for (int k = 0; k < 4; ++k) sh.Ss[k] = sk ? 0.0 : Sm_keep[k];
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        sh.Hs[c][0][a] = H0[a];
+        sh.Hs[c][1][a] = H1[a];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sh.Sis[c][k] = Si[k];
+      sh.nu[c][0] = nv0;
+      sh.nu[c][1] = nv1;
+    }
+    lds_publish3(&sh.pub, c + 1);
+    EKF_STAMP(68 + 8 * c);
+    if (more) {
+      // K and M of the five Bx rows / columns: broadcast LDS reads of what this step stored
+      // above (issued before geometry(c + 1), so its latency hides; ds_read_b128 each)
+      double kx0[5], kx1[5], mx0[5], mx1[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int l = k < 3 ? k : nx + k - 3;
+        const double kkx = sh.KU[c][l][0], kky = sh.KU[c][l][1];
+        const double mkx = sh.MU[c][l][0], mky = sh.MU[c][l][1];
+        kx0[k] = kkx;
+        kx1[k] = kky;
+        mx0[k] = mkx;
+        mx1[k] = mky;
+      }
+      geometry(c + 1);
+      // wave 3's step c−1 writes outside this step's cross must land before this cross update
+      // overwrites the nx columns / rows (waited for above already when c + 2 < m)
+      if (c + 2 >= m) lds_wait_ge3(&sh.pdone, c);
+      // all rows × Bx columns: next step's pk
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int col = k < 3 ? k : nx + k - 3;
+        pk[k] = rank2_sub(xr[k], K0, K1, mx0[k], mx1[k]);
+        *(lane < nu ? &sh.P[0][lane][col] : &sh.junk[0][lane]) = pk[k];
+      }
+      // Bx rows × every other column (the block is kept whole so that the chunk's final Σ[U,U]
+      // can seed the next chunk): next step's pm there
+      const bool later = lane >= 3 && lane < nu && lane != nx && lane != nx + 1;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int row = k < 3 ? k : nx + k - 3;
+        const double v = rank2_sub(xq[k], kx0[k], kx1[k], mm0, mm1);
+        pm[k] = v;
+        *(later ? &sh.P[0][row][lane] : &sh.junk[0][lane]) = v;
+      }
+      // (the Bx × Bx entries: lane `row` stored the same value as its pk, same operands)
+      kp0 = K0;
+      kp1 = K1;
+      mp0 = mm0;
+      mp1 = mm1;
+    }
+    EKF_STAMP(70 + 8 * c);
+  }
 }
 
 constexpr int kChainThreads = 256;
@@ -644,226 +889,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     pending = 0;
   }
   if (wave == 0) {
-    // Lane ℓ carries row ℓ of the step's block columns (pk = Σ[ℓ, pA]) and column ℓ of its block
-    // rows (pm = Σ[pA, ℓ]) in registers from one step to the next: the cross update of step c
-    // produces exactly step c+1's pk (and pm for the later columns). S needs no block read:
-    // (Σ·Hᵀ)[ℓ] is the first half of K anyway, and S = H·(Σ·Hᵀ)[pA] takes five lanes' values by
-    // v_readlane. The pose / landmark x of a step come by v_readlane from the lane that updated
-    // them. Lanes ≥ |U| carry a clamped row and never store.
-    const int lr = lane < kMaxU ? lane : kMaxU - 1;
-    const int ul = sh.u[lr];
-    double pk[5], pm[5];
-    double xl = sh.xU[0][lr];
-#pragma unroll
-    for (int a = 0; a < 5; ++a) {
-      const int col = a < 3 ? a : 3 + a - 3;  // pA of step 0 = {0, 1, 2, 3, 4}
-      pk[a] = sh.P[0][lr][col];
-      pm[a] = sh.P[0][col][lr];
-    }
-    // Look-ahead operands of the next marker's cross (see the step): rn = Σ[ℓ, nx..nx+1] and
-    // qn = Σ[nx..nx+1, ℓ] one step old, and the previous step's K (kp) and M (mp) of this lane.
-    double rn[2], qn[2], kp0 = 0.0, kp1 = 0.0, mp0 = 0.0, mp1 = 0.0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = min(5 + j, kMaxU - 1);
-      rn[j] = sh.P[0][lr][col];
-      qn[j] = sh.P[0][col][lr];
-    }
-    // A step's geometry (first sighting, ẑ, H) needs only x after the step before. It is computed
-    // right after that step's state update, ahead of the step's cross update, so the two
-    // independent chains (f64 ALU vs LDS round trips) interleave in one basic block.
-    double lx = 0.0, ly = 0.0, H0[5], H1[5], zhat[2], braw = 0.0;
-    bool init = false, bok = true;
-    auto geometry = [&](int c) {
-      const int pj = 3 + 2 * c;
-      const double pose[3] = {readlane_f64(xl, 0), readlane_f64(xl, 1), readlane_f64(xl, 2)};
-      lx = readlane_f64(xl, pj);
-      ly = readlane_f64(xl, pj + 1);
-      init = false;
-      if (!sh.skip[c] && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
-        init = true;
-        const double z0 = d.z[c][0], z1 = d.z[c][1];
-        lx = pose[1] + z0 * cos(z1 + pose[0]);
-        ly = pose[2] + z0 * sin(z1 + pose[0]);
-      }
-      range_bearing(pose, lx, ly, zhat, H0, H1, &braw, &bok);
-    };
-    if (m > 0) geometry(0);
-    for (int c = 0; c < m; ++c) {
-      const int pj = 3 + 2 * c, nx = pj + 2;
-      const bool more = c + 1 < m;
-      EKF_STAMP(64 + 8 * c);
-      const double z0 = d.z[c][0], z1 = d.z[c][1];
-      bool sk = sh.skip[c] != 0;
-      double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0, Sm_keep[4];
-      if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
-      EKF_STAMP(65 + 8 * c);
-      // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]
-      double ka = 0.0, kb = 0.0, mm0 = 0.0, mm1 = 0.0;
-#pragma unroll
-      for (int a = 0; a < 5; ++a) {
-        ka += pk[a] * H0[a];
-        kb += pk[a] * H1[a];
-        mm0 += H0[a] * pm[a];
-        mm1 += H1[a] * pm[a];
-      }
-      {
-        double Sm[4] = {0.0, 0.0, 0.0, 0.0};  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:252)
-#pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          const int l = a < 3 ? a : pj + a - 3;
-          const double ta = readlane_f64(ka, l), tb = readlane_f64(kb, l);
-          Sm[0] += H0[a] * ta;
-          Sm[1] += H0[a] * tb;
-          Sm[2] += H1[a] * ta;
-          Sm[3] += H1[a] * tb;
-        }
-        Sm[0] += A.r;
-        Sm[3] += A.r;
-        for (int k = 0; k < 4; ++k) Sm_keep[k] = Sm[k];
-        if (!sk && inv2(Sm, Si)) {
-          nv0 = z0 - zhat[0];
-          bool nok;
-          const double nn = normalize_angle_near(z1 - zhat[1], &nok);
-          nv1 = nok ? nn : normalize_angle(z1 - zhat[1]);
-        } else {
-          if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every lane
-          sk = true;
-        }
-      }
-      if (sk) {
-#pragma unroll
-        for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
-        Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
-        nv0 = nv1 = 0.0;
-        ka = kb = mm0 = mm1 = 0.0;
-      }
-      // The next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}) after step c−1. Pose columns /
-      // rows: pk / pm (pA ⊃ pose). The nx columns / rows were read one step back (rn / qn, after
-      // step c−2) and get step c−1's rank-2 term here from registers: K_{c−1} of this lane (kp)
-      // and of the nx rows (v_readlane), M_{c−1} of this column (mp) and of the nx columns
-      // (v_readlane) — the writers' expression, operands and order (wave 3's, or this wave's cross
-      // update), so the same bits. Step 0 has kp = mp = 0: rank2_sub(v, 0, 0, 0, 0) = v.
-      double xr[5], xq[5];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        xr[k] = pk[k];
-        xq[k] = pm[k];
-      }
-      {  // K_{c−1} and M_{c−1} of the nx rows / columns: broadcast LDS reads of what step c−1
-         // stored (the stored values are the registers' values; two reads instead of 8 readlanes)
-        const int l0 = more ? nx : 0, cp = c > 0 ? c - 1 : 0;
-        const double2 mq = *reinterpret_cast<const double2*>(&sh.MU[cp][l0][0]);
-        const double2 mq2 = *reinterpret_cast<const double2*>(&sh.MU[cp][l0 + 1][0]);
-        const double2 kq = *reinterpret_cast<const double2*>(&sh.KU[cp][l0][0]);
-        const double2 kq2 = *reinterpret_cast<const double2*>(&sh.KU[cp][l0 + 1][0]);
-        const bool p0 = c > 0;  // step 0: kp = mp = 0, rank2_sub(v, 0, 0, 0, 0) = v
-        xr[3] = rank2_sub(rn[0], kp0, kp1, p0 ? mq.x : 0.0, p0 ? mq.y : 0.0);
-        xr[4] = rank2_sub(rn[1], kp0, kp1, p0 ? mq2.x : 0.0, p0 ? mq2.y : 0.0);
-        xq[3] = rank2_sub(qn[0], p0 ? kq.x : 0.0, p0 ? kq.y : 0.0, mp0, mp1);
-        xq[4] = rank2_sub(qn[1], p0 ? kq2.x : 0.0, p0 ? kq2.y : 0.0, mp0, mp1);
-      }
-      EKF_STAMP(66 + 8 * c);
-      // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's
-      // cross, before this step's cross update writes its Bx rows (wave 3 writes these entries for
-      // step c only after the publish below, whose release waits for the reads)
-      if (c + 2 < m) {
-        lds_wait_ge(&sh.pdone, c);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          rn[j] = sh.P[0][lr][nx + 2 + j];
-          qn[j] = sh.P[0][nx + 2 + j][lr];
-        }
-      }
-      const int jx = sh.u[pj];
-      EKF_STAMP(67 + 8 * c);
-      const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
-      const double K1 = ka * Si[1] + kb * Si[3];
-      {
-        double xt = xl;
-        if (init) {
-          if (ul == jx) xt = lx;
-          else if (ul == jx + 1) xt = ly;
-        }
-        xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
-        bool tok;                                     // slam.cpp:267 on lane 0, branch-free
-        const double tn = normalize_angle_near(xt, &tok);
-        if (lane == 0) xt = tok ? tn : normalize_angle(xt);
-        xl = xt;
-        *(lane < nu ? &sh.xU[0][lane] : &sh.junk[0][lane]) = xt;
-      }
-      {
-        const bool in = lane < nu, st = lane < kMaxU;
-        double* kd = st ? &sh.KU[c][lane][0] : &sh.junk2[lane][0];
-        double* md = st ? &sh.MU[c][lane][0] : &sh.junk2[lane][0];
-        kd[0] = in ? K0 : 0.0;
-        kd[1] = in ? K1 : 0.0;
-        md[0] = in ? mm0 : 0.0;
-        md[1] = in ? mm1 : 0.0;
-        if (joseph) {  // G = Σ·Hᵀ and S for the (ΣHᵀ − K·S)·Kᵀ term (chunks of one marker)
-          double* gd = st ? &sh.GU[lane][0] : &sh.junk2[lane][0];
-          gd[0] = in ? ka : 0.0;
-          gd[1] = in ? kb : 0.0;
-          if (lane == 0)
-            for (int k = 0; k < 4; ++k) sh.Ss[k] = sk ? 0.0 : Sm_keep[k];
-        }
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          sh.Hs[c][0][a] = H0[a];
-          sh.Hs[c][1][a] = H1[a];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) sh.Sis[c][k] = Si[k];
-        sh.nu[c][0] = nv0;
-        sh.nu[c][1] = nv1;
-      }
-      lds_publish(&sh.pub, c + 1);
-      EKF_STAMP(68 + 8 * c);
-      if (more) {
-        // K and M of the five Bx rows / columns: broadcast LDS reads of what this step stored
-        // above (issued before geometry(c + 1), so its latency hides; ds_read_b128 each)
-        double kx0[5], kx1[5], mx0[5], mx1[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const int l = k < 3 ? k : nx + k - 3;
-          const double2 kk = *reinterpret_cast<const double2*>(&sh.KU[c][l][0]);
-          const double2 mk = *reinterpret_cast<const double2*>(&sh.MU[c][l][0]);
-          kx0[k] = kk.x;
-          kx1[k] = kk.y;
-          mx0[k] = mk.x;
-          mx1[k] = mk.y;
-        }
-        geometry(c + 1);
-        // wave 3's step c−1 writes outside this step's cross must land before this cross update
-        // overwrites the nx columns / rows (waited for above already when c + 2 < m)
-        if (c + 2 >= m) lds_wait_ge(&sh.pdone, c);
-        // all rows × Bx columns: next step's pk
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const int col = k < 3 ? k : nx + k - 3;
-          pk[k] = rank2_sub(xr[k], K0, K1, mx0[k], mx1[k]);
-          *(lane < nu ? &sh.P[0][lane][col] : &sh.junk[0][lane]) = pk[k];
-        }
-        // Bx rows × every other column (the block is kept whole so that the chunk's final Σ[U,U]
-        // can seed the next chunk): next step's pm there
-        const bool later = lane >= 3 && lane < nu && lane != nx && lane != nx + 1;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-          const int row = k < 3 ? k : nx + k - 3;
-          const double v = rank2_sub(xq[k], kx0[k], kx1[k], mm0, mm1);
-          pm[k] = v;
-          *(later ? &sh.P[0][row][lane] : &sh.junk[0][lane]) = v;
-        }
-        // (the Bx × Bx entries: lane `row` stored the same value as its pk, same operands)
-        kp0 = K0;
-        kp1 = K1;
-        mp0 = mm0;
-        mp1 = mm1;
-      }
-      EKF_STAMP(70 + 8 * c);
-    }
+    chain_wave0((LdsChain*)(&sh), (LdsDesc*)(&d), m, nu, joseph, A.r, seq);
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
     // lane → column 3+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
     const int hb = lane & 31, hr = lane >> 5;
@@ -893,15 +919,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       lds_publish(&sh.pdone, c + 1);
       EKF_STAMPT(193 + 2 * c, 192);
     }
-  } else if (wave == 1) {  // Z_c and Φ (live columns)
-    const int hb = lane & 31, hr = lane >> 5;
-    // The record parity this chunk writes was last written two chunks back: the prologue's poll
-    // (that chunk's Σ-pass epoch) has made the bulk stream done with it. Z_c goes to the record as
-    // soon as it is computed (write-through, off the chain's path).
-    for (int e = lane; e < kMaxU * (kMaxU + 1); e += 64) {  // Φ = I
-      const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
-      (&sh.Phi[0][0][0])[e] = a == b ? 1.0 : 0.0;
-    }
+  } else if (wave == 1) {  // Z_c: K_c[i] = r_0(i)·Z_c for every row i
+    // Σ_c[i, pA_c] = r_0(i)·(E_c − Σ_{k<c} Z_k·M_k[:, pA_c]) (E_c selects the positions pA_c), so
+    // Z_c = E_c·G − Σ_{k<c} Z_k·C_k with G = Hᵀ·S⁻¹ (5×2) and C_k = M_k[:, pA_c]·G (2×2): lane k
+    // forms C_k, lane i its row of Z_c — 4c FMAs a row instead of a |U|×|U| row map updated per
+    // step. The record parity this chunk writes was last written two chunks back: the prologue's
+    // poll (that chunk's Σ-pass epoch) has made the bulk stream done with it. Z_c goes to the
+    // record as soon as it is computed (write-through, off the chain's path).
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     const __amdgpu_buffer_rsrc_t rr =
         __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
@@ -915,104 +939,139 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         st_wt(&rec->Z[b][k], 0.0);
       }
     }
+    const int li = lane < kMaxU ? lane : kMaxU - 1;
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
-      const int pA[5] = {0, 1, 2, pj, pj + 1};
-      if (lane < kMaxU) {
-        double Z0 = 0.0, Z1 = 0.0, V0 = 0.0, V1 = 0.0;
-        if (lane < nu) {
-          double pa = 0.0, pb = 0.0;
+      double H0[5], H1[5], Si[4], G0[5], G1[5];
 #pragma unroll
-          for (int a = 0; a < 5; ++a) {
-            const double w = sh.Phi[0][lane][pA[a]];
-            pa += w * sh.Hs[c][0][a];
-            pb += w * sh.Hs[c][1][a];
-          }
-          Z0 = pa * sh.Sis[c][0] + pb * sh.Sis[c][2];
-          Z1 = pa * sh.Sis[c][1] + pb * sh.Sis[c][3];
-          if (joseph) {  // V = W − Z·S with W = Φ[:, pA]·Hᵀ: r₀(i)·V = (ΣHᵀ − K·S)[i]
-            V0 = pa - (Z0 * sh.Ss[0] + Z1 * sh.Ss[2]);
-            V1 = pb - (Z0 * sh.Ss[1] + Z1 * sh.Ss[3]);
-          }
-        }
-        sh.Z[lane][2 * c] = Z0;
-        sh.Z[lane][2 * c + 1] = Z1;
-        st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
-        if (joseph) {
-          sh.Z[lane][2] = V0;
-          sh.Z[lane][3] = V1;
-          st_wt2(rr, oZ + 8 * (kZC * lane + 2), V0, V1);
-        }
+      for (int a = 0; a < 5; ++a) {
+        H0[a] = sh.Hs[c][0][a];
+        H1[a] = sh.Hs[c][1][a];
       }
-      if (c + 1 < m) {
-        const int live = 3 + (nu - pj - 2);
-        for (int bi = hb; bi < live; bi += 32) {  // Φ[a][b] −= Z_c[a]·M_c[b], all rows a
-          const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
-          const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
-          double pv[18], z0[18], z1[18];
 #pragma unroll
-          for (int i = 0; i < 18; ++i) {
-            const int a = min(hr + 2 * i, kMaxU - 1);
-            pv[i] = sh.Phi[0][a][b];
-            z0[i] = sh.Z[a][2 * c];
-            z1[i] = sh.Z[a][2 * c + 1];
-          }
+      for (int k = 0; k < 4; ++k) Si[k] = sh.Sis[c][k];
 #pragma unroll
-          for (int i = 0; i < 18; ++i) {
-            const int a = hr + 2 * i;
-            if (a < nu) sh.Phi[0][a][b] = rank2_sub(pv[i], z0[i], z1[i], mb0, mb1);
+      for (int a = 0; a < 5; ++a) {
+        G0[a] = H0[a] * Si[0] + H1[a] * Si[2];
+        G1[a] = H0[a] * Si[1] + H1[a] * Si[3];
+      }
+      {  // lane k < c: C_k (lanes ≥ c store to a junk slot: no divergent branch)
+        const int k = lane < c ? lane : 0;
+        double m0[5], m1[5];
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          const int pa = a < 3 ? a : pj + a - 3;
+          m0[a] = sh.MU[k][pa][0];
+          m1[a] = sh.MU[k][pa][1];
+        }
+        double c00 = 0.0, c01 = 0.0, c10 = 0.0, c11 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          c00 = fma(m0[a], G0[a], c00);
+          c01 = fma(m0[a], G1[a], c01);
+          c10 = fma(m1[a], G0[a], c10);
+          c11 = fma(m1[a], G1[a], c11);
+        }
+        double* cd = lane < c ? &sh.Cz[lane][0] : &sh.junk[1][0];
+        cd[0] = c00;
+        cd[1] = c01;
+        cd[2] = c10;
+        cd[3] = c11;
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: LDS keeps its order)
+      {  // row li of Z_c
+        const int pos = li < 3 ? li : (li == pj ? 3 : (li == pj + 1 ? 4 : -1));
+        double z0 = 0.0, z1 = 0.0, W0 = 0.0, W1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          z0 = pos == a ? G0[a] : z0;
+          z1 = pos == a ? G1[a] : z1;
+          W0 = pos == a ? H0[a] : W0;
+          W1 = pos == a ? H1[a] : W1;
+        }
+        for (int k = 0; k < c; ++k) {
+          const double zk0 = sh.Z[li][2 * k], zk1 = sh.Z[li][2 * k + 1];
+          const double c00 = sh.Cz[k][0], c01 = sh.Cz[k][1], c10 = sh.Cz[k][2], c11 = sh.Cz[k][3];
+          z0 = fma(-zk1, c10, fma(-zk0, c00, z0));
+          z1 = fma(-zk1, c11, fma(-zk0, c01, z1));
+        }
+        const bool in = lane < nu;
+        const double Z0 = in ? z0 : 0.0, Z1 = in ? z1 : 0.0;
+        if (lane < kMaxU) {
+          sh.Z[lane][2 * c] = Z0;
+          sh.Z[lane][2 * c + 1] = Z1;
+          st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
+          if (joseph) {  // V = W − Z·S with W = E·Hᵀ (c = 0): r₀(i)·V = (ΣHᵀ − K·S)[i]
+            const double V0 = in ? W0 - (Z0 * sh.Ss[0] + Z1 * sh.Ss[2]) : 0.0;
+            const double V1 = in ? W1 - (Z0 * sh.Ss[1] + Z1 * sh.Ss[3]) : 0.0;
+            sh.Z[lane][2] = V0;
+            sh.Z[lane][3] = V1;
+            st_wt2(rr, oZ + 8 * (kZC * lane + 2), V0, V1);
           }
         }
       }
     }
-  } else {  // wave 2: Y_c and Ψ (live rows); Y_c to the record as soon as it is computed
-    const int ha = lane & 31, hr = lane >> 5;
-    for (int e = lane; e < kMaxU * (kMaxU + 1); e += 64) {  // Ψ = I
-      const int a = e / (kMaxU + 1), b = e - a * (kMaxU + 1);
-      (&sh.Psi[0][0][0])[e] = a == b ? 1.0 : 0.0;
-    }
+  } else {  // wave 2: Y_c: M_c[:, j] = Y_c·c_0(j) for every column j; Y_c to the record at once
+    // Σ_c[pA_c, j] = (E_cᵀ − Σ_{k<c} K_k[pA_c]·Y_k)·c_0(j), so Y_c = H·E_cᵀ − Σ_{k<c} D_k·Y_k with
+    // D_k = H·K_k[pA_c] (2×2): lane k forms D_k, lane j its column of Y_c.
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     for (int e = lane; e < (kZC - 2 * m) * kMaxU; e += 64)  // rows ≥ 2m of the record's Y are zero
       st_wt(&(&rec->Y[2 * m][0])[e], 0.0);
+    const int lj = lane < kMaxU ? lane : kMaxU - 1;
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
-      const int pA[5] = {0, 1, 2, pj, pj + 1};
-      if (lane < kMaxU) {
-        double y0 = 0.0, y1 = 0.0;
-        if (lane < nu) {
+      double H0[5], H1[5];
 #pragma unroll
-          for (int a = 0; a < 5; ++a) {
-            const double v = sh.Psi[0][pA[a]][lane];
-            y0 += sh.Hs[c][0][a] * v;
-            y1 += sh.Hs[c][1][a] * v;
-          }
-        }
-        sh.Y[2 * c][lane] = y0;
-        sh.Y[2 * c + 1][lane] = y1;
-        st_wt(&rec->Y[2 * c][lane], y0);
-        st_wt(&rec->Y[2 * c + 1][lane], y1);
+      for (int a = 0; a < 5; ++a) {
+        H0[a] = sh.Hs[c][0][a];
+        H1[a] = sh.Hs[c][1][a];
       }
-      if (c + 1 < m) {
-        const int live = 3 + (nu - pj - 2);
-        for (int a = ha; a < nu; a += 32) {  // Ψ[b][a] −= K_c[b]·Y_c[a], live rows b
-          const double ya0 = sh.Y[2 * c][a], ya1 = sh.Y[2 * c + 1][a];
-          double pv[17], k0[17], k1[17];
+      {  // lane k < c: D_k
+        const int k = lane < c ? lane : 0;
+        double k0[5], k1[5];
 #pragma unroll
-          for (int i = 0; i < 17; ++i) {
-            const int bi = hr + 2 * i;
-            const int b = min(bi < 3 ? bi : pj + 2 + (bi - 3), kMaxU - 1);
-            pv[i] = sh.Psi[0][b][a];
-            k0[i] = sh.KU[c][b][0];
-            k1[i] = sh.KU[c][b][1];
-          }
+        for (int a = 0; a < 5; ++a) {
+          const int pa = a < 3 ? a : pj + a - 3;
+          k0[a] = sh.KU[k][pa][0];
+          k1[a] = sh.KU[k][pa][1];
+        }
+        double d00 = 0.0, d01 = 0.0, d10 = 0.0, d11 = 0.0;
 #pragma unroll
-          for (int i = 0; i < 17; ++i) {
-            const int bi = hr + 2 * i;
-            const int b = bi < 3 ? bi : pj + 2 + (bi - 3);
-            if (bi < live) sh.Psi[0][b][a] = rank2_sub(pv[i], k0[i], k1[i], ya0, ya1);
-          }
+        for (int a = 0; a < 5; ++a) {
+          d00 = fma(H0[a], k0[a], d00);
+          d01 = fma(H0[a], k1[a], d01);
+          d10 = fma(H1[a], k0[a], d10);
+          d11 = fma(H1[a], k1[a], d11);
+        }
+        double* dd = lane < c ? &sh.Dy[lane][0] : &sh.junk[2][0];
+        dd[0] = d00;
+        dd[1] = d01;
+        dd[2] = d10;
+        dd[3] = d11;
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      {  // column lj of Y_c
+        const int pos = lj < 3 ? lj : (lj == pj ? 3 : (lj == pj + 1 ? 4 : -1));
+        double y0 = 0.0, y1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          y0 = pos == a ? H0[a] : y0;
+          y1 = pos == a ? H1[a] : y1;
+        }
+        for (int k = 0; k < c; ++k) {
+          const double yk0 = sh.Y[2 * k][lj], yk1 = sh.Y[2 * k + 1][lj];
+          const double d00 = sh.Dy[k][0], d01 = sh.Dy[k][1], d10 = sh.Dy[k][2], d11 = sh.Dy[k][3];
+          y0 = fma(-d01, yk1, fma(-d00, yk0, y0));
+          y1 = fma(-d11, yk1, fma(-d10, yk0, y1));
+        }
+        if (lane < kMaxU) {
+          const bool in = lane < nu;
+          sh.Y[2 * c][lane] = in ? y0 : 0.0;
+          sh.Y[2 * c + 1][lane] = in ? y1 : 0.0;
+          st_wt(&rec->Y[2 * c][lane], in ? y0 : 0.0);
+          st_wt(&rec->Y[2 * c + 1][lane], in ? y1 : 0.0);
         }
       }
     }
