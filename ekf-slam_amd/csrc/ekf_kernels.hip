@@ -307,28 +307,28 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
     double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0, Sm_keep[4];
     if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
     EKF_STAMP(65 + 8 * c);
-    // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]
-    double ka = 0.0, kb = 0.0, mm0 = 0.0, mm1 = 0.0;
-#pragma unroll
-    for (int a = 0; a < 5; ++a) {
-      ka += pk[a] * H0[a];
-      kb += pk[a] * H1[a];
-      mm0 += H0[a] * pm[a];
-      mm1 += H1[a] * pm[a];
-    }
+    // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]. H's shape (range_bearing): H0 = [0, h1, h2, −h1, −h2],
+    // H1 = [−1, g1, g2, −g1, −g2] — a row times H is two FMAs on (v1 − v3, v2 − v4) (exact negations)
+    const double dk1 = pk[1] - pk[3], dk2 = pk[2] - pk[4];
+    const double dm1 = pm[1] - pm[3], dm2 = pm[2] - pm[4];
+    double ka = fma(H0[2], dk2, H0[1] * dk1), kb = fma(H1[2], dk2, fma(H1[1], dk1, -pk[0]));
+    double mm0 = fma(H0[2], dm2, H0[1] * dm1), mm1 = fma(H1[2], dm2, fma(H1[1], dm1, -pm[0]));
     {
-      double Sm[4] = {0.0, 0.0, 0.0, 0.0};  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:252)
+      double Sm[4];  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:252), the same shape
+      {
+        double ta[5], tb[5];
 #pragma unroll
-      for (int a = 0; a < 5; ++a) {
-        const int l = a < 3 ? a : pj + a - 3;
-        const double ta = readlane_f64(ka, l), tb = readlane_f64(kb, l);
-        Sm[0] += H0[a] * ta;
-        Sm[1] += H0[a] * tb;
-        Sm[2] += H1[a] * ta;
-        Sm[3] += H1[a] * tb;
+        for (int a = 0; a < 5; ++a) {
+          const int l = a < 3 ? a : pj + a - 3;
+          ta[a] = readlane_f64(ka, l);
+          tb[a] = readlane_f64(kb, l);
+        }
+        const double ta1 = ta[1] - ta[3], ta2 = ta[2] - ta[4], tb1 = tb[1] - tb[3], tb2 = tb[2] - tb[4];
+        Sm[0] = fma(H0[2], ta2, H0[1] * ta1) + r_noise;
+        Sm[1] = fma(H0[2], tb2, H0[1] * tb1);
+        Sm[2] = fma(H1[2], ta2, fma(H1[1], ta1, -ta[0]));
+        Sm[3] = fma(H1[2], tb2, fma(H1[1], tb1, -tb[0])) + r_noise;
       }
-      Sm[0] += r_noise;
-      Sm[3] += r_noise;
       for (int k = 0; k < 4; ++k) Sm_keep[k] = Sm[k];
       if (!sk && inv2(Sm, Si)) {
         nv0 = z0 - zhat[0];
@@ -366,11 +366,11 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
       const double mq2x = sh.MU[cp][l0 + 1][0], mq2y = sh.MU[cp][l0 + 1][1];
       const double kqx = sh.KU[cp][l0][0], kqy = sh.KU[cp][l0][1];
       const double kq2x = sh.KU[cp][l0 + 1][0], kq2y = sh.KU[cp][l0 + 1][1];
-      const bool p0 = c > 0;  // step 0: kp = mp = 0, rank2_sub(v, 0, 0, 0, 0) = v
-      xr[3] = rank2_sub(rn[0], kp0, kp1, p0 ? mqx : 0.0, p0 ? mqy : 0.0);
-      xr[4] = rank2_sub(rn[1], kp0, kp1, p0 ? mq2x : 0.0, p0 ? mq2y : 0.0);
-      xq[3] = rank2_sub(qn[0], p0 ? kqx : 0.0, p0 ? kqy : 0.0, mp0, mp1);
-      xq[4] = rank2_sub(qn[1], p0 ? kq2x : 0.0, p0 ? kq2y : 0.0, mp0, mp1);
+      // step 0: kp = mp = 0 and the (stale, finite) reads multiply zeros: rank2_sub returns v
+      xr[3] = rank2_sub(rn[0], kp0, kp1, mqx, mqy);
+      xr[4] = rank2_sub(rn[1], kp0, kp1, mq2x, mq2y);
+      xq[3] = rank2_sub(qn[0], kqx, kqy, mp0, mp1);
+      xq[4] = rank2_sub(qn[1], kq2x, kq2y, mp0, mp1);
     }
     EKF_STAMP(66 + 8 * c);
     // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's

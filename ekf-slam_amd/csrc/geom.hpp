@@ -43,8 +43,9 @@ __host__ __device__ inline double normalize_angle_near(double rad, bool* ok) {
   return d <= 0.0 ? d + kPi : d - kPi;
 }
 
-// atan2 in ~45 f64 operations (one division) for the bearing of every EKF step; max error
-// 0.59 ulp for the reduced atan (fitted at 60 digits by tools/fit_atan.py), ≤ 2 ulp overall.
+// atan2 in ~40 f64 operations (one reciprocal) for the bearing of every EKF step; max error
+// 0.59 ulp for the reduced atan polynomial (fitted at 60 digits by tools/fit_atan.py), a few ulp
+// overall (Estrin evaluation and the refined reciprocal each add rounding).
 // ocml's atan2 costs ~190 f64 operations and sits on the correction chain's critical path.
 __host__ __device__ inline double atan2_fast(double y, double x) {
   constexpr double kC[11] = {
@@ -56,12 +57,28 @@ __host__ __device__ inline double atan2_fast(double y, double x) {
   const double num = swap ? ax : ay, den = swap ? ay : ax;  // t = num/den ∈ [0, 1]
   // atan(t) = π/4 + atan((t−1)/(t+1)) above tan(π/8); selects, one division, no branch
   const bool hi = num > 0.41421356237309503 * den;
-  const double tq = (hi ? num - den : num) / (hi ? num + den : (den > 0.0 ? den : 1.0));
+  const double tn = hi ? num - den : num, td = hi ? num + den : (den > 0.0 ? den : 1.0);
+#ifdef __HIP_DEVICE_COMPILE__
+  // reciprocal with two Newton steps (≤ 1 ulp) and a product: 6 operations against the 10 of the
+  // IEEE division sequence on the correction chain
+  double ri = __builtin_amdgcn_rcp(td);
+  ri = fma(ri, fma(-td, ri, 1.0), ri);
+  ri = fma(ri, fma(-td, ri, 1.0), ri);
+  const double tq = tn * ri;
+#else
+  const double tq = tn / td;
+#endif
   const double t = hi || den > 0.0 ? tq : 0.0;
   const double off = hi ? 0.78539816339744831 : 0.0;
   const double z = t * t;
-  double r = kC[10];
-  for (int k = 9; k >= 0; --k) r = fma(r, z, kC[k]);
+  // Estrin's scheme: independent pairs, then powers of z (fewer dependent steps than Horner)
+  const double z2 = z * z, z4 = z2 * z2, z8 = z4 * z4;
+  const double p01 = fma(kC[1], z, kC[0]), p23 = fma(kC[3], z, kC[2]);
+  const double p45 = fma(kC[5], z, kC[4]), p67 = fma(kC[7], z, kC[6]);
+  const double p89 = fma(kC[9], z, kC[8]);
+  const double p03 = fma(p23, z2, p01), p47 = fma(p67, z2, p45);
+  const double p8a = fma(kC[10], z2, p89);
+  const double r = fma(p8a, z8, fma(p47, z4, p03));
   double a = off + fma(t * z, r, t);
   if (swap) a = 1.5707963267948966 - a;
   if (x < 0.0) a = kPi - a;
