@@ -41,6 +41,8 @@ constexpr int kStageOut = 256;  // behind this chunk's Σ pass (k_patch_stage): 
 constexpr int kStageIn = 512;   // kLook chain: read its rebuild operands from StageRec (contiguous)
                                 // instead of gathering them from Σ_in' at the chunk's start
 constexpr int kStW = kMaxU + 1;  // chain block stride (entry e = a·kStW + b)
+constexpr int kPendValid = 1024;  // ChunkRec::flags only: Pend holds the chain's final Σ[U, U]
+                                  // (fp32 chunks with a first sighting or an association)
 
 // One chunk of one message for one filter (uploaded by the host, read by every kernel of the pair).
 struct alignas(16) MsgDesc {

@@ -166,6 +166,7 @@ struct ChainShared {
   unsigned status;
   int pub;    // steps whose K, M, H, S⁻¹ wave 0 has published
   int pdone;  // steps wave 3 has applied outside the cross
+  int any_init;  // a correction of this chunk initialised its landmark (slam.cpp:213-216)
 };
 
 
@@ -291,6 +292,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
     init = false;
     if (!sh.skip[c] && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
       init = true;
+      sh.any_init = 1;
       const double z0 = d.z[c][0], z1 = d.z[c][1];
       lx = pose[1] + z0 * cos(z1 + pose[0]);
       ly = pose[2] + z0 * sin(z1 + pose[0]);
@@ -881,6 +883,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   if (tid == 0) {
     sh.pub = 0;
     sh.pdone = 0;
+    sh.any_init = 0;
   }
   if (pending) drain_stores();
   __syncthreads();
@@ -1078,8 +1081,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
   __syncthreads();
   // fp32 Σ: the last step's rank-2 term on the whole block (earlier steps are applied), the final
-  // Σ[U, U] in fp64, to the record (write-through) for k_patch_stage (the Σ pass's U × U entries)
-  if constexpr (sizeof(T) == 4) {
+  // Σ[U, U] in fp64, to the record (write-through) for k_patch_stage (the Σ pass's U × U entries).
+  // Only a chunk that initialises a landmark has the 1e7 − (1e7 − δ) cancellation the patch is
+  // for (slam.cpp:130's prior has no cross terms; an untouched landmark's rows stay exact): a first
+  // sighting, or an association chunk (its new landmark is written by k_assoc). Other chunks keep
+  // the pass's own values and skip this.
+  const bool pend = sizeof(T) == 4 && (sh.any_init || (d.flags & kNoInit));
+  if (pend) {
     const int c = max(m - 1, 0);
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     for (int e = tid; e < kMaxU * kMaxU; e += blockDim.x) {
@@ -1141,7 +1149,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     if (tid == 0) {
       st_wt(&rec->m, m);
       st_wt(&rec->nu, nu);
-      st_wt(&rec->flags, d.flags);
+      st_wt(&rec->flags, d.flags | (pend ? kPendValid : 0));
       st_wt(&rec->a1, sh.a1);
       st_wt(&rec->a2, sh.a2);
       st_wt(&rec->s00, sh.s00);
@@ -1600,6 +1608,9 @@ __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
   const int f = A.f0 + blockIdx.x;
   const int tid = threadIdx.x;
   const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+  // the chain wrote Pend only for chunks that initialised a landmark (k_chain: `pend`)
+  const bool patch = kPatch && (rec->flags & kPendValid);
+  if (!patch && !stage) return;
   __shared__ int su[kMaxU];
   __shared__ int sfirst[kMaxU];           // position is its index's first in this chunk's U
   __shared__ double spend[kMaxU][kMaxU + 1];
@@ -1608,7 +1619,7 @@ __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
   // ---- one global round trip: the record's block and U, the staged chunks' ids ----
   constexpr int kPer = (kMaxU * kMaxU + 255) / 256;
   double pv[kPer];
-  if (kPatch) {
+  if (patch) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = min(tid + 256 * i, kMaxU * kMaxU - 1);
@@ -1623,7 +1634,7 @@ __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
   const int sm = isp ? d.stg_pm : d.stg_m;
   const int sid = (isp ? d.stg_pids : d.stg_ids)[min(max(sa - 3, 0) >> 1, kMaxChunk - 1)];
   if (tid < kMaxU) su[tid] = myu;
-  if (kPatch) {
+  if (patch) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + 256 * i;
@@ -1648,7 +1659,7 @@ __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
       // k_chain's A0 mapping: marker c → 3 + 2·id (+1), a bad id → slot 0's, padding → 0
       col = (sid < 0 || sid >= A.N ? 3 : 3 + 2 * sid) + ((sa - 3) & 1);
     int fpos = -1;  // the first position of col in this chunk's U = its patched entry
-    if (kPatch) {
+    if (patch) {
 #pragma unroll
       for (int k = kMaxU - 1; k >= 0; --k) fpos = (k < nu && uall[k] == col) ? k : fpos;
     }
@@ -1657,7 +1668,7 @@ __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
   }
   __syncthreads();
   T* S = A.sig[d.parity ^ 1] + f * A.sig_stride;
-  if (kPatch) {
+  if (patch) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + 256 * i, a = e / kMaxU, b = e % kMaxU;
@@ -1673,7 +1684,7 @@ __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
   // the scatter above and is discarded)
   auto val = [&](int r, int fr, int c, int fc) -> T {
     const T g = S[static_cast<size_t>(r) * A.ld + c];
-    return (kPatch && fr >= 0 && fc >= 0) ? static_cast<T>(spend[fr][fc]) : g;
+    return (patch && fr >= 0 && fc >= 0) ? static_cast<T>(spend[fr][fc]) : g;
   };
   constexpr int kSPer = (kStW * kStW + 255) / 256;  // 6
   T od[kSPer], orr[kSPer], oc[kSPer];
