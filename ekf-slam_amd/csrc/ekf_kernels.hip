@@ -757,17 +757,26 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     if (tid < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
       const int u = sh.u[tid];
       int pos = -1;
-      double acc = 0.0;
 #pragma unroll
       for (int k = kMaxU - 1; k >= 0; --k) {
         const bool hit = k < np && sh.pv.u[k] == u;
         pos = hit ? k : pos;
       }
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};  // four partial sums (k mod 4): a 9-deep chain
 #pragma unroll
-      for (int k = 0; k < kMaxU; ++k) acc = fma(sh.pv.R[tid][k], sh.pv.Zx[k], acc);  // R[·][k ≥ |U'|] = 0
-      sh.xU[0][tid] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[tid] + acc;
+      for (int k = 0; k < kMaxU; ++k) acc[k & 3] = fma(sh.pv.R[tid][k], sh.pv.Zx[k], acc[k & 3]);
+      const double r = (acc[0] + acc[1]) + (acc[2] + acc[3]);  // R[·][k ≥ |U'|] = 0
+      sh.xU[0][tid] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[tid] + r;
     }
     if (tid < 3) sh.xpose[tid] = sh.pv.xU[tid];  // pose ∈ U' always
+    if (tid == 192) {  // waves 1–3 have no x[U] rows: the predicted pose (slam.cpp:184-196) here,
+                       // from x' of the pose (= xpose, stored above by wave 0)
+      double a1, a2;
+      const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
+      predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
+      sh.a1 = a1;
+      sh.a2 = a2;
+    }
     __syncthreads();
     EKF_STAMP(5);
     // a Joseph chunk before: its V'·K'ᵀ term as rank 2..3 (K' columns 2..3 are V' = R·Z'[:, 2..3];
@@ -779,12 +788,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         sh.pv.M[2 + k][b] = b < kMaxU ? sh.pv.K[b][k] : 0.0;
       }
       __syncthreads();
-    }
-    if (tid == 192) {  // wave 3 has one P tile fewer: the predicted pose (slam.cpp:184-196) here
-      double a1, a2;
-      predicted_pose(sh.tmo, d, sh.xpose, sh.pose, &a1, &a2);
-      sh.a1 = a1;
-      sh.a2 = a2;
     }
     // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
     // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4)
