@@ -57,6 +57,7 @@ struct ekf_ctx {
   hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
+  bool nb = false;               // EKF_NB=1: the chain's helper waves rebuild the next block
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
   bool defer = false;            // ekf_defer: plan now, upload and launch later
   bool joseph = false;           // ekf_set_joseph (resident: its own kernel; pipeline: kJoseph chunks)
@@ -226,6 +227,7 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
   const bool two = pipelined && !h->serial;
   hipStream_t ms = h->stream, bs = two ? h->bulk : h->stream;
   a.polls = two && h->devsync ? 1 : 0;
+  a.nb = a.polls && h->nb ? 1 : 0;
   if (pipelined && !nolook) {
     // events: a rebuilding (kLook) chain needs the Σ pass two launches back
     if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s0 & 1], 0));
@@ -788,6 +790,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   };
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
   if (const char* e = std::getenv("EKF_SERIAL")) h->serial = std::atoi(e) != 0;
+  if (const char* e = std::getenv("EKF_NB")) h->nb = std::atoi(e) != 0;
   {  // EKF_RESIDENT=0: the HBM pipeline at every size (tests compare the two)
     const char* e = std::getenv("EKF_RESIDENT");
     h->resident = cfg.dtype == EKF_F64 && h->n <= kResidentMaxN && !(e && std::atoi(e) == 0);
@@ -1237,6 +1240,9 @@ int ekf_debug_poison_lds(int device) {
 int ekfslam_diag_read_stamps(unsigned long long* out, int n);  // ekf_kernels.hip
 // dev only (libekfslam_diag.so): the chain kernel's s_memtime stamps of filter 0's last chunk
 int ekf_diag_stamps(unsigned long long* out, int n) { return ekfslam_diag_read_stamps(out, n); }
+extern "C" int ekfslam_diag_read_nb(double* out, unsigned* info);  // ekf_kernels.hip
+// dev only: the helper-rebuilt block vs the prologue's (tools/chain_stamps.py NBCHK=1)
+int ekf_diag_nb(double* out, unsigned* info) { return ekfslam_diag_read_nb(out, info); }
 int ekfslam_res_read_stamps(unsigned long long* out, int n);  // ekf_resident.hip
 // dev only: the resident kernel's stamps (filter flo, thread 0): 6 per correction
 int ekf_diag_res_stamps(unsigned long long* out, int n) { return ekfslam_res_read_stamps(out, n); }

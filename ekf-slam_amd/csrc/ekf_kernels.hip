@@ -47,8 +47,16 @@ __device__ unsigned long long g_stamps[4 * 512];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == (t))                 \
       g_stamps[512 * (seq & 3) + (i)] = __builtin_amdgcn_s_memtime();             \
   } while (0)
+#define EKF_STAMPV(i, v)                                                          \
+  do {                                                                            \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                   \
+      g_stamps[512 * (seq & 3) + (i)] = (v);                                      \
+  } while (0)
 #else
 #define EKF_STAMPT(i, t) \
+  do {                   \
+  } while (0)
+#define EKF_STAMPV(i, v) \
   do {                   \
   } while (0)
 #define EKF_STAMP(i) \
@@ -81,7 +89,7 @@ namespace ekfslam {
     __syncthreads();                                                                \
     if (blockIdx.y == 0) {                                                          \
       for (int e = threadIdx.x; e < kMaxU * (kMaxU + 1); e += blockDim.x)           \
-        (&g_blocks[(seq) & 63][0][0])[e] = (&sh.P[0][0][0])[e];                      \
+        (&g_blocks[(seq) & 63][0][0])[e] = (&P[0][0])[e];                             \
       if (threadIdx.x < kMaxU) g_blockx[(seq) & 63][threadIdx.x] = sh.xU[0][threadIdx.x]; \
     }                                                                               \
     __syncthreads();                                                                \
@@ -91,6 +99,7 @@ namespace ekfslam {
   do {                      \
   } while (0)
 #endif
+
 
 // Diagnostic build only (tools/sigma_bench.hip): s_memrealtime (100 MHz) per Σ-pass workgroup.
 #ifdef EKF_DIAG_STAMPS
@@ -127,7 +136,8 @@ struct ChainShared {
   double row0raw[kMaxU];  // Σ_in[0][u_b]
   double col0raw[kMaxU];  // Σ_in[u_a][0]
   double xU[1][kMaxU];    // x[U], owned by wave 0 during the corrections
-  double P[1][kMaxU][kMaxU + 1];    // Σ[U,U] (rows all, columns live)
+  double P[2][kMaxU][kMaxU + 1];    // Σ[U,U] (rows all, columns live) by chunk parity: waves 1–2
+                                    // rebuild the next chunk's block in the other one
   double Cz[kMaxChunk][4];  // wave 1, step c: C_k = M_k[:, pA_c]·Hᵀ·S⁻¹ (2×2) for k < c
   double Dy[kMaxChunk][4];  // wave 2, step c: D_k = H·K_k[pA_c] (2×2) for k < c
   double KU[kMaxChunk][kMaxU][2];
@@ -167,6 +177,13 @@ struct ChainShared {
   int pub;    // steps whose K, M, H, S⁻¹ wave 0 has published
   int pdone;  // steps wave 3 has applied outside the cross
   int any_init;  // a correction of this chunk initialised its landmark (slam.cpp:213-216)
+  // the next chunk's block, rebuilt by waves 1–2 during this chunk's corrections
+  unsigned built;  // seq + 1 of the chunk whose block the chunk before rebuilt
+  int kdone;       // k-blocks whose K' columns wave 1 has stored
+  int nb_ok1, nb_ok2;  // wave 1 / 2 completed its part (set at their ends)
+  int w1fin;       // wave 1 has decided (wave 2 waits for it before finishing)
+  int un[kMaxU];   // the next chunk's U
+  double c0U2[kMaxU];  // Σ_in[u⁺_a][0] (wave 2's copy)
 };
 
 
@@ -234,6 +251,30 @@ __device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
 // Wave 0's corrections (see k_chain, A2): a function of its own, so that its register allocation
 // is not the one of the kernel's four wave programs together (the shared allocation spilled
 // SGPRs, and their reloads sat in this loop). LDS through address-space-3 references.
+#ifdef EKF_DIAG_STAMPS
+// Diagnostic build only: a chunk whose block waves 1–2 rebuilt runs the prologue's rebuild as well;
+// both versions of R̃, C̃, K', M', P̃ and the vectors (filter 0), kept from the first mismatch on.
+__device__ double g_nb[2][6][kMaxU + 1][kMaxU + 1];
+__device__ unsigned g_nbinfo[8];
+__device__ double g_nbdbg[4][12];  // mismatching chunks, seq of the first, checked chunks, frozen
+__device__ void nb_snapshot(ChainShared& sh, const double (&P)[kMaxU][kMaxU + 1], int w) {
+  for (int e = threadIdx.x; e < (kMaxU + 1) * (kMaxU + 1); e += blockDim.x) {
+    const int a = e / (kMaxU + 1), b = e % (kMaxU + 1);
+    g_nb[w][0][a][b] = a < kMaxU ? sh.pv.R[a][b] : 0.0;
+    g_nb[w][1][a][b] = sh.pv.C[a][b];
+    g_nb[w][2][a][b] = a < kMaxU && b < kZC ? sh.pv.K[a][b] : 0.0;
+    g_nb[w][3][a][b] = a < kZC ? sh.pv.M[a][b] : 0.0;
+    g_nb[w][4][a][b] = a < kMaxU ? P[a][b] : 0.0;
+    double v = 0.0;
+    if (b < kMaxU) v = a == 0 ? sh.pv.xU[b] : a == 1 ? sh.pv.Zx[b] : a == 2 ? sh.pv.xg[b] : 0.0;
+    if (a == 3 && b < 3) v = sh.tmo[b];
+    if (b < kMaxU && a >= 4 && a <= 8)
+      v = a == 4 ? sh.pv.r0U[b] : a == 5 ? sh.pv.c0U[b] : a == 6 ? sh.pv.r0P[b] : a == 7 ? sh.pv.c0P[b] : sh.c0U2[b];
+    g_nb[w][5][a][b] = v;
+  }
+}
+#endif
+
 typedef __attribute__((address_space(3))) ChainShared LdsChain;
 typedef __attribute__((address_space(3))) const MsgDesc LdsDesc;
 typedef __attribute__((address_space(3))) double ldsd;
@@ -248,8 +289,8 @@ __device__ __forceinline__ void lds_wait_ge3(const __attribute__((address_space(
     __builtin_amdgcn_s_sleep(1);
 }
 
-__device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int nu, bool joseph,
-                                         double r_noise, unsigned seq) {
+__device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int m, int nu,
+                                         bool joseph, double r_noise, unsigned seq) {
   LdsChain& sh = *shp;
   LdsDesc& d = *dp;
   const int lane = threadIdx.x & 63;
@@ -267,8 +308,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
 #pragma unroll
   for (int a = 0; a < 5; ++a) {
     const int col = a < 3 ? a : 3 + a - 3;  // pA of step 0 = {0, 1, 2, 3, 4}
-    pk[a] = sh.P[0][lr][col];
-    pm[a] = sh.P[0][col][lr];
+    pk[a] = sh.P[pb][lr][col];
+    pm[a] = sh.P[pb][col][lr];
   }
   // Look-ahead operands of the next marker's cross (see the step): rn = Σ[ℓ, nx..nx+1] and
   // qn = Σ[nx..nx+1, ℓ] one step old, and the previous step's K (kp) and M (mp) of this lane.
@@ -276,8 +317,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = min(5 + j, kMaxU - 1);
-    rn[j] = sh.P[0][lr][col];
-    qn[j] = sh.P[0][col][lr];
+    rn[j] = sh.P[pb][lr][col];
+    qn[j] = sh.P[pb][col][lr];
   }
   // A step's geometry (first sighting, ẑ, H) needs only x after the step before. It is computed
   // right after that step's state update, ahead of the step's cross update, so the two
@@ -382,8 +423,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
       lds_wait_ge3(&sh.pdone, c);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        rn[j] = sh.P[0][lr][nx + 2 + j];
-        qn[j] = sh.P[0][nx + 2 + j][lr];
+        rn[j] = sh.P[pb][lr][nx + 2 + j];
+        qn[j] = sh.P[pb][nx + 2 + j][lr];
       }
     }
     const int jx = sh.u[pj];
@@ -455,7 +496,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
       for (int k = 0; k < 5; ++k) {
         const int col = k < 3 ? k : nx + k - 3;
         pk[k] = rank2_sub(xr[k], K0, K1, mx0[k], mx1[k]);
-        *(lane < nu ? &sh.P[0][lane][col] : &sh.junk[0][lane]) = pk[k];
+        *(lane < nu ? &sh.P[pb][lane][col] : &sh.junk[0][lane]) = pk[k];
       }
       // Bx rows × every other column (the block is kept whole so that the chunk's final Σ[U,U]
       // can seed the next chunk): next step's pm there
@@ -465,7 +506,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
         const int row = k < 3 ? k : nx + k - 3;
         const double v = rank2_sub(xq[k], kx0[k], kx1[k], mm0, mm1);
         pm[k] = v;
-        *(later ? &sh.P[0][row][lane] : &sh.junk[0][lane]) = v;
+        *(later ? &sh.P[pb][row][lane] : &sh.junk[0][lane]) = v;
       }
       // (the Bx × Bx entries: lane `row` stored the same value as its pk, same operands)
       kp0 = K0;
@@ -474,6 +515,244 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int m, int 
       mp1 = mm1;
     }
     EKF_STAMP(70 + 8 * c);
+  }
+}
+
+
+// ---- the next chunk's block, rebuilt by k_chain's waves 1–2 during this chunk's corrections ----
+// (device-epoch groups, when the staged operands land in time.) The prologue's rebuild, spread
+// over the corrections: the same formulas and the same MFMA sequence (K' and M' tiles over U',
+// then P̃ −= K'·M' per k-block of 4 factor columns = 2 corrections, in order), so the block is
+// bit-identical to the one the prologue builds. LDS through address-space-3 pointers.
+constexpr int kStE = (kStW * kStW + 63) / 64;  // 21 block entries per lane of one wave
+
+// the next chunk's U (k_chain A0's mapping: bad id → slot 0's columns, padding → 0)
+__device__ __forceinline__ int nb_ucol(LdsDesc* nd, int nun, int a, int N) {
+  if (a < 3) return a;
+  if (a >= nun) return 0;
+  const int id = nd->ids[(a - 3) >> 1];
+  return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
+}
+
+// the next chunk's staged operands have landed: the Σ-pass epoch it waits for (k_chain's `need`)
+__device__ __forceinline__ bool nb_landed(const unsigned* sync, unsigned seq) {
+  return static_cast<int>(__builtin_amdgcn_readfirstlane(epoch_load(sync + kSyncSigma)) - seq) >= 0;
+}
+
+// Wave 1: R̃ = pred(Σ_in[U⁺, U]) into pv.R (the prologue's R), x_in[U⁺] into pv.xg. U⁺ = the next
+// chunk's U (nun entries), U = this chunk's (nu); the predict is this chunk's (first, a1, a2).
+template <typename T>
+__device__ __noinline__ void nb_intake_r(LdsChain* sh, LdsDesc* nd, const StageRec<T>* sgn, int nu,
+                                         int nun, int first, double q, int N) {
+  // lanes exchange values through LDS here: a convergent operation keeps the function convergent,
+  // so the compiler cannot split its call over divergent paths of the caller (it did, around a
+  // one-lane branch, and lane 0 ran the function alone)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int lane = threadIdx.x & 63;
+  const int t = min(lane, kMaxU - 1);
+  T vr[kStE];  // every load in flight at once: one round trip
+#pragma unroll
+  for (int i = 0; i < kStE; ++i) vr[i] = sgn->v[1][min(lane + 64 * i, kStW * kStW - 1)];
+  const double s00 = sgn->r0u[0];
+  const double r0p = sgn->r0p[t], c0u = sgn->c0u[t], xg = sgn->xg[t];
+  if (lane < kMaxU) {
+    sh->pv.r0P[lane] = r0p;
+    sh->pv.c0U[lane] = c0u;
+    sh->pv.xg[lane] = xg;
+    sh->un[lane] = nb_ucol(nd, nun, lane, N);
+  }
+#ifdef EKF_DIAG_STAMPS
+  if (blockIdx.y == 0 && lane < 3 && g_nbinfo[7] == 0) {
+    g_nbdbg[3][4 * lane] = r0p;
+    g_nbdbg[3][4 * lane + 1] = c0u;
+    g_nbdbg[3][4 * lane + 2] = s00;
+    g_nbdbg[3][4 * lane + 3] = sh->pv.c0U[0];
+  }
+#endif
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const double a1 = sh->a1, a2 = sh->a2;
+#pragma unroll
+  for (int i = 0; i < kStE; ++i) {
+    const int e = lane + 64 * i, a = e / kStW, b = e - a * kStW;
+    if (e < kStW * kStW && a < nun) {
+      double v = 0.0;
+      if (b < nu) {
+        v = static_cast<double>(vr[i]);
+        if (first) {
+          const int ua = sh->un[a], ub = sh->u[b];
+          const double ai = alpha_of(ua, a1, a2), ak = alpha_of(ub, a1, a2);
+#ifdef EKF_DIAG_STAMPS
+          if (blockIdx.y == 0 && (e == 1 || e == 37 || e == 36) && g_nbinfo[7] == 0) {
+            double* g = g_nbdbg[e == 1 ? 0 : e == 37 ? 1 : 2];
+            g[0] = ua; g[1] = ub; g[2] = ai; g[3] = ak; g[4] = sh->pv.c0U[a]; g[5] = sh->pv.r0P[b];
+            g[6] = s00; g[7] = v; g[8] = a1; g[9] = a2; g[10] = first; g[11] = nu;
+          }
+#endif
+          v = v + ai * sh->pv.r0P[b];
+          v = v + (sh->pv.c0U[a] + ai * s00) * ak;
+          if (ua == ub && ua < 3) v += q;
+        }
+      }
+      sh->pv.R[a][b] = v;
+    }
+  }
+#ifdef EKF_DIAG_STAMPS
+  if (blockIdx.y == 0 && lane == 0) g_nbinfo[7] = 1;
+#endif
+}
+
+// Wave 1: K' = R̃·Z (the prologue's K' tiles) for the complete k-blocks [kb, upto): column tile
+// kb/4, 3 row tiles; a tile's columns of later k-blocks are recomputed once final (a column's bits
+// depend on it alone). Z columns ≥ 2m and its padding row read as the record's zeros. Returns upto.
+__device__ __noinline__ int nb_ktiles(LdsChain* sh, int kb, int upto, int m, int nu) {
+  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+  while (kb < upto) {
+    const int tj = kb >> 2, col = 16 * tj + i16;
+    for (int ti = 0; ti < 3; ++ti) {
+      double av[9], bv[9];
+      const int ar = min(16 * ti + i16, kMaxU - 1);
+#pragma unroll
+      for (int s0 = 0; s0 < 9; ++s0) {
+        const int k = 4 * s0 + k4;
+        av[s0] = sh->pv.R[ar][k];
+        bv[s0] = (k < kMaxU && col < 2 * m) ? sh->Z[min(k, kMaxU - 1)][col] : 0.0;
+      }
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s0 = 0; s0 < 9; ++s0)
+        if (4 * s0 < nu) acc = mfma_f64(av[s0], bv[s0], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * ti + k4 + 4 * r;
+        if (row < kMaxU) sh->pv.K[row][col] = acc[r];
+      }
+    }
+    kb = min(upto, 4 * tj + 4);
+  }
+  lds_publish3(&sh->kdone, kb);
+  return kb;
+}
+
+// Wave 2: C̃ = pred(Σ_in[U, U⁺]) into pv.C and D̃ = pred(Σ_in[U⁺, U⁺]) into P[pn] (the prologue's
+// C and P before K'·M').
+template <typename T>
+__device__ __noinline__ void nb_intake_cd(LdsChain* sh, LdsDesc* nd, const StageRec<T>* sgn, int pn,
+                                          int nu, int nun, int first, double q, int N) {
+  // lanes exchange values through LDS here: a convergent operation keeps the function convergent,
+  // so the compiler cannot split its call over divergent paths of the caller (it did, around a
+  // one-lane branch, and lane 0 ran the function alone)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int lane = threadIdx.x & 63;
+  const int t = min(lane, kMaxU - 1);
+  T vc[kStE], vd[kStE];  // every load in flight at once: one round trip
+#pragma unroll
+  for (int i = 0; i < kStE; ++i) {
+    vc[i] = sgn->v[2][min(lane + 64 * i, kStW * kStW - 1)];
+    vd[i] = sgn->v[0][min(lane + 64 * i, kStW * kStW - 1)];
+  }
+  const double s00 = sgn->r0u[0];
+  const double r0u = sgn->r0u[t], c0p = sgn->c0p[t], c0u = sgn->c0u[t];
+  if (lane < kMaxU) {
+    sh->pv.r0U[lane] = r0u;
+    sh->pv.c0P[lane] = c0p;
+    sh->c0U2[lane] = c0u;
+    sh->un[lane] = nb_ucol(nd, nun, lane, N);  // (wave 1 stores the same)
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  const double a1 = sh->a1, a2 = sh->a2;
+#pragma unroll
+  for (int i = 0; i < kStE; ++i) {
+    const int e = lane + 64 * i, a = e / kStW, b = e - a * kStW;
+    if (e < kStW * kStW && a < nun) {
+      double w = 0.0;
+      if (b < nu) {
+        w = static_cast<double>(vc[i]);
+        if (first) {
+          const int ua = sh->un[a], ub = sh->u[b];
+          const double ai = alpha_of(ua, a1, a2), ak = alpha_of(ub, a1, a2);
+          w = w + ak * sh->pv.r0U[a];
+          w = w + (sh->pv.c0P[b] + ak * s00) * ai;
+          if (ua == ub && ua < 3) w += q;
+        }
+      }
+      sh->pv.C[b][a] = w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kStE; ++i) {
+    const int e = lane + 64 * i, a = e / kStW, b = e - a * kStW;
+    if (e < kStW * kStW && a < nun && b < nun) {
+      double v = static_cast<double>(vd[i]);
+      if (first) {
+        const int ua = sh->un[a], ub = sh->un[b];
+        const double ai = alpha_of(ua, a1, a2), aj = alpha_of(ub, a1, a2);
+        v = v + ai * sh->pv.r0U[b];
+        v = v + (sh->c0U2[a] + ai * s00) * aj;
+        if (ua == ub && ua < 3) v += q;
+      }
+      sh->P[pn][a][b] = v;
+    }
+  }
+}
+
+// Wave 2: M' = Y·C̃ (the prologue's M' tiles) for k-blocks [mb, upto). Y rows ≥ 2m and its
+// padding column read as the record's zeros. Returns upto.
+__device__ __noinline__ int nb_mtiles(LdsChain* sh, int mb, int upto, int m, int nu) {
+  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+  while (mb < upto) {  // M' tiles of row tile ti (3 column tiles)
+    const int ti = mb >> 2, row = 16 * ti + i16;
+    for (int tj = 0; tj < 3; ++tj) {
+      double av[9], bv[9];
+      const int bc = min(16 * tj + i16, kMaxU - 1);
+#pragma unroll
+      for (int s0 = 0; s0 < 9; ++s0) {
+        const int k = 4 * s0 + k4;
+        av[s0] = (row < 2 * m && k < kMaxU) ? sh->Y[row][min(k, kMaxU - 1)] : 0.0;
+        bv[s0] = sh->pv.C[k][bc];
+      }
+      d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s0 = 0; s0 < 9; ++s0)
+        if (4 * s0 < nu) acc = mfma_f64(av[s0], bv[s0], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (16 * tj + i16 < kMaxU) sh->pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[r];
+    }
+    mb = min(upto, 4 * ti + 4);
+  }
+  return mb;
+}
+
+// Wave 2: P̃ −= K'·M' over k-block pb (the prologue's P-tile MFMA sequence): all 9 tiles'
+// operands and accumulators read first, then the MFMAs. K' columns of the block from wave 1.
+__device__ __noinline__ void nb_pblock(LdsChain* sh, int pn, int pb, int nun) {
+  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+  const int k = 4 * pb + k4;
+  double av[3], bv[3];
+  d4 acc[9];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    av[t] = -sh->pv.K[min(16 * t + i16, kMaxU - 1)][k];
+    bv[t] = sh->pv.M[k][min(16 * t + i16, kMaxU - 1)];
+  }
+#pragma unroll
+  for (int tt = 0; tt < 9; ++tt) {
+    const int ti = tt / 3, tj = tt - 3 * ti, cc = min(16 * tj + i16, kMaxU - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[tt][r] = sh->P[pn][min(16 * ti + k4 + 4 * r, kMaxU - 1)][cc];
+  }
+#pragma unroll
+  for (int tt = 0; tt < 9; ++tt) acc[tt] = mfma_f64(av[tt / 3], bv[tt % 3], acc[tt]);
+#pragma unroll
+  for (int tt = 0; tt < 9; ++tt) {
+    const int ti = tt / 3, tj = tt - 3 * ti, col = 16 * tj + i16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row2 = 16 * ti + k4 + 4 * r;
+      if (row2 < nun && col < nun) sh->P[pn][row2][col] = acc[tt][r];
+    }
   }
 }
 
@@ -515,6 +794,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
   pre = false;
   const MsgDesc& d = sdesc[ci & 1];
+  auto& P = sh.P[ci & 1];
   const bool active = (d.flags & kActive) != 0;
   const bool look = (d.flags & kLook) != 0;
   // Publish the previous chunk's record before this chunk waits on anything the bulk stream
@@ -531,12 +811,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // stream), and this record parity is free again once that pass is done (its factor kernel read
   // it); a chunk that gathers its own Σ_in needs the pass one back.
   const unsigned need = look ? (seq >= 2 ? seq - 1 : 0u) : seq;
-  if (A.polls && need && tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, need))
+  // the chunk before rebuilt this chunk's block (it saw the epoch `need` already)
+  bool built = look && ci > 0 && sh.built == seq;
+#ifdef EKF_DIAG_STAMPS
+  const bool nbchk = built && blockIdx.y == 0 && !g_nbinfo[3];
+  if (nbchk) nb_snapshot(sh, sh.P[ci & 1], 0);
+  built = false;
+#endif
+  if (A.polls && need && tid == 0 && !built && !epoch_wait_acquire(A.sync + kSyncSigma, need))
     atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
   if (tid == 0) sh.status = 0;
   __syncthreads();
   EKF_STAMP(0);
+  EKF_STAMPV(304, built ? 1ull : 0ull);
   const T* S = A.sig[d.parity] + f * A.sig_stride;
   const double* xin = A.x[d.parity] + f * A.x_stride;
   const int m = d.m;
@@ -566,6 +854,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     sh.u[tid] = u;
   }
   if (tid == 0) sh.nu_cnt = 3 + 2 * m;
+  if (ci + 1 < nchunks && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
+    reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
+        &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
   if (look && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0)
     const int pm = d.prev_m;
     int u = 0;
@@ -584,6 +875,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   __syncthreads();
   EKF_STAMP(1);
   const int nu = sh.nu_cnt;
+  // The next chunk's block is rebuilt by waves 1–2 during this chunk's corrections (device epochs,
+  // staged operands, not after a Joseph chunk: its rank-4 factor stays with the prologue).
+  const MsgDesc& nd = sdesc[(ci + 1) & 1];
+  constexpr int kNbFlags = kActive | kLook | kStageIn;
+  const bool nbw = A.nb && ci + 1 < nchunks && !joseph && (nd.flags & kNbFlags) == kNbFlags;
 
   // ---- A1: every global load of the prologue in one round ---------------------------------------
   // Each thread issues all of its loads before its first LDS store: indices are clamped rather
@@ -599,6 +895,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const T* Sp = A.sig[d.parity ^ 1] + f * A.sig_stride;
     const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
     const int np = sh.pv.nu;
+    if (!built) {  // (built: R̃, K', M', P̃ and the record's scalars are in LDS already)
     double vz[kPer], vy[kPer], vd[kPer], vr[kPer], vc[kPer];
     double r0u, c0u, r0p, c0p, x2;
     const int tc = tid < kMaxU ? tid : 0;
@@ -690,7 +987,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           v = v + (sh.pv.c0U[a] + ai * s00) * aj;
           if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
         }
-        sh.P[0][a][b] = v;
+        P[a][b] = v;
       }
       if (a < nu && b < kW) {  // b = k over U'
         double v = 0.0, w = 0.0;
@@ -754,6 +1051,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
     EKF_STAMP(7);
+    }  // !built
     if (tid < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
       const int u = sh.u[tid];
       int pos = -1;
@@ -781,6 +1079,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     EKF_STAMP(5);
     // a Joseph chunk before: its V'·K'ᵀ term as rank 2..3 (K' columns 2..3 are V' = R·Z'[:, 2..3];
     // M' rows 2..3 become K'ᵀ, the column factor)
+    if (!built) {
     const bool pj = sh.pv.joseph != 0;
     if (pj) {
       for (int e = tid; e < 2 * kW; e += blockDim.x) {
@@ -805,7 +1104,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = min(16 * ti + k4 + 4 * r, kMaxU - 1);
-        acc[r] = sh.P[0][row][cc];
+        acc[r] = P[row][cc];
       }
 #pragma unroll
       for (int s0 = 0; s0 < 8; ++s0)
@@ -813,9 +1112,34 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * ti + k4 + 4 * r;
-        if (row < nu && col < nu) sh.P[0][row][col] = acc[r];
+        if (row < nu && col < nu) P[row][col] = acc[r];
       }
     }
+    }  // !built
+#ifdef EKF_DIAG_STAMPS
+    if (nbchk) {
+      __syncthreads();
+      nb_snapshot(sh, P, 1);
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) {
+        bool bad = false;
+        for (int a = 0; a < nu && !bad; ++a)
+          for (int b = 0; b < nu; ++b)
+            if (__double_as_longlong(g_nb[0][4][a][b]) != __double_as_longlong(g_nb[1][4][a][b])) bad = true;
+        g_nbinfo[2] += 1;
+        if (bad) {
+          g_nbinfo[0] += 1;
+          g_nbinfo[1] = seq;
+          g_nbinfo[3] = 1;
+          g_nbinfo[4] = nu;
+          g_nbinfo[5] = np;
+          g_nbinfo[6] = sh.pv.m;
+        }
+      }
+      __syncthreads();
+    }
+#endif
   } else {
     double vd[kPer];
 #pragma unroll
@@ -831,7 +1155,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * kChainThreads;
       const int a = e / kW, b = e % kW;
-      if (a < nu && b < nu) sh.P[0][a][b] = vd[i];
+      if (a < nu && b < nu) P[a][b] = vd[i];
     }
     if (tid < nu) sh.xU[0][tid] = xv;
     if (tid < 3) {
@@ -852,20 +1176,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   if (tid < nu) {
     if (tid < 3) sh.xU[0][tid] = sh.pose[tid];
     sh.alphaU[tid] = first ? alpha_of(sh.u[tid], sh.a1, sh.a2) : 0.0;
-    sh.row0raw[tid] = sh.P[0][0][tid];
-    sh.col0raw[tid] = sh.P[0][tid][0];
+    sh.row0raw[tid] = P[0][tid];
+    sh.col0raw[tid] = P[tid][0];
   }
-  if (tid == 0) sh.s00 = sh.P[0][0][0];
+  if (tid == 0) sh.s00 = P[0][0];
   __syncthreads();
   // predict folded in: P ← A P Aᵀ + Q̄ on the block (slam.cpp:198)
   if (first) {
     for (int e = tid; e < kW * kW; e += blockDim.x) {
       const int a = e / kW, b = e % kW;
       if (a >= nu || b >= nu) continue;
-      double v = sh.P[0][a][b] + sh.alphaU[a] * sh.row0raw[b];
+      double v = P[a][b] + sh.alphaU[a] * sh.row0raw[b];
       v = v + (sh.col0raw[a] + sh.alphaU[a] * sh.s00) * sh.alphaU[b];
       if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
-      sh.P[0][a][b] = v;
+      P[a][b] = v;
     }
   }
   __syncthreads();
@@ -887,6 +1211,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     sh.pub = 0;
     sh.pdone = 0;
     sh.any_init = 0;
+    sh.kdone = 0;
+    sh.w1fin = 0;
+    sh.nb_ok1 = 0;
+    sh.nb_ok2 = 0;
   }
   if (pending) drain_stores();
   __syncthreads();
@@ -895,7 +1223,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     pending = 0;
   }
   if (wave == 0) {
-    chain_wave0((LdsChain*)(&sh), (LdsDesc*)(&d), m, nu, joseph, A.r, seq);
+    chain_wave0((LdsChain*)(&sh), (LdsDesc*)(&d), ci & 1, m, nu, joseph, A.r, seq);
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
     // lane → column 3+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
     const int hb = lane & 31, hr = lane >> 5;
@@ -910,7 +1238,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
 #pragma unroll
       for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
         const int a = min(3 + hr + 2 * i, kMaxU - 1);
-        pv[i] = sh.P[0][a][b];
+        pv[i] = P[a][b];
         k0[i] = sh.KU[c][a][0];
         k1[i] = sh.KU[c][a][1];
       }
@@ -920,7 +1248,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       for (int i = 0; i < 16; ++i) {
         const int a = 3 + hr + 2 * i;
         const bool ok = colok && a < nu && a != nx && a != nx + 1;
-        *(ok ? &sh.P[0][a][b] : &sh.junk[3][lane]) = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
+        *(ok ? &P[a][b] : &sh.junk[3][lane]) = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
       }
       lds_publish(&sh.pdone, c + 1);
       EKF_STAMPT(193 + 2 * c, 192);
@@ -946,6 +1274,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
     const int li = lane < kMaxU ? lane : kMaxU - 1;
+    const StageRec<T>* sgn = A.stage + static_cast<size_t>(nd.parity) * A.rec_stride + f;
+    const int nun = 3 + 2 * nd.m;
+    bool land = false;
+    int kb = 0;
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1017,6 +1349,28 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           }
         }
       }
+      if (nbw) {  // the next chunk's K' columns of the complete k-blocks
+        if (!land && nb_landed(A.sync, seq)) {
+          EKF_STAMPT(300, 64);
+          nb_intake_r<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, nu, nun, first, A.q, A.N);
+          EKF_STAMPT(306, 64);
+          land = true;
+        }
+        if (land) kb = nb_ktiles((LdsChain*)(&sh), kb, (c + 1) >> 1, m, nu);
+      }
+      EKF_STAMPT(320 + c, 64);
+    }
+    if (nbw) {  // (m odd: the last k-block's second pair of columns is zero)
+      if (!land && nb_landed(A.sync, seq)) {
+        EKF_STAMPT(300, 64);
+        nb_intake_r<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, nu, nun, first, A.q, A.N);
+        land = true;
+      }
+      EKF_STAMPT(305, 64);
+      if (land) kb = nb_ktiles((LdsChain*)(&sh), kb, (m + 1) >> 1, m, nu);
+      EKF_STAMPT(301, 64);
+      if (lane == 0) sh.nb_ok1 = land ? 1 : 0;
+      lds_publish(&sh.w1fin, 1);
     }
   } else {  // wave 2: Y_c: M_c[:, j] = Y_c·c_0(j) for every column j; Y_c to the record at once
     // Σ_c[pA_c, j] = (E_cᵀ − Σ_{k<c} K_k[pA_c]·Y_k)·c_0(j), so Y_c = H·E_cᵀ − Σ_{k<c} D_k·Y_k with
@@ -1025,6 +1379,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     for (int e = lane; e < (kZC - 2 * m) * kMaxU; e += 64)  // rows ≥ 2m of the record's Y are zero
       st_wt(&(&rec->Y[2 * m][0])[e], 0.0);
     const int lj = lane < kMaxU ? lane : kMaxU - 1;
+    const StageRec<T>* sgn = A.stage + static_cast<size_t>(nd.parity) * A.rec_stride + f;
+    const int nun = 3 + 2 * nd.m, pn = (ci + 1) & 1;
+    bool land = false;
+    int mb = 0, pb = 0;
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1080,6 +1438,48 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           st_wt(&rec->Y[2 * c + 1][lane], in ? y1 : 0.0);
         }
       }
+      if (nbw) {  // the next chunk's M' rows, then P̃ −= K'·M' over the k-blocks wave 1 has done
+        if (!land && nb_landed(A.sync, seq)) {
+          EKF_STAMPT(302, 128);
+          nb_intake_cd<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, pn, nu, nun, first, A.q, A.N);
+          EKF_STAMPT(307, 128);
+          land = true;
+        }
+        if (land) {
+          mb = nb_mtiles((LdsChain*)(&sh), mb, (c + 1) >> 1, m, nu);
+          EKF_STAMPT(340 + c, 128);
+          const int kd = min(mb, __builtin_amdgcn_readfirstlane(
+                                     __hip_atomic_load(&sh.kdone, __ATOMIC_ACQUIRE,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP)));
+          for (; pb < kd; ++pb) nb_pblock((LdsChain*)(&sh), pn, pb, nun);
+        }
+      }
+      EKF_STAMPT(360 + c, 128);
+    }
+    if (nbw) {
+      if (!land && nb_landed(A.sync, seq)) {
+        EKF_STAMPT(302, 128);
+        nb_intake_cd<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, pn, nu, nun, first, A.q, A.N);
+        land = true;
+      }
+      const int nk = (m + 1) >> 1;
+      if (land) {
+        mb = nb_mtiles((LdsChain*)(&sh), mb, nk, m, nu);
+        while (pb < nk) {  // wave 1 ends with kdone = nk, or without (no stage yet): w1fin either way
+          int kd;
+          for (;;) {
+            const int fin = __hip_atomic_load(&sh.w1fin, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            kd = __hip_atomic_load(&sh.kdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            kd = __builtin_amdgcn_readfirstlane(kd);
+            if (kd > pb || __builtin_amdgcn_readfirstlane(fin)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (kd <= pb) break;
+          for (; pb < kd; ++pb) nb_pblock((LdsChain*)(&sh), pn, pb, nun);
+        }
+      }
+      if (lane == 0) sh.nb_ok2 = land && pb == nk ? 1 : 0;
+      EKF_STAMPT(303, 128);
     }
   }
   __syncthreads();
@@ -1095,7 +1495,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     for (int e = tid; e < kMaxU * kMaxU; e += blockDim.x) {
       const int a = e / kMaxU, b = e - a * kMaxU;
-      double v = sh.P[0][a][b];
+      double v = P[a][b];
       if (m > 0)
         v = rank2_sub(v, sh.KU[c][a][0], sh.KU[c][a][1], sh.MU[c][b][0], sh.MU[c][b][1]);
       if (m > 0 && joseph) {  // − (G − K·S)[a]·K[b]ᵀ
@@ -1116,7 +1516,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // stalling this one. The record parity's release (the bulk stream done with it) was awaited by
   // the prologue's poll.
   const double* xfin = sh.xU[0];
-  const bool pre_next = ci + 1 < nchunks;
+  const bool pre_next = ci + 1 < nchunks;  // (its descriptor was loaded at A0)
+  const bool nb_ok = nbw && sh.nb_ok1 && sh.nb_ok2;  // waves 1–2 rebuilt the next chunk's block
+  if (nb_ok && tid == 0) sh.built = seq + 1u;
   if (wave == 3) {
     if (lane == 0) {
       if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
@@ -1125,12 +1527,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         ctl->tmo[0] = tmo.theta;
         ctl->tmo[1] = tmo.x;
         ctl->tmo[2] = tmo.y;
+        sh.tmo[0] = tmo.theta;  // (a built next chunk does not reload it)
+        sh.tmo[1] = tmo.x;
+        sh.tmo[2] = tmo.y;
       }
     }
   } else {
-    if (pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
-      reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
-          &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
     if (tid == 0 && sh.status) atomicOr(&ctl->status, sh.status);
     // hand the chunk to the factor kernel (and the next chain): write-through record
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
@@ -1142,6 +1544,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         zx += c < m ? t : 0.0;
       }
       const bool in = tid < nu;
+      if (nb_ok) {  // what the next chunk's prologue reads from the record
+        sh.pv.Zx[tid] = zx;
+        sh.pv.xU[tid] = in ? xfin[tid] : 0.0;
+      }
       st_wt(&rec->Zx[tid], zx);
       st_wt(&rec->u[tid], sh.u[tid]);
       st_wt(&rec->alphaU[tid], in ? sh.alphaU[tid] : 0.0);
@@ -2007,3 +2413,12 @@ EKF_INSTANTIATE(double)
 EKF_INSTANTIATE(float)
 
 }  // namespace ekfslam
+
+#ifdef EKF_DIAG_STAMPS
+extern "C" int ekfslam_diag_read_nb(double* out, unsigned* info) {
+  using namespace ekfslam;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nb), sizeof(g_nb)) != hipSuccess) return -5;
+  if (hipMemcpyFromSymbol(out + sizeof(g_nb) / 8, HIP_SYMBOL(g_nbdbg), sizeof(g_nbdbg)) != hipSuccess) return -5;
+  return hipMemcpyFromSymbol(info, HIP_SYMBOL(g_nbinfo), sizeof(g_nbinfo)) == hipSuccess ? 0 : -5;
+}
+#endif

@@ -33,6 +33,9 @@ struct PassArgs {
   unsigned pub_sigma;   // factors: publish this Σ-pass epoch first (the previous chunk's pass, 0 = none)
   int polls;            // 1: the streams hand off through device epochs (kernels poll them);
                         // 0: stream order / events order everything, no poll and no epoch kernel
+  int nb;               // chain (polls only): waves 1–2 rebuild the next chunk's block during the
+                        // corrections (EKF_NB=1; off by default: the staged operands land too late
+                        // in the chunk at N = 1024)
   const MsgDesc* desc;
   int desc_stride;      // descriptors between consecutive chunks of a chain launch
   int n, ld, N, f0;

@@ -41,7 +41,7 @@ else:
     e = e64
 replay(e, slice(w, w + T))
 e.sync()
-assert e.status() == 0
+print("status", e.status())
 L = pyekf.lib()
 st = (C.c_ulonglong * 2048)()
 L.ekf_diag_stamps.argtypes = [C.c_void_p, C.c_int]
@@ -60,6 +60,12 @@ print(f"N={N} {DT}, chunk {-1 - int(os.environ.get('WHICH', '1'))} of {T} messag
       f"the chunk's stamp 0); chunk starts of the ring, relative: {sorted(ring[:, 0] - ring[:, 0].min())}")
 for k in (1, 21, 3, 7, 5, 6, 2, 12, 16, 40):
     print(f"{names[k]:24s} {s[k] - t0:8d}")
+print(f"built by the chunk before: {s[304]}; next-chunk rebuild (waves 1-2): w1 landed {s[300] - t0}, "
+      f"w1 loop end {s[305] - t0}, w1 done {s[301] - t0}, w2 landed {s[302] - t0}, w2 done {s[303] - t0}")
+print(f"  w1 intake done {s[306] - t0}, w2 intake done {s[307] - t0}")
+print("  w1 step ends:", [int(s[320 + c] - t0) for c in range(16)])
+print("  w2 mtiles ends:", [int(s[340 + c] - t0) for c in range(16)])
+print("  w2 step ends:", [int(s[360 + c] - t0) for c in range(16)])
 m = int(sc.count[w + T - 1 - int(os.environ.get("WHICH", "1"))])
 steps = [int(s[64 + 8 * c] - t0) for c in range(m)]
 print("step starts:", steps)
@@ -71,4 +77,31 @@ for c in (0, 1, m // 2, m - 2):
           f"  geometry(c+1)+cross update {s[b + 6] - s[b + 4]}  -> next {s[b + 8] - s[b + 6]}")
     print(f"   wave3: pub seen at {s[192 + 2 * c] - s[b]}, pdone at {s[193 + 2 * c] - s[b]} "
           f"(wave0 publish at {s[b + 4] - s[b]}, next-step pdone wait at {s[b + 8 + 2] - s[b]})")
+if os.environ.get("NBCHK"):
+    import ctypes
+    # the diag build's g_nb / g_nbinfo (device symbols) through the lib's diag accessor
+    L.ekf_diag_nb.argtypes = [C.c_void_p, C.c_void_p]
+    buf = np.zeros(2 * 6 * 36 * 36 + 48)
+    info = np.zeros(8, dtype=np.uint32)
+    assert L.ekf_diag_nb(buf.ctypes.data, info.ctypes.data) == 0
+    dbg = buf[2 * 6 * 36 * 36:].reshape(4, 12)
+    buf = buf[:2 * 6 * 36 * 36].reshape(2, 6, 36, 36)
+    print("dbg regs lane0..2 (r0p c0u s00 lds c0U[0]):", dbg[3].tolist())
+    for r in range(3):
+        print("dbg e=", [1, 37, 36][r], "ua ub ai ak c0U[a] r0P[b] s00 v a1 a2 first nu:", dbg[r].tolist())
+    print("nb check: mismatching chunks", info[0], "first seq", info[1], "checked", info[2],
+          "nu", info[4], "np", info[5], "pm", info[6])
+    if info[0]:
+        nu, np_ = int(info[4]), int(info[5])
+        for k, nm in enumerate(["R", "C", "K", "M", "P", "vec"]):
+            d = buf[0][k] != buf[1][k]
+            if nm == "R": d = d[:nu, :36]
+            if nm == "P": d = d[:nu, :nu]
+            idx = np.argwhere(d)
+            print(nm, "mismatches", len(idx), idx[:8].tolist())
+            if nm == "vec":
+                for r in range(9):
+                    print("   vec row", r, buf[0][5][r, :6], buf[1][5][r, :6])
+            for a, b in idx[:4]:
+                print("   ", a, b, buf[0][k][a, b], buf[1][k][a, b])
 e.close()
