@@ -1804,44 +1804,85 @@ __device__ __forceinline__ double ld_f64(__amdgpu_buffer_rsrc_t r, unsigned vo, 
 template <typename T>
 struct SigmaTile;
 
+// The factor rank is at most 2 + 2·kMaxChunk = 34 (a Joseph chunk: 2 + 4): 17 k-steps of the
+// 32×32×2 MFMA. (kw, the rank rounded up to 4 for the fp64 tiles, would make it 18, the last one
+// on the two zero rows 34–35.)
+constexpr int kSteps = (2 + 2 * kMaxChunk + 1) / 2;
+static_assert(2 + 4 <= 2 * kSteps, "Joseph rank within the fp32 k-steps");
+struct F32TileRegs {  // one fp32 tile's loads
+  float a[kSteps], b[kSteps], sv[16];
+};
 template <>
 struct SigmaTile<float> {
   static constexpr int kRows = 32, kCols = 32;
-  static __device__ __forceinline__ void run(const float* Sin, float* Sout, const float* kc,
-                                             const float* mc, int n, int ld, int ldk, int kw,
-                                             bool first, double qd, int R0, int C0, int lane,
-                                             float*, const int*, int, int*) {
+  // descriptors based at the wave's row panel: offsets stay 32-bit for any n (a filter's Σ may
+  // exceed 4 GiB), and the records end at row n
+  static __device__ __forceinline__ __amdgpu_buffer_rsrc_t panel(const float* S, int n, int ld,
+                                                                 int R0) {
+    return buf_rsrc(S + static_cast<size_t>(R0) * ld,
+                    static_cast<unsigned>(min(n - R0, kRows)) * ld * 4u);
+  }
+  static __device__ __forceinline__ unsigned soff(int n, int ld, int C0, int lane) {
+    const int col = C0 + (lane & 31);
+    return col < n ? static_cast<unsigned>(4 * (lane >> 5) * ld + col) * 4u : kOOB;
+  }
+  // every load of the tile: the operands (L2-hot) first, then Σ_in
+  static __device__ __forceinline__ void load(F32TileRegs& g, const float* Sin, const float* kc,
+                                              const float* mc, int n, int ld, int ldk, int R0,
+                                              int C0, int lane) {
+    load_ops(g, kc, mc, n, ldk, R0, C0, lane);
+    // keep the operand loads ahead of Σ_in's: the MFMAs then wait for vmcnt(16), not vmcnt(0)
+    __builtin_amdgcn_sched_barrier(0);
+    load_sig(g, Sin, n, ld, R0, C0, lane);
+  }
+  static __device__ __forceinline__ void load_ops(F32TileRegs& g, const float* kc, const float* mc,
+                                                  int n, int ldk, int R0, int C0, int lane) {
     const int kr = lane >> 5, kcol = lane & 31;
-    // descriptors based at the wave's row panel: offsets stay 32-bit for any n (a filter's Σ
-    // may exceed 4 GiB), and the records end at row n
-    const size_t pbase = static_cast<size_t>(R0) * ld;
-    const unsigned sbytes = static_cast<unsigned>(min(n - R0, kRows)) * ld * 4u;
     const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 4u;
-    const auto rin = buf_rsrc(Sin + pbase, sbytes), rout = buf_rsrc(Sout + pbase, sbytes);
     const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
-    float a[18], b[18], sv[16];
     const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 4u;
     const unsigned mo = static_cast<unsigned>(kr * ldk + min(C0 + kcol, n - 1)) * 4u;
     const unsigned kstep = 2u * ldk * 4u;
 #pragma unroll
-    for (int s = 0; s < 18; ++s) {
-      a[s] = ld_f32(rk, ko, s * kstep);
-      b[s] = ld_f32(rm, mo, s * kstep);
+    for (int s = 0; s < kSteps; ++s) {
+      g.a[s] = ld_f32(rk, ko, s * kstep);
+      g.b[s] = ld_f32(rm, mo, s * kstep);
     }
-    const int col = C0 + kcol;
-    const unsigned so = col < n ? static_cast<unsigned>(4 * kr * ld + col) * 4u : kOOB;
+  }
+  static __device__ __forceinline__ void load_sig(F32TileRegs& g, const float* Sin, int n, int ld,
+                                                  int R0, int C0, int lane) {
+    const auto rin = panel(Sin, n, ld, R0);
+    const unsigned so = soff(n, ld, C0, lane);
     const unsigned rstride = static_cast<unsigned>(ld) * 4u;
-    // keep the operand loads ahead of Σ_in's: the MFMAs then wait for vmcnt(16), not vmcnt(0)
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sv[r] = ld_f32(rin, so + ((r & 3) + 8 * (r >> 2)) * rstride, 0);
+    for (int r = 0; r < 16; ++r) g.sv[r] = ld_f32(rin, so + ((r & 3) + 8 * (r >> 2)) * rstride, 0);
+  }
+  static __device__ __forceinline__ void run(const float* Sin, float* Sout, const float* kc,
+                                             const float* mc, int n, int ld, int ldk, int kw,
+                                             bool first, double qd, int R0, int C0, int lane,
+                                             float*, const int*, int, int*) {
+    F32TileRegs g;
+    load(g, Sin, kc, mc, n, ld, ldk, R0, C0, lane);
+    finish(g, Sout, n, ld, kw, first, qd, R0, C0, lane);
+  }
+  // the MFMAs on the tile's operands, Σ_in − K·M (+ Q̄), the stores
+  static __device__ __forceinline__ void finish(const F32TileRegs& g, float* Sout, int n, int ld,
+                                                int kw, bool first, double qd, int R0, int C0,
+                                                int lane) {
+    const int kr = lane >> 5, col = C0 + (lane & 31);
+    const auto rout = panel(Sout, n, ld, R0);
+    const unsigned so = soff(n, ld, C0, lane);
+    const unsigned rstride = static_cast<unsigned>(ld) * 4u;
+    const float* a = g.a;
+    const float* b = g.b;
+    const float* sv = g.sv;
     f16v acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
     // every MFMA issued, factor rows ≥ kw (stale) zeroed by a select: a branch per k-step let
     // the compiler sink each operand load into its branch behind a vmcnt(0)
 #pragma unroll
-    for (int s = 0; s < 18; ++s) {
+    for (int s = 0; s < kSteps; ++s) {
       const bool live = 2 * s < kw;
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(live ? a[s] : 0.0f, live ? b[s] : 0.0f, acc, 0,
                                                  0, 0);
@@ -1962,6 +2003,13 @@ using PassTile = typename std::conditional<sizeof(T) == 8 && WIDE, SigmaTile64<4
 // 8·⌊(L/8)/B⌋ + L % 8, tile block (L/8) % B, so all of a filter's blocks share one XCD and its
 // Kcat/Mcat are fetched into one L2 instead of eight. Placement only changes speed.
 // Waves take tiles row-major over a trows × tcols grid.
+// xcd_b = −1 (few filters, one per blockIdx.y): the tile grid is cut 2 × 4 into regions, block L
+// takes region L % 8 (so XCD L % 8 does): each XCD's L2 then fetches half of Kcat and a quarter
+// of Mcat instead of both whole (the fetch beyond Σ: 8 × (Kcat + Mcat) → 4 × Kcat + 2 × Mcat).
+constexpr int kRegRows = 2, kRegCols = 4;
+__host__ __device__ inline int region_tiles(int trows, int tcols) {  // the largest region's tiles
+  return ((trows + kRegRows - 1) / kRegRows) * ((tcols + kRegCols - 1) / kRegCols);
+}
 template <typename T, bool WIDE>
 __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, int xcd_b, int nf) {
   using Tile = PassTile<T, WIDE>;
@@ -1979,13 +2027,29 @@ __global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, in
   const int trows = (A.n + Tile::kRows - 1) / Tile::kRows;
   // the wave's tile index, provably wave-uniform (readfirstlane): the buffer descriptors built
   // from it stay in SGPRs instead of a waterfall loop around every buffer access
-  const int t = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  if ((d.flags & kActive) && t < trows * tcols) {
+  int t = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  int tr = 0, tc = 0;
+  bool ok;
+  if (xcd_b < 0) {
+    const int x = blockIdx.x & 7, w = (blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int hx = x / kRegCols, qx = x % kRegCols;
+    const int r0 = hx * trows / kRegRows, r1 = (hx + 1) * trows / kRegRows;
+    const int c0 = qx * tcols / kRegCols, c1 = (qx + 1) * tcols / kRegCols;
+    const int cw = c1 - c0;
+    const int tt = __builtin_amdgcn_readfirstlane(w);
+    ok = tt < (r1 - r0) * cw;
+    tr = r0 + tt / cw;
+    tc = c0 + tt % cw;
+  } else {
+    ok = t < trows * tcols;
+    tr = t / tcols;
+    tc = t - tr * tcols;
+  }
+  if ((d.flags & kActive) && ok) {
     SIG_STAMP(1);
     const int f = A.f0 + fb;
     // this filter's rank (Joseph: K·M and V·Kᵀ per marker); rows beyond are stale
     const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
-    const int tr = t / tcols, tc = t - tr * tcols;
     T* rows = (d.flags & kRowsOut) ? A.rows + f * A.rows_stride : nullptr;
     Tile::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
                       A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
@@ -2353,9 +2417,14 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool st
     using Tile = PassTile<T, false>;
     const int trows = (a.n + Tile::kRows - 1) / Tile::kRows;
     const int tcols = (a.n + Tile::kCols - 1) / Tile::kCols;
-    const int per_filter = (trows * tcols + wpb - 1) / wpb;
-    const dim3 grid(per_filter, nf);
-    launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
+    if (trows >= 2 * kRegRows && tcols >= 2 * kRegCols) {  // XCD regions (k_sigma_pass)
+      const dim3 grid(8 * ((region_tiles(trows, tcols) + wpb - 1) / wpb), nf);
+      launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, -1, nf);
+    } else {
+      const int per_filter = (trows * tcols + wpb - 1) / wpb;
+      const dim3 grid(per_filter, nf);
+      launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
+    }
   }
   if (sizeof(T) == 4 || stage) hipLaunchKernelGGL(k_patch_stage<T>, dim3(nf), dim3(256), 0, s, a);
   // the pass's epoch (otherwise published by the next chunk's factor kernel, PassArgs::pub_sigma)

@@ -75,11 +75,11 @@ void run(int N, int F, int reps) {
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double cbytes = 2.0 * stride * F * sizeof(T);
   printf("N=%d F=%d %s: copy %.2f us (%.0f GB/s)", N, F, sizeof(T) == 4 ? "f32" : "f64", ms * 1e3 / reps, cbytes / (ms / reps * 1e-3) / 1e9);
-  for (int i = 0; i < 3; ++i) CK(launch_sigma_pass<T>(a, F, 36, s));
+  for (int i = 0; i < 3; ++i) CK(launch_sigma_pass<T>(a, F, false, false, s));
   CK(hipEventRecord(e0, s));
   for (int i = 0; i < reps; ++i) {
     if (g_pingpong) a.desc = dd + (i & 1) * F;
-    CK(launch_sigma_pass<T>(a, F, 36, s));
+    CK(launch_sigma_pass<T>(a, F, false, false, s));
   }
   a.desc = dd;
   CK(hipEventRecord(e1, s));
@@ -89,8 +89,8 @@ void run(int N, int F, int reps) {
 #ifdef EKF_DIAG_STAMPS
   {
     const int tiles = ((n + SigmaTile<T>::kRows - 1) / SigmaTile<T>::kRows * ((n + SigmaTile<T>::kCols - 1) / SigmaTile<T>::kCols) + 3) / 4, nb = std::min(tiles, 4096);
-    CK(launch_sigma_pass<T>(a, F, 36, s));
-    CK(launch_sigma_pass<T>(a, F, 36, s));
+    CK(launch_sigma_pass<T>(a, F, false, false, s));
+    CK(launch_sigma_pass<T>(a, F, false, false, s));
     CK(hipStreamSynchronize(s));
     std::vector<unsigned long long> st(4096 * 5);
     CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_sig_stamps), st.size() * sizeof(unsigned long long)));

@@ -20,8 +20,9 @@ int check(int N, int m = 16) {
   srand(7);
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) S[static_cast<size_t>(i) * ld + j] = static_cast<T>((rand() % 2001 - 1000) * 1e-3);
-  const int kw = ((2 + 2 * m + 3) / 4) * 4;
-  for (int k = 0; k < kw; ++k)
+  // the factor kernel writes the rank's 2 + 2m rows; the padding rows up to kw stay zero
+  const int kw = ((2 + 2 * m + 3) / 4) * 4, rank = m >= 0 ? 2 + 2 * m : 0;
+  for (int k = 0; k < rank && k < kw; ++k)
     for (int i = 0; i < n; ++i) {
       K[static_cast<size_t>(k) * ldk + i] = static_cast<T>((rand() % 2001 - 1000) * 1e-3);
       M[static_cast<size_t>(k) * ldk + i] = static_cast<T>((rand() % 2001 - 1000) * 1e-3);
@@ -47,7 +48,7 @@ int check(int N, int m = 16) {
   a.kcat = dK; a.mcat = dM; a.km_stride = ks; a.ldk = ldk;
   a.rec = rec; a.rec_stride = 1; a.desc = dd;
   a.n = n; a.ld = ld; a.N = N; a.q = 0.01;
-  CK(launch_sigma_pass<T>(a, 1, false, nullptr));
+  CK(launch_sigma_pass<T>(a, 1, false, false, nullptr));
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(out.data(), dS1, ss * sizeof(T), hipMemcpyDeviceToHost));
   double worst = 0;
