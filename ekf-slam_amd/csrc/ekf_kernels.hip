@@ -975,39 +975,50 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // R / C columns k ≥ |U'| up to 36 are zeroed (MFMA k padding)
     const bool pf = sh.pv.first != 0;
     const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
+    // every LDS read of the six entries first (clamped indices, no branch around a read): one
+    // LDS round instead of a wait per predicated read
+    double r0Ub[kPer], r0Ua[kPer], c0Ua[kPer], r0Pb[kPer], c0Pb[kPer];
+    int ua[kPer], ub[kPer], pu[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads;
+      const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
+      ua[i] = sh.u[a];
+      ub[i] = sh.u[b];
+      pu[i] = sh.pv.u[b];
+      r0Ub[i] = sh.pv.r0U[b];
+      r0Ua[i] = sh.pv.r0U[a];
+      c0Ua[i] = sh.pv.c0U[a];
+      r0Pb[i] = sh.pv.r0P[b];
+      c0Pb[i] = sh.pv.c0P[b];
+    }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * kChainThreads;
       const int a = e / kW, b = e % kW;
-      if (a < nu && b < nu) {
-        double v = vd[i];
-        if (pf) {
-          const double ai = alpha_of(sh.u[a], qa1, qa2), aj = alpha_of(sh.u[b], qa1, qa2);
-          v = v + ai * sh.pv.r0U[b];
-          v = v + (sh.pv.c0U[a] + ai * s00) * aj;
-          if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
-        }
-        P[a][b] = v;
+      double v = vd[i], vR = 0.0, wC = 0.0;
+      if (b < np) {
+        vR = vr[i];
+        wC = vc[i];
       }
-      if (a < nu && b < kW) {  // b = k over U'
-        double v = 0.0, w = 0.0;
-        if (b < np) {
-          v = vr[i];
-          w = vc[i];
-          if (pf) {
-            const double ai = alpha_of(sh.u[a], qa1, qa2), ak = alpha_of(sh.pv.u[b], qa1, qa2);
-            v = v + ai * sh.pv.r0P[b];
-            v = v + (sh.pv.c0U[a] + ai * s00) * ak;
-            w = w + ak * sh.pv.r0U[a];
-            w = w + (sh.pv.c0P[b] + ak * s00) * ai;
-            if (sh.u[a] == sh.pv.u[b] && sh.u[a] < 3) {
-              v += A.q;
-              w += A.q;
-            }
-          }
-        }
-        sh.pv.R[a][b] = v;
-        sh.pv.C[b][a] = w;
+      if (pf) {
+        const double ai = alpha_of(ua[i], qa1, qa2), aj = alpha_of(ub[i], qa1, qa2);
+        const double ak = alpha_of(pu[i], qa1, qa2);
+        v = v + ai * r0Ub[i];
+        v = v + (c0Ua[i] + ai * s00) * aj;
+        v = (ua[i] == ub[i] && ua[i] < 3) ? v + A.q : v;
+        double v2 = vR + ai * r0Pb[i];
+        v2 = v2 + (c0Ua[i] + ai * s00) * ak;
+        double w2 = wC + ak * r0Ua[i];
+        w2 = w2 + (c0Pb[i] + ak * s00) * ai;
+        const bool qd = ua[i] == pu[i] && ua[i] < 3;
+        vR = b < np ? (qd ? v2 + A.q : v2) : 0.0;
+        wC = b < np ? (qd ? w2 + A.q : w2) : 0.0;
+      }
+      if (a < nu && b < nu) P[a][b] = v;
+      if (a < nu) {  // b = k over U' (36: the MFMA k padding, zero)
+        sh.pv.R[a][b] = vR;
+        sh.pv.C[b][a] = wC;
       }
     }
     __syncthreads();
