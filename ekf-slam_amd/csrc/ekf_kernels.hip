@@ -1063,29 +1063,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
     EKF_STAMP(7);
     }  // !built
-    if (tid < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
-      const int u = sh.u[tid];
-      int pos = -1;
-#pragma unroll
-      for (int k = kMaxU - 1; k >= 0; --k) {
-        const bool hit = k < np && sh.pv.u[k] == u;
-        pos = hit ? k : pos;
-      }
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};  // four partial sums (k mod 4): a 9-deep chain
-#pragma unroll
-      for (int k = 0; k < kMaxU; ++k) acc[k & 3] = fma(sh.pv.R[tid][k], sh.pv.Zx[k], acc[k & 3]);
-      const double r = (acc[0] + acc[1]) + (acc[2] + acc[3]);  // R[·][k ≥ |U'|] = 0
-      sh.xU[0][tid] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[tid] + r;
-    }
-    if (tid < 3) sh.xpose[tid] = sh.pv.xU[tid];  // pose ∈ U' always
-    if (tid == 192) {  // waves 1–3 have no x[U] rows: the predicted pose (slam.cpp:184-196) here,
-                       // from x' of the pose (= xpose, stored above by wave 0)
-      double a1, a2;
-      const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
-      predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
-      sh.a1 = a1;
-      sh.a2 = a2;
-    }
     __syncthreads();
     EKF_STAMP(5);
     // a Joseph chunk before: its V'·K'ᵀ term as rank 2..3 (K' columns 2..3 are V' = R·Z'[:, 2..3];
@@ -1127,6 +1104,31 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
     }  // !built
+    // wave 3 (two P tiles against wave 0's three): x_in[U] and the predicted pose
+    if (wv == 3) {
+      if (ln < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
+        const int u = sh.u[ln];
+        int pos = -1;
+#pragma unroll
+        for (int k = kMaxU - 1; k >= 0; --k) {
+          const bool hit = k < np && sh.pv.u[k] == u;
+          pos = hit ? k : pos;
+        }
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};  // four partial sums (k mod 4): a 9-deep chain
+#pragma unroll
+        for (int k = 0; k < kMaxU; ++k) acc[k & 3] = fma(sh.pv.R[ln][k], sh.pv.Zx[k], acc[k & 3]);
+        const double r = (acc[0] + acc[1]) + (acc[2] + acc[3]);  // R[·][k ≥ |U'|] = 0
+        sh.xU[0][ln] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[ln] + r;
+      }
+      if (ln < 3) sh.xpose[ln] = sh.pv.xU[ln];  // pose ∈ U' always
+      if (ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
+        double a1, a2;
+        const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
+        predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
+        sh.a1 = a1;
+        sh.a2 = a2;
+      }
+    }
 #ifdef EKF_DIAG_STAMPS
     if (nbchk) {
       __syncthreads();
@@ -1184,23 +1186,42 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   EKF_STAMP(6);
   // ---- A3: x[U] pose, α, this chunk's predict folded in: P ← A P Aᵀ + Q̄ (slam.cpp:198) --------
   __syncthreads();
-  if (tid < nu) {
-    if (tid < 3) sh.xU[0][tid] = sh.pose[tid];
-    sh.alphaU[tid] = first ? alpha_of(sh.u[tid], sh.a1, sh.a2) : 0.0;
-    sh.row0raw[tid] = P[0][tid];
-    sh.col0raw[tid] = P[tid][0];
-  }
-  if (tid == 0) sh.s00 = P[0][0];
-  __syncthreads();
-  // predict folded in: P ← A P Aᵀ + Q̄ on the block (slam.cpp:198)
-  if (first) {
-    for (int e = tid; e < kW * kW; e += blockDim.x) {
-      const int a = e / kW, b = e % kW;
-      if (a >= nu || b >= nu) continue;
-      double v = P[a][b] + sh.alphaU[a] * sh.row0raw[b];
-      v = v + (sh.col0raw[a] + sh.alphaU[a] * sh.s00) * sh.alphaU[b];
-      if (sh.u[a] == sh.u[b] && sh.u[a] < 3) v += A.q;
-      P[a][b] = v;
+  {
+    // every thread reads its raw entries, row 0 and column 0 straight from the block (one LDS
+    // round, no α / row / column exchange); α, row 0, column 0 also go to LDS for the record
+    const double a1 = sh.a1, a2 = sh.a2, s00 = P[0][0];
+    double pr[kPer], r0[kPer], c0[kPer];
+    int ua[kPer], ub[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads;
+      const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
+      pr[i] = P[a][b];
+      r0[i] = P[0][b];
+      c0[i] = P[a][0];
+      ua[i] = sh.u[a];
+      ub[i] = sh.u[b];
+    }
+    if (tid < nu) {
+      if (tid < 3) sh.xU[0][tid] = sh.pose[tid];
+      sh.alphaU[tid] = first ? alpha_of(sh.u[tid], a1, a2) : 0.0;
+      sh.row0raw[tid] = P[0][tid];
+      sh.col0raw[tid] = P[tid][0];
+    }
+    if (tid == 0) sh.s00 = s00;
+    // predict folded in: P ← A P Aᵀ + Q̄ on the block (slam.cpp:198)
+    if (first) {
+      __syncthreads();  // every raw read done before the first write
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        const int e = tid + i * kChainThreads;
+        const int a = e / kW, b = e % kW;
+        const double ai = alpha_of(ua[i], a1, a2), aj = alpha_of(ub[i], a1, a2);
+        double v = pr[i] + ai * r0[i];
+        v = v + (c0[i] + ai * s00) * aj;
+        v = (ua[i] == ub[i] && ua[i] < 3) ? v + A.q : v;
+        if (a < nu && b < nu) P[a][b] = v;
+      }
     }
   }
   __syncthreads();
