@@ -854,7 +854,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     sh.u[tid] = u;
   }
   if (tid == 0) sh.nu_cnt = 3 + 2 * m;
-  if (ci + 1 < nchunks && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
+  // the next descriptor: here when waves 1–2 rebuild the next block (they need it during the
+  // corrections), else in the epilogue (off this barrier's path)
+  if (A.nb && ci + 1 < nchunks && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
     reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
         &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
   if (look && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0)
@@ -1548,7 +1550,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // stalling this one. The record parity's release (the bulk stream done with it) was awaited by
   // the prologue's poll.
   const double* xfin = sh.xU[0];
-  const bool pre_next = ci + 1 < nchunks;  // (its descriptor was loaded at A0)
+  const bool pre_next = ci + 1 < nchunks;
   const bool nb_ok = nbw && sh.nb_ok1 && sh.nb_ok2;  // waves 1–2 rebuilt the next chunk's block
   if (nb_ok && tid == 0) sh.built = seq + 1u;
   if (wave == 3) {
@@ -1565,6 +1567,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
   } else {
+    if (!A.nb && pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
+      reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
+          &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
     if (tid == 0 && sh.status) atomicOr(&ctl->status, sh.status);
     // hand the chunk to the factor kernel (and the next chain): write-through record
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
