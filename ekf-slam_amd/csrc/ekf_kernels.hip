@@ -2240,11 +2240,13 @@ __global__ void k_sigma_epoch(unsigned* sync, unsigned epoch) {
 // slam.cpp:344-440 for the marker in desc.z[0]: d_k = νᵀψ_k⁻¹ν over the known landmarks k < counter
 // (predict folded in when pending), the new slot's d forced to the gate (:406-408), first-index
 // argmin (arma::index_min), then commit (new landmark written into x_in, counter++) or roll back.
+constexpr int kAssocThreads = 1024;  // one known landmark per lane up to counter 1024: the gathers
+                                     // of every landmark in flight in one round
 template <typename T>
-__global__ __launch_bounds__(256) void k_assoc(PassArgs<T> A) {
+__global__ __launch_bounds__(kAssocThreads) void k_assoc(PassArgs<T> A) {
   __shared__ double s_pose[3], s_a[2], s_P33[3][3];
-  __shared__ double s_bd[4];
-  __shared__ int s_bk[4];
+  __shared__ double s_bd[kAssocThreads / 64];
+  __shared__ int s_bk[kAssocThreads / 64];
   __shared__ int s_abort;
   const MsgDesc& d = A.desc[blockIdx.y];
   if (!(d.flags & kActive) || d.m == 0) return;
@@ -2471,7 +2473,7 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool st
 
 template <typename T>
 hipError_t launch_assoc(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  launch(k_assoc<T>, dim3(1, nf), dim3(256), s, e0, e1, a);
+  launch(k_assoc<T>, dim3(1, nf), dim3(kAssocThreads), s, e0, e1, a);
   return hipGetLastError();
 }
 
