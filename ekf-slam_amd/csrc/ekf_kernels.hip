@@ -255,8 +255,7 @@ __device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
 // Diagnostic build only: a chunk whose block waves 1–2 rebuilt runs the prologue's rebuild as well;
 // both versions of R̃, C̃, K', M', P̃ and the vectors (filter 0), kept from the first mismatch on.
 __device__ double g_nb[2][6][kMaxU + 1][kMaxU + 1];
-__device__ unsigned g_nbinfo[8];
-__device__ double g_nbdbg[4][12];  // mismatching chunks, seq of the first, checked chunks, frozen
+__device__ unsigned g_nbinfo[8];  // mismatching chunks, seq of the first, checked chunks, frozen
 __device__ void nb_snapshot(ChainShared& sh, const double (&P)[kMaxU][kMaxU + 1], int w) {
   for (int e = threadIdx.x; e < (kMaxU + 1) * (kMaxU + 1); e += blockDim.x) {
     const int a = e / (kMaxU + 1), b = e % (kMaxU + 1);
@@ -562,14 +561,6 @@ __device__ __noinline__ void nb_intake_r(LdsChain* sh, LdsDesc* nd, const StageR
     sh->pv.xg[lane] = xg;
     sh->un[lane] = nb_ucol(nd, nun, lane, N);
   }
-#ifdef EKF_DIAG_STAMPS
-  if (blockIdx.y == 0 && lane < 3 && g_nbinfo[7] == 0) {
-    g_nbdbg[3][4 * lane] = r0p;
-    g_nbdbg[3][4 * lane + 1] = c0u;
-    g_nbdbg[3][4 * lane + 2] = s00;
-    g_nbdbg[3][4 * lane + 3] = sh->pv.c0U[0];
-  }
-#endif
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   const double a1 = sh->a1, a2 = sh->a2;
 #pragma unroll
@@ -582,13 +573,6 @@ __device__ __noinline__ void nb_intake_r(LdsChain* sh, LdsDesc* nd, const StageR
         if (first) {
           const int ua = sh->un[a], ub = sh->u[b];
           const double ai = alpha_of(ua, a1, a2), ak = alpha_of(ub, a1, a2);
-#ifdef EKF_DIAG_STAMPS
-          if (blockIdx.y == 0 && (e == 1 || e == 37 || e == 36) && g_nbinfo[7] == 0) {
-            double* g = g_nbdbg[e == 1 ? 0 : e == 37 ? 1 : 2];
-            g[0] = ua; g[1] = ub; g[2] = ai; g[3] = ak; g[4] = sh->pv.c0U[a]; g[5] = sh->pv.r0P[b];
-            g[6] = s00; g[7] = v; g[8] = a1; g[9] = a2; g[10] = first; g[11] = nu;
-          }
-#endif
           v = v + ai * sh->pv.r0P[b];
           v = v + (sh->pv.c0U[a] + ai * s00) * ak;
           if (ua == ub && ua < 3) v += q;
@@ -597,9 +581,7 @@ __device__ __noinline__ void nb_intake_r(LdsChain* sh, LdsDesc* nd, const StageR
       sh->pv.R[a][b] = v;
     }
   }
-#ifdef EKF_DIAG_STAMPS
-  if (blockIdx.y == 0 && lane == 0) g_nbinfo[7] = 1;
-#endif
+
 }
 
 // Wave 1: K' = R̃·Z (the prologue's K' tiles) for the complete k-blocks [kb, upto): column tile
@@ -2526,7 +2508,6 @@ EKF_INSTANTIATE(float)
 extern "C" int ekfslam_diag_read_nb(double* out, unsigned* info) {
   using namespace ekfslam;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nb), sizeof(g_nb)) != hipSuccess) return -5;
-  if (hipMemcpyFromSymbol(out + sizeof(g_nb) / 8, HIP_SYMBOL(g_nbdbg), sizeof(g_nbdbg)) != hipSuccess) return -5;
   return hipMemcpyFromSymbol(info, HIP_SYMBOL(g_nbinfo), sizeof(g_nbinfo)) == hipSuccess ? 0 : -5;
 }
 #endif

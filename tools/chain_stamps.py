@@ -78,17 +78,11 @@ for c in (0, 1, m // 2, m - 2):
     print(f"   wave3: pub seen at {s[192 + 2 * c] - s[b]}, pdone at {s[193 + 2 * c] - s[b]} "
           f"(wave0 publish at {s[b + 4] - s[b]}, next-step pdone wait at {s[b + 8 + 2] - s[b]})")
 if os.environ.get("NBCHK"):
-    import ctypes
     # the diag build's g_nb / g_nbinfo (device symbols) through the lib's diag accessor
     L.ekf_diag_nb.argtypes = [C.c_void_p, C.c_void_p]
-    buf = np.zeros(2 * 6 * 36 * 36 + 48)
+    buf = np.zeros((2, 6, 36, 36))
     info = np.zeros(8, dtype=np.uint32)
     assert L.ekf_diag_nb(buf.ctypes.data, info.ctypes.data) == 0
-    dbg = buf[2 * 6 * 36 * 36:].reshape(4, 12)
-    buf = buf[:2 * 6 * 36 * 36].reshape(2, 6, 36, 36)
-    print("dbg regs lane0..2 (r0p c0u s00 lds c0U[0]):", dbg[3].tolist())
-    for r in range(3):
-        print("dbg e=", [1, 37, 36][r], "ua ub ai ak c0U[a] r0P[b] s00 v a1 a2 first nu:", dbg[r].tolist())
     print("nb check: mismatching chunks", info[0], "first seq", info[1], "checked", info[2],
           "nu", info[4], "np", info[5], "pm", info[6])
     if info[0]:
