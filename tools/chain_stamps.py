@@ -2,7 +2,9 @@
 pipelined replay (libekfslam_diag.so; build: make -C ekf-slam_amd diag).
 
   python tools/chain_stamps.py [N] [f32|f64]   (default 1024 f32: configs[2]'s headline shape —
-  the fp64 survey lap, then fp32 circle messages from its state, as bench.py runs it)"""
+  the fp64 survey lap, then fp32 circle messages from its state, as bench.py runs it)
+  EKF_NB=1 NBCHK=1: with the helper-wave rebuild on, every chunk it built also runs the
+  prologue's rebuild; prints how many of the two blocks differ (and where, for the first one)"""
 import ctypes as C
 import os
 import sys
