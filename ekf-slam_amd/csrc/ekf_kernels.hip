@@ -1294,6 +1294,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const int nun = 3 + 2 * nd.m;
     bool land = false;
     int kb = 0;
+    double zxa = 0.0;  // Σ_c Z_c ν_c of row `lane`, accumulated as the Z_c come (the record's Zx)
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1352,6 +1353,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
         const bool in = lane < nu;
         const double Z0 = in ? z0 : 0.0, Z1 = in ? z1 : 0.0;
+        const double t = Z0 * sh.nu[c][0] + Z1 * sh.nu[c][1];
+        zxa += t;
         if (lane < kMaxU) {
           sh.Z[lane][2 * c] = Z0;
           sh.Z[lane][2 * c + 1] = Z1;
@@ -1376,6 +1379,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
       EKF_STAMPT(320 + c, 64);
     }
+    if (lane < kMaxU) sh.Zx[lane] = zxa;
     if (nbw) {  // (m odd: the last k-block's second pair of columns is zero)
       if (!land && nb_landed(A.sync, seq)) {
         EKF_STAMPT(300, 64);
@@ -1556,12 +1560,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // hand the chunk to the factor kernel (and the next chain): write-through record
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
-      double zx = 0.0;  // (reads unconditional, terms past m selected away: one LDS round trip)
-#pragma unroll
-      for (int c = 0; c < kMaxChunk; ++c) {
-        const double t = sh.Z[tid][2 * c] * sh.nu[c][0] + sh.Z[tid][2 * c + 1] * sh.nu[c][1];
-        zx += c < m ? t : 0.0;
-      }
+      const double zx = sh.Zx[tid];  // (wave 1's sum over the corrections)
       const bool in = tid < nu;
       if (nb_ok) {  // what the next chunk's prologue reads from the record
         sh.pv.Zx[tid] = zx;
