@@ -325,14 +325,20 @@ int drain(ekf_ctx* h) {
   return EKF_OK;
 }
 
-int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
+// devsync: k_assoc waits on the device for the last Σ pass (its epoch is h->seq) instead of the
+// main stream joining the bulk stream first
+int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, bool poll) {
   if (h->cfg.dtype == EKF_F32) {
-    const PassArgs<float> a = args<float>(h, dptr, f0);
+    PassArgs<float> a = args<float>(h, dptr, f0);
+    a.polls = poll ? 1 : 0;
+    a.need_sigma = poll ? static_cast<unsigned>(h->seq) : 0u;
     return timed(h, 2, h->stream, [&](hipEvent_t e0, hipEvent_t e1) {
       return launch_assoc<float>(a, nf, h->stream, e0, e1);
     });
   }
-  const PassArgs<double> a = args<double>(h, dptr, f0);
+  PassArgs<double> a = args<double>(h, dptr, f0);
+  a.polls = poll ? 1 : 0;
+  a.need_sigma = poll ? static_cast<unsigned>(h->seq) : 0u;
   return timed(h, 2, h->stream, [&](hipEvent_t e0, hipEvent_t e1) {
     return launch_assoc<double>(a, nf, h->stream, e0, e1);
   });
@@ -580,8 +586,9 @@ int flush(ekf_ctx* h) {
       continue;
     }
     if (L.kind == 1) {
-      if (join_bulk(h)) return EKF_E_HIP;
-      rc = assoc(h, dp, L.f0, L.nf);
+      const bool poll = h->devsync && !h->serial;
+      if (!poll && join_bulk(h)) return EKF_E_HIP;
+      rc = assoc(h, dp, L.f0, L.nf, poll);
       // the chunk's factors and Σ pass on the bulk stream (with split CU masks the main stream
       // has 4 CUs per XCD: a pass there took 33 µs against 9 at N = 1024 fp32); the next
       // association joins the bulk stream first

@@ -2237,6 +2237,12 @@ __global__ __launch_bounds__(kAssocThreads) void k_assoc(PassArgs<T> A) {
   const T* S = A.sig[d.parity] + f * A.sig_stride;
   double* x = A.x[d.parity] + f * A.x_stride;
   FilterCtl* ctl = A.ctl + f;
+  // device epochs: Σ_in and x are the last Σ pass's (bulk stream), its epoch A.need_sigma
+  if (A.polls && A.need_sigma) {
+    if (tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, A.need_sigma))
+      atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+    __syncthreads();
+  }
   const unsigned s = ctl->counter;
   const int slot = d.assoc_slot;
   if (tid == 0) {
