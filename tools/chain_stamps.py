@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-os.environ["EKF_LIB"] = "libekfslam_diag.so"
+os.environ.setdefault("EKF_LIB", "libekfslam_diag.so")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ekf-slam_amd"))
 import pyekf  # noqa: E402
