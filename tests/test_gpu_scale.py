@@ -337,6 +337,31 @@ def test_association_at_scale_decisions(known_map):
     assert np.abs(Sg - Sr).max() < SIGMA_TOL
 
 
+def test_association_at_scale_schedules_bit_identical(known_map, monkeypatch):
+    """Unknown association on the pipeline under the three schedules — device epochs (k_assoc
+    polls the last Σ pass's epoch), HIP events (the main stream joins the bulk stream before each
+    k_assoc) and one stream: the same decisions and bit-identical state."""
+    sc, odom, ws = known_map
+    w = sc.n_warm
+    out = []
+    for env in ({"EKF_DEVSYNC": "1"}, {"EKF_DEVSYNC": "0"}, {"EKF_SERIAL": "1"}):
+        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        e = pyekf.EKF(n_landmarks=512)
+        x, S, tmo, cnt = ws
+        e.set_state(x, S, tmo=tmo, counter=cnt)
+        _replay(e, slice(w, w + 4), sc, odom, assoc=True)
+        out.append(e.state())
+        assert e.status() == 0
+        e.close()
+    for o in out[1:]:
+        assert o[2] == out[0][2]
+        np.testing.assert_array_equal(o[0], out[0][0])
+        np.testing.assert_array_equal(o[1], out[0][1])
+
+
 def test_association_at_scale_batched_replay(known_map):
     """The same messages through ekf_replay(assoc=1) (decisions on the device, no host round
     trip), from the same state: the final state equals the oracle's."""
