@@ -1088,7 +1088,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
     }  // !built
-    // wave 3 (two P tiles against wave 0's three): x_in[U] and the predicted pose
+    // waves 2 and 3 (two P tiles against wave 0's three): the predicted pose and x_in[U]
+    if (wv == 2 && ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
+      double a1, a2;
+      const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
+      predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
+      sh.a1 = a1;
+      sh.a2 = a2;
+    }
     if (wv == 3) {
       if (ln < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
         const int u = sh.u[ln];
@@ -1105,13 +1112,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         sh.xU[0][ln] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[ln] + r;
       }
       if (ln < 3) sh.xpose[ln] = sh.pv.xU[ln];  // pose ∈ U' always
-      if (ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
-        double a1, a2;
-        const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
-        predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
-        sh.a1 = a1;
-        sh.a2 = a2;
-      }
     }
 #ifdef EKF_DIAG_STAMPS
     if (nbchk) {
