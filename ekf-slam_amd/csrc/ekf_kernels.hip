@@ -234,6 +234,32 @@ __device__ __forceinline__ void st_wt(int* p, int v) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Buffer loads (32-bit offsets; a load past the descriptor's size returns 0 and touches nothing)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double ld_f64(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+}
+__device__ __forceinline__ float ld_t(__amdgpu_buffer_rsrc_t r, unsigned vo, float) {
+  return ld_f32(r, vo, 0);
+}
+__device__ __forceinline__ double ld_t(__amdgpu_buffer_rsrc_t r, unsigned vo, double) {
+  return ld_f64(r, vo, 0);
+}
+
+// A workgroup barrier that orders LDS only: global loads in flight stay in flight across it
+// (__syncthreads waits vmcnt(0), and vmcnt counts loads too).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Intra-workgroup hand-off through LDS (waves on different SIMDs; no s_barrier).
 // The LDS executes one wave's accesses in issue order, so a flag stored after the data is seen
 // after it by any wave: no s_waitcnt before the flag (a release would drain every LDS op of the
@@ -800,6 +826,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   if (nbchk) nb_snapshot(sh, sh.P[ci & 1], 0);
   built = false;
 #endif
+  // A0's associated ids (k_assoc, earlier on this stream), loaded unconditionally (clamped) and
+  // here, so that the barrier below completes them: under A0's branch the load was waited for,
+  // vmcnt(0), together with every early load below
+  const int cA = tid >= 3 && tid < 3 + 2 * d.m ? (tid - 3) >> 1 : 0;
+  const int aj = ctl->assoc_j[min(max(d.assoc_slot + cA, 0), kMaxAssoc - 1)];
   if (A.polls && need && tid == 0 && !built && !epoch_wait_acquire(A.sync + kSyncSigma, need))
     atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
@@ -820,12 +851,56 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // the chain needs from the chunk before: Σ_in' (the other buffer, complete) and its record.
   const ChunkRec* rp = A.rec + static_cast<size_t>(d.parity ^ 1) * A.rec_stride + f;
 
+  constexpr int kW = kMaxU + 1;  // block entries are indexed e = a·36 + b (constant divisor)
+  constexpr int kPer = (kW * kW + kChainThreads - 1) / kChainThreads;  // 6
+  // kLook with staged operands: the loads do not depend on A0's index sets, so they are issued
+  // here and land during A0 (whose barrier orders LDS only)
+  const bool early = look && !built && (d.flags & kStageIn);
+  double vz[kPer], vy[kPer];
+  T vd[kPer], vr[kPer], vc[kPer];  // (as stored: half the registers at fp32 while A0 runs)
+  double r0u = 0.0, c0u = 0.0, r0p = 0.0, c0p = 0.0, x2 = 0.0;
+  double x0 = 0.0, x1 = 0.0, pa1 = 0.0, pa2 = 0.0, tq = 0.0;
+  int pflags = 0;
+  {
+    // staged by the k_patch_stage two chunks back, right behind the Σ pass that wrote Σ_in':
+    // the same values as the gather below, contiguous (≈ 5 000 cycles less than the ≈ 1 900
+    // scattered lines of the gather through one CU). Issued unconditionally, through buffer
+    // descriptors of size 0 unless `early` (zeros, no access): a load under a branch is waited for
+    // at the branch's join on the path that skipped it — vmcnt(0) before A0's first use of `aj`
+    const int tc = tid < kMaxU ? tid : 0;
+    const StageRec<T>* sg = A.stage + static_cast<size_t>(d.parity) * A.rec_stride + f;
+    const auto rs = buf_rsrc(sg, early ? static_cast<unsigned>(sizeof(StageRec<T>)) : 0u);
+    const auto rr = buf_rsrc(rp, early ? static_cast<unsigned>(sizeof(ChunkRec)) : 0u);
+    constexpr unsigned oZ = offsetof(ChunkRec, Z), oY = offsetof(ChunkRec, Y);
+    constexpr unsigned oV = offsetof(StageRec<T>, v), oT = kW * kW * sizeof(T);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + i * kChainThreads, es = min(e, kW * kW - 1);
+      vz[i] = ld_f64(rr, oZ + 8u * (e < kMaxU * kZC ? e : 0), 0);
+      vy[i] = ld_f64(rr, oY + 8u * (e < kZC * kMaxU ? e : 0), 0);
+      vd[i] = ld_t(rs, oV + sizeof(T) * es, T{});
+      vr[i] = ld_t(rs, oV + oT + sizeof(T) * es, T{});
+      vc[i] = ld_t(rs, oV + 2 * oT + sizeof(T) * es, T{});
+    }
+    r0u = ld_f64(rs, offsetof(StageRec<T>, r0u) + 8u * tc, 0);
+    c0u = ld_f64(rs, offsetof(StageRec<T>, c0u) + 8u * tc, 0);
+    r0p = ld_f64(rs, offsetof(StageRec<T>, r0p) + 8u * tc, 0);
+    c0p = ld_f64(rs, offsetof(StageRec<T>, c0p) + 8u * tc, 0);
+    x2 = ld_f64(rs, offsetof(StageRec<T>, xg) + 8u * tc, 0);
+    x0 = ld_f64(rr, offsetof(ChunkRec, xU) + 8u * tc, 0);
+    x1 = ld_f64(rr, offsetof(ChunkRec, Zx) + 8u * tc, 0);
+    pflags = static_cast<int>(__builtin_amdgcn_raw_buffer_load_b32(rr, offsetof(ChunkRec, flags), 0, 0));
+    pa1 = ld_f64(rr, offsetof(ChunkRec, a1), 0);
+    pa2 = ld_f64(rr, offsetof(ChunkRec, a2), 0);
+    tq = ctl->tmo[tid < 3 ? tid : 0];
+  }
+
   // ---- A0: index sets U (this chunk) and U' (kLook: the previous chunk, from the descriptor) ----
   if (tid < kMaxU) {  // u[3+2c], u[4+2c] = the columns of marker c's landmark (bad id → slot 0's)
     int u = tid < 3 ? tid : 0;  // padding 0: loads stay in bounds
     if (tid >= 3 && tid < 3 + 2 * m) {
       const int c = (tid - 3) >> 1, idd = d.ids[c];
-      const int id = idd >= 0 ? idd : ctl->assoc_j[d.assoc_slot + c];
+      const int id = idd >= 0 ? idd : aj;
       const bool bad = id < 0 || id >= A.N;
       u = (bad ? 3 : 3 + 2 * id) + ((tid - 3) & 1);
       if (((tid - 3) & 1) == 0) {
@@ -856,7 +931,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       sh.pv.m = pm;
     }
   }
-  __syncthreads();
+  lds_barrier();
   EKF_STAMP(1);
   const int nu = sh.nu_cnt;
   // The next chunk's block is rebuilt by waves 1–2 during this chunk's corrections (device epochs,
@@ -869,8 +944,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // Each thread issues all of its loads before its first LDS store: indices are clamped rather
   // than predicated (a predicated load becomes a branch with its own wait), so the loads of a
   // thread are in flight together instead of one memory round trip per loop iteration.
-  constexpr int kW = kMaxU + 1;  // block entries are indexed e = a·36 + b (constant divisor)
-  constexpr int kPer = (kW * kW + kChainThreads - 1) / kChainThreads;  // 6
   const int wv = tid >> 6, ln = tid & 63, i16 = ln & 15, k4 = ln >> 4;
   if (look) {
     // Σ_in[U,U] = Σ_pred'[U,U] − K'·M' with Σ_pred' = A'·Σ_in'·A'ᵀ + Q̄' (the previous chunk's
@@ -880,29 +953,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
     const int np = sh.pv.nu;
     if (!built) {  // (built: R̃, K', M', P̃ and the record's scalars are in LDS already)
-    double vz[kPer], vy[kPer], vd[kPer], vr[kPer], vc[kPer];
-    double r0u, c0u, r0p, c0p, x2;
     const int tc = tid < kMaxU ? tid : 0;
-    if (d.flags & kStageIn) {
-      // staged by the k_patch_stage two chunks back, right behind the Σ pass that wrote Σ_in':
-      // the same values as the gather below, contiguous (≈ 5 000 cycles less than the ≈ 1 900
-      // scattered lines of the gather through one CU)
-      const StageRec<T>* sg = A.stage + static_cast<size_t>(d.parity) * A.rec_stride + f;
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const int e = tid + i * kChainThreads, es = min(e, kW * kW - 1);
-        vz[i] = (&rp->Z[0][0])[e < kMaxU * kZC ? e : 0];
-        vy[i] = (&rp->Y[0][0])[e < kZC * kMaxU ? e : 0];
-        vd[i] = static_cast<double>(sg->v[0][es]);
-        vr[i] = static_cast<double>(sg->v[1][es]);
-        vc[i] = static_cast<double>(sg->v[2][es]);
-      }
-      r0u = sg->r0u[tc];
-      c0u = sg->c0u[tc];
-      r0p = sg->r0p[tc];
-      c0p = sg->c0p[tc];
-      x2 = sg->xg[tc];
-    } else {
+    if (!early) {  // (early: the staged operands and the record's values are in registers)
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
         const int e = tid + i * kChainThreads;
@@ -910,9 +962,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         vy[i] = (&rp->Y[0][0])[e < kZC * kMaxU ? e : 0];
         const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);  // clamped: in bounds
         const size_t ua = static_cast<size_t>(sh.u[a]) * ld, pa = static_cast<size_t>(sh.pv.u[b]);
-        vd[i] = static_cast<double>(Sp[ua + sh.u[b]]);
-        vr[i] = static_cast<double>(Sp[ua + pa]);
-        vc[i] = static_cast<double>(Sp[pa * ld + sh.u[a]]);
+        vd[i] = Sp[ua + sh.u[b]];
+        vr[i] = Sp[ua + pa];
+        vc[i] = Sp[pa * ld + sh.u[a]];
       }
       // raw row 0 / column 0 of Σ_in' at U and U' (for the previous predict), x'
       const int uu = sh.u[tc], pu = sh.pv.u[tc];
@@ -921,12 +973,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       r0p = static_cast<double>(Sp[pu]);
       c0p = static_cast<double>(Sp[static_cast<size_t>(pu) * ld]);
       x2 = xp[uu];
+      // record scalars
+      x0 = rp->xU[tc];
+      x1 = rp->Zx[tc];
+      pflags = rp->flags;
+      pa1 = rp->a1;
+      pa2 = rp->a2;
+      tq = ctl->tmo[tid < 3 ? tid : 0];
     }
-    // record scalars
-    const double x0 = rp->xU[tc], x1 = rp->Zx[tc];
-    const int pflags = rp->flags;
-    const double pa1 = rp->a1, pa2 = rp->a2;
-    const double tq = ctl->tmo[tid < 3 ? tid : 0];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * kChainThreads;
@@ -980,10 +1034,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * kChainThreads;
       const int a = e / kW, b = e % kW;
-      double v = vd[i], vR = 0.0, wC = 0.0;
+      double v = static_cast<double>(vd[i]), vR = 0.0, wC = 0.0;
       if (b < np) {
-        vR = vr[i];
-        wC = vc[i];
+        vR = static_cast<double>(vr[i]);
+        wC = static_cast<double>(vc[i]);
       }
       if (pf) {
         const double ai = alpha_of(ua[i], qa1, qa2), aj = alpha_of(ub[i], qa1, qa2);
@@ -1808,16 +1862,6 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
 typedef float f16v __attribute__((ext_vector_type(16)));
 constexpr unsigned kOOB = 0x80000000u;  // voffset past any Σ panel descriptor (32·ld·w < 2 GiB)
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
-}
-__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
-}
-typedef unsigned u2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ double ld_f64(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
-}
 
 template <typename T>
 struct SigmaTile;
