@@ -427,6 +427,9 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       xr[k] = pk[k];
       xq[k] = pm[k];
     }
+    // wave 3's progress, read here (≈ 1 000 cycles into the step, when it has normally finished
+    // step c − 1) and tested below: the flag's LDS round trip off the chain's path
+    const int pd_early = __hip_atomic_load(&sh.pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     {  // K_{c−1} and M_{c−1} of the nx rows / columns: broadcast LDS reads of what step c−1
        // stored (the stored values are the registers' values; two reads instead of 8 readlanes)
       const int l0 = more ? nx : 0, cp = c > 0 ? c - 1 : 0;
@@ -445,14 +448,18 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
     // cross, before this step's cross update writes its Bx rows (wave 3 writes these entries for
     // step c only after the publish below, whose release waits for the reads)
     if (c + 2 < m) {
-      lds_wait_ge3(&sh.pdone, c);
+      // the LDS serves this wave's accesses in order, and wave 3 stored its entries before the
+      // flag: once a flag value ≥ c has been read, later reads see the entries (a compiler fence
+      // keeps them after the test)
+      if (__builtin_amdgcn_readfirstlane(pd_early) < c) lds_wait_ge3(&sh.pdone, c);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         rn[j] = sh.P[pb][lr][nx + 2 + j];
         qn[j] = sh.P[pb][nx + 2 + j][lr];
       }
     }
-    const int jx = sh.u[pj];
+    const int jx = __builtin_amdgcn_readlane(ul, pj);  // sh.u[pj] (ul = sh.u[lane], pj < kMaxU)
     EKF_STAMP(67 + 8 * c);
     const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
     const double K1 = ka * Si[1] + kb * Si[3];
@@ -515,7 +522,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       geometry(c + 1);
       // wave 3's step c−1 writes outside this step's cross must land before this cross update
       // overwrites the nx columns / rows (waited for above already when c + 2 < m)
-      if (c + 2 >= m) lds_wait_ge3(&sh.pdone, c);
+      if (c + 2 >= m && __builtin_amdgcn_readfirstlane(pd_early) < c) lds_wait_ge3(&sh.pdone, c);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
       // all rows × Bx columns: next step's pk
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
