@@ -1670,14 +1670,24 @@ struct FactorShared {
 // Kcat = R_pred·Z (rows) and Mcat = Y·C_pred (columns) on f64 MFMA, plus the new state.
 // 16 rows or 16 columns per wave; R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j].
 template <typename T>
-__global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
+__global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int nf) {
   __shared__ FactorShared sh;
+  // xcd_b = 0: grid (blocks per filter, filters). xcd_b = B > 0 (swarms): the Σ pass's XCD-aware
+  // 1-D grid — block L on XCD L % 8 takes filter 8·⌊(L/8)/B⌋ + L % 8, block (L/8) % B — so a
+  // filter's record is fetched into one L2 instead of eight. Placement only changes speed.
+  int fb = blockIdx.y, bx = blockIdx.x;
+  if (xcd_b > 0) {
+    const int L = blockIdx.x, j = L >> 3;
+    fb = (L & 7) + 8 * (j / xcd_b);
+    bx = j % xcd_b;
+  }
   // the previous chunk's Σ pass ended before this launch (same stream): its epoch, for the chains
   if (A.pub_sigma && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     epoch_store(A.sync + kSyncSigma, A.pub_sigma);
-  const MsgDesc& d = A.desc[blockIdx.y];
+  if (fb >= nf) return;
+  const MsgDesc& d = A.desc[fb];
   if (!(d.flags & kActive)) return;
-  const int f = A.f0 + blockIdx.y;
+  const int f = A.f0 + fb;
   const int tid = threadIdx.x;
   const int n = A.n, ld = A.ld, ldk = A.ldk;
   const T* S = A.sig[d.parity] + f * A.sig_stride;
@@ -1715,7 +1725,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
     }
   }
   if (tid < kMaxU) {
-    const int ub = rec->u[tid], rnu = rec->nu, rbase = blockIdx.x * 64;
+    const int ub = rec->u[tid], rnu = rec->nu, rbase = bx * 64;
     sh.u[tid] = ub;
     if (tid < rnu && ub >= rbase && ub < rbase + 64) atomicMin(&sh.pos64[ub - rbase], tid);
     sh.alphaU[tid] = rec->alphaU[tid];
@@ -1736,7 +1746,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
   // ---- phase B: Kcat = R_pred·Z, Mcat = Y·C_pred on f64 MFMA, 16 rows (or columns) per wave ----
   // R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j] (predict folded in as above).
   const int lane = tid & 63;
-  const int wg = blockIdx.x * (blockDim.x >> 6) + (tid >> 6);  // global wave index
+  const int wg = bx * (blockDim.x >> 6) + (tid >> 6);  // the filter's wave index
   const int row_tiles = (n + 15) / 16;
   const int ks = lane >> 4, l16 = lane & 15;
   const double s00 = sh.s00;
@@ -1784,7 +1794,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A) {
       acc1 = mfma_f64(av[s], z1, acc1);
       acc2 = mfma_f64(av[s], zx, acc2);
     }
-    const int rbase = blockIdx.x * 64;
+    const int rbase = bx * 64;
     if (vi && ks == 0) {  // the predict's two rank-1 factors (slam.cpp:198)
       kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
       kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
@@ -2475,8 +2485,13 @@ template <typename T>
 hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1) {
   const int waves = 2 * ((a.n + 15) / 16);  // 16 rows or 16 columns per wave
-  const dim3 grid((waves + 3) / 4, nf);
-  launch(k_factors<T>, grid, dim3(256), s, e0, e1, a);
+  const int per_filter = (waves + 3) / 4;
+  if (nf >= 16) {  // XCD-aware 1-D grid, as the swarm's Σ pass
+    launch(k_factors<T>, dim3(8 * ((nf + 7) / 8) * per_filter), dim3(256), s, e0, e1, a,
+           per_filter, nf);
+  } else {
+    launch(k_factors<T>, dim3(per_filter, nf), dim3(256), s, e0, e1, a, 0, nf);
+  }
   return hipGetLastError();
 }
 
