@@ -1984,9 +1984,17 @@ struct SigmaTile<float> {
 // (≥ 16 filters): the M operand rows are read once per 64 columns instead of per 32 — the
 // operand loads are the pass's VMEM bottleneck there (swarm pass 589 → 564 µs; one filter's pass
 // 5.2 → 7.6 µs, so it keeps TJ = 2)
+// 2 = nt: the swarm's 2.2 GB of Σ stream through HBM once per message (≫ the 256 MB MALL), so its
+// Σ_in loads and Σ_out stores skip cache retention — swarm 1.09e7 → 1.15e7 corrections/s
+// (profiles/r2/r2z_*, two alternating runs each). The MALL-resident single-filter tiles keep the default.
+#ifndef EKF_SIG_POL
+#define EKF_SIG_POL 2
+#endif
 template <int TJ_>
 struct SigmaTile64 {
   static constexpr int TJ = TJ_;
+  // cache policy of the swarm tile's Σ_in loads / Σ_out stores (the swarm's Σ streams through HBM)
+  static constexpr int kPol = TJ == 4 ? EKF_SIG_POL : 0;
   static constexpr int kRows = 32, kCols = 16 * TJ;
   // rows ≠ null (kRowsOut): also Σ_out[i, U_next] → rows[b·ldk + i] for the next chunk's factor
   // kernel, b = the first position of the column in U_next (nxt[0..nnu))
@@ -2027,7 +2035,8 @@ struct SigmaTile64 {
       for (int tj = 0; tj < TJ; ++tj)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          sv[ti][tj][r] = ld_f64(rin, so[tj] + (16 * ti + 4 * r) * rstride, 0);
+          sv[ti][tj][r] = __builtin_bit_cast(
+              double, __builtin_amdgcn_raw_buffer_load_b64(rin, so[tj] + (16 * ti + 4 * r) * rstride, 0, kPol));
     d4 acc[2][TJ];
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
@@ -2067,7 +2076,7 @@ struct SigmaTile64 {
           double v = sv[ti][tj][r] - acc[ti][tj][r];
           if (first && row == col && row < 3) v += q;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rout,
-                                                so[tj] + (16 * ti + 4 * r) * rstride, 0, 0);
+                                                so[tj] + (16 * ti + 4 * r) * rstride, 0, kPol);
           if (bpos[tj] >= 0 && row < n) rows[static_cast<size_t>(bpos[tj]) * ldk + row] = v;
         }
   }
