@@ -442,13 +442,24 @@ def run(args, rank, world, local, backend=None):
     if world > 1:
         dist.barrier()
     be.sync()
+    trace = os.environ.get("EKF_BENCH_TRACE") == "1"  # dev: host clocks around the timed region
     t0 = time.perf_counter()
+    if trace:
+        clk = [("t0", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+                time.clock_gettime_ns(time.CLOCK_BOOTTIME))]
     msgs(t0s, t0s + K)
+    if trace:
+        clk.append(("enqueued", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+                    time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
     ekf.sync()
     be.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if trace:
+        clk.append(("synced", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+                    time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
+        print(json.dumps({"trace_clocks": clk}), file=sys.stderr, flush=True)
     live = np.arange(act.shape[2]) < counts[t0s:t0s + K][..., None]
     corrections = int(np.count_nonzero(live & (act[t0s:t0s + K] != 2)))  # slam.cpp:205
     poses = np.stack([ekf.pose(f) for f in range(F)])

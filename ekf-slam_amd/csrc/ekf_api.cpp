@@ -91,8 +91,9 @@ struct ekf_ctx {
   std::vector<MsgDesc> plan_d;
   std::vector<Launch> plan_l;
   size_t ddesc_cap = 0;
-  // pinned staging ring (the host may run kRing uploads ahead of the device)
+  // pinned staging ring (the host may run kRing uploads ahead of the device), every slot ring_cap
   StageSlot ring[kRing];
+  size_t ring_cap = 0;
   int ring_next = 0;
   // scratch
   std::vector<std::vector<Marker>> msgs;
@@ -480,6 +481,46 @@ int posterior_launch(ekf_ctx* h, const MsgDesc* dp, int f0, int nf) {
   return e == hipSuccess ? EKF_OK : EKF_E_HIP;
 }
 
+// Upload capacity for `need` descriptors: the device buffer and EVERY pinned ring slot grow together
+// (geometrically), so an allocation happens the first time a plan this large is seen, never on a
+// later same-sized call that lands on a ring slot not used before (a hipHostMalloc costs ≈ 120 µs,
+// a device re-allocation a drain: round 3 measured both inside a 20-message bench region).
+constexpr size_t kDescInit = 256;  // descriptors at creation (×F/64 for wide handles)
+int reserve_upload(ekf_ctx* h, size_t need) {
+  if (need > h->ddesc_cap) {  // the previous launch may still read the old buffer
+    if (drain(h)) return EKF_E_HIP;
+    if (h->ddesc) HIPCHK(hipFree(h->ddesc));
+    h->ddesc = nullptr;
+    const size_t cap = std::max(need, 2 * h->ddesc_cap);
+    if (hipMalloc(&h->ddesc, cap * sizeof(MsgDesc)) != hipSuccess) return EKF_E_NOMEM;
+    h->ddesc_cap = cap;
+  }
+  if (need > h->ring_cap || !h->ring[0].p) {
+    const size_t cap = std::max(need, std::max(h->ring_cap, h->ddesc_cap));
+    for (StageSlot& sl : h->ring) {
+      if (sl.used) HIPCHK(hipEventSynchronize(sl.ev));
+      if (sl.p) HIPCHK(hipHostFree(sl.p));
+      sl.p = nullptr;
+      sl.used = false;
+      if (hipHostMalloc(reinterpret_cast<void**>(&sl.p), cap * sizeof(MsgDesc),
+                        hipHostMallocDefault) != hipSuccess)
+        return EKF_E_NOMEM;
+      sl.cap = cap;
+    }
+    h->ring_cap = cap;
+  }
+  return EKF_OK;
+}
+
+// The next pinned staging slot, once the device is done with its last upload.
+int next_slot(ekf_ctx* h, StageSlot** out) {
+  StageSlot& sl = h->ring[h->ring_next];
+  h->ring_next = (h->ring_next + 1) % kRing;
+  if (sl.used) HIPCHK(hipEventSynchronize(sl.ev));
+  *out = &sl;
+  return EKF_OK;
+}
+
 // Resident path: the plan's descriptors and its entry list (packed behind them, in MsgDesc-sized
 // slots) go up with one copy, then ONE kernel launch runs the whole plan, a workgroup per filter.
 int flush_resident(ekf_ctx* h) {
@@ -487,26 +528,10 @@ int flush_resident(ekf_ctx* h) {
   if (nl == 0) return EKF_OK;
   const size_t pslots = (nl * sizeof(PlanEntry) + sizeof(MsgDesc) - 1) / sizeof(MsgDesc);
   const size_t ns = nd + pslots;
-  if (ns > h->ddesc_cap) {  // the previous launch may still read the old buffer
-    if (drain(h)) return EKF_E_HIP;
-    if (h->ddesc) HIPCHK(hipFree(h->ddesc));
-    h->ddesc = nullptr;
-    const size_t cap = std::max(ns, 2 * h->ddesc_cap);
-    if (hipMalloc(&h->ddesc, cap * sizeof(MsgDesc)) != hipSuccess) return EKF_E_NOMEM;
-    h->ddesc_cap = cap;
-  }
-  StageSlot& sl = h->ring[h->ring_next];
-  h->ring_next = (h->ring_next + 1) % kRing;
-  if (sl.used) HIPCHK(hipEventSynchronize(sl.ev));
-  if (ns > sl.cap) {
-    if (sl.p) HIPCHK(hipHostFree(sl.p));
-    sl.p = nullptr;
-    const size_t cap = std::max<size_t>(ns, 64);
-    if (hipHostMalloc(reinterpret_cast<void**>(&sl.p), cap * sizeof(MsgDesc),
-                      hipHostMallocDefault) != hipSuccess)
-      return EKF_E_NOMEM;
-    sl.cap = cap;
-  }
+  if (int rc = reserve_upload(h, ns)) return rc;
+  StageSlot* slp = nullptr;
+  if (int rc = next_slot(h, &slp)) return rc;
+  StageSlot& sl = *slp;
   std::memcpy(sl.p, h->plan_d.data(), nd * sizeof(MsgDesc));
   PlanEntry* pe = reinterpret_cast<PlanEntry*>(sl.p + nd);
   int flo = INT_MAX, fhi = 0;
@@ -536,26 +561,10 @@ int flush(ekf_ctx* h) {
   if (h->resident) return flush_resident(h);
   const size_t nd = h->plan_d.size();
   if (nd == 0) return EKF_OK;
-  if (nd > h->ddesc_cap) {  // grow the device descriptor buffer (kernels may still read the old one)
-    if (drain(h)) return EKF_E_HIP;
-    if (h->ddesc) HIPCHK(hipFree(h->ddesc));
-    h->ddesc = nullptr;
-    const size_t cap = std::max(nd, 2 * h->ddesc_cap);
-    if (hipMalloc(&h->ddesc, cap * sizeof(MsgDesc)) != hipSuccess) return EKF_E_NOMEM;
-    h->ddesc_cap = cap;
-  }
-  StageSlot& sl = h->ring[h->ring_next];
-  h->ring_next = (h->ring_next + 1) % kRing;
-  if (sl.used) HIPCHK(hipEventSynchronize(sl.ev));
-  if (nd > sl.cap) {
-    if (sl.p) HIPCHK(hipHostFree(sl.p));
-    sl.p = nullptr;
-    const size_t cap = std::max<size_t>(nd, 64);
-    if (hipHostMalloc(reinterpret_cast<void**>(&sl.p), cap * sizeof(MsgDesc),
-                      hipHostMallocDefault) != hipSuccess)
-      return EKF_E_NOMEM;
-    sl.cap = cap;
-  }
+  if (int rc = reserve_upload(h, nd)) return rc;
+  StageSlot* slp = nullptr;
+  if (int rc = next_slot(h, &slp)) return rc;
+  StageSlot& sl = *slp;
   std::memcpy(sl.p, h->plan_d.data(), nd * sizeof(MsgDesc));
   if (join_bulk(h)) return EKF_E_HIP;  // the bulk stream may still read descriptors
   HIPCHK(hipMemcpyAsync(h->ddesc, sl.p, nd * sizeof(MsgDesc), hipMemcpyHostToDevice, h->stream));
@@ -692,6 +701,7 @@ int handle_info(ekf_t h, HandleInfo* out) {
   out->device = h->cfg.device;
   out->resident = h->resident;
   out->rows = h->rows != nullptr && !h->resident;
+  out->joseph = h->joseph;
   out->stream = h->stream;
   return EKF_OK;
 }
@@ -703,8 +713,8 @@ int handle_parity(ekf_t h, int* parity) {
 }
 
 int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
-                    const int* parity_after) {
-  if (!h || T < 0 || !dd || !parity_after) return EKF_E_ARG;
+                    const int* parity_after, const double* odom_after) {
+  if (!h || T < 0 || !dd || !parity_after || !odom_after) return EKF_E_ARG;
   hipSetDevice(h->cfg.device);
   int rc = EKF_OK;
   if (T > 0) {
@@ -728,6 +738,7 @@ int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
   }
   for (int f = 0; f < h->F; ++f) {
     h->parity[f] = parity_after[f];
+    h->odom[f] = Pose2{odom_after[3 * f], odom_after[3 * f + 1], odom_after[3 * f + 2]};
     h->pending[f] = 0;
     h->prev_m[f] = -1;
     forget_desc(h, f);
@@ -838,11 +849,12 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + h->F);
   if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
-  h->ddesc_cap = static_cast<size_t>(h->F) * 4;
+  h->ddesc_cap = std::max(kDescInit, static_cast<size_t>(h->F) * 4);
   if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->ddesc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
   for (int i = 0; i < kRing; ++i)
     if (hipEventCreateWithFlags(&h->ring[i].ev, hipEventDisableTiming) != hipSuccess)
       return fail(EKF_E_HIP);
+  if (int rc = reserve_upload(h, h->ddesc_cap)) return fail(rc);  // every pinned slot up front
   // Σ₀ = diag(0,0,0, init_var·I_2N), state = 0 (slam.cpp:127-132, :674)
   for (int p = 0; p < 2; ++p) {
     if (hipMemsetAsync(h->sig[p], 0, sig_bytes, h->stream) != hipSuccess) return fail(EKF_E_HIP);

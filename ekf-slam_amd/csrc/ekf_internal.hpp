@@ -13,6 +13,7 @@ struct HandleInfo {
   int F, N, n, dtype, device;
   bool resident;  // n ≤ kResidentMaxN fp64: one resident launch per plan
   bool rows;      // fp64 pipeline: Σ-pass → factor-kernel row hand-off planned
+  bool joseph;    // ekf_set_joseph is on (the HBM pipeline then needs one marker per chunk)
   hipStream_t stream;
 };
 
@@ -23,8 +24,9 @@ int handle_parity(ekf_t h, int* parity);
 // T messages whose descriptors the device wrote into dd[t·F + f] on the handle's main stream (one
 // known-association chunk per message, the first of each filter non-pipelined), and for the
 // resident path the plan entries dplan[T]. Enqueues the filter kernels behind them; then the host
-// mirror takes parity_after[F], no pending predict, and a non-pipelined next chunk.
+// mirror takes parity_after[F], odom_after[F][3] (t_odom_robot after the plan's last message, the
+// predict input of the next host-planned call), no pending predict, and a non-pipelined next chunk.
 int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
-                    const int* parity_after);
+                    const int* parity_after, const double* odom_after);
 
 }  // namespace ekfslam

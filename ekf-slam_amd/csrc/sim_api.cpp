@@ -32,6 +32,7 @@ struct ekf_sim {
   hipEvent_t ev_sim = nullptr;      // simulation of the current run done
   hipEvent_t ev_done[2] = {nullptr, nullptr};  // filter work of the run that used buffer b done
   int* host_par_pinned = nullptr;
+  SimState* host_st_pinned = nullptr;  // [F] poses after the last run (the handle's t_odom_robot)
   int buf = 0;                      // run buffer of the next run
   double* cmd[2] = {nullptr, nullptr};
   int* sense[2] = {nullptr, nullptr};
@@ -47,6 +48,7 @@ struct ekf_sim {
   double* odom = nullptr;
   int last_T = 0;
   std::vector<int> host_par;
+  std::vector<double> host_odom;    // [F][3] t_odom_robot after the last run
 };
 
 namespace {
@@ -98,13 +100,15 @@ int reserve(ekf_sim* s, int T) {
     free_run(s);
     return EKF_E_NOMEM;
   }
-  s->cap_msgs = Tn;
-  s->cap_ticks = tk;
   // the resident plan: one entry per message, every filter (off = t·F)
   std::vector<PlanEntry> pe(Tn);
   for (size_t t = 0; t < Tn; ++t) pe[t] = PlanEntry{static_cast<int>(t * F), 0, static_cast<int>(F), 0};
-  if (hipMemcpy(s->plan, pe.data(), Tn * sizeof(PlanEntry), hipMemcpyHostToDevice) != hipSuccess)
+  if (hipMemcpy(s->plan, pe.data(), Tn * sizeof(PlanEntry), hipMemcpyHostToDevice) != hipSuccess) {
+    free_run(s);  // no capacity is recorded for buffers whose plan never arrived
     return EKF_E_HIP;
+  }
+  s->cap_msgs = Tn;
+  s->cap_ticks = tk;
   return EKF_OK;
 }
 
@@ -165,6 +169,8 @@ int ekf_sim_create(ekf_sim_t* out, ekf_t filter, const ekf_sim_config* cfg, int 
        hipEventCreateWithFlags(&s->ev_done[1], hipEventDisableTiming) == hipSuccess &&
        hipHostMalloc(reinterpret_cast<void**>(&s->host_par_pinned), F * sizeof(int),
                      hipHostMallocDefault) == hipSuccess &&
+       hipHostMalloc(reinterpret_cast<void**>(&s->host_st_pinned), F * sizeof(SimState),
+                     hipHostMallocDefault) == hipSuccess &&
        hipEventRecord(s->ev_done[0], s->info.stream) == hipSuccess &&
        hipEventRecord(s->ev_done[1], s->info.stream) == hipSuccess &&
        hipMemcpy(s->lm, landmarks, F * n_map * 2 * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
@@ -175,6 +181,7 @@ int ekf_sim_create(ekf_sim_t* out, ekf_t filter, const ekf_sim_config* cfg, int 
     return EKF_E_NOMEM;
   }
   s->host_par.assign(F, 0);
+  s->host_odom.assign(3 * F, 0.0);
   *out = s;
   return EKF_OK;
 }
@@ -188,6 +195,7 @@ int ekf_sim_destroy(ekf_sim_t s) {
                   static_cast<void*>(s->st), static_cast<void*>(s->par)})
     if (p) hipFree(p);
   if (s->host_par_pinned) hipHostFree(s->host_par_pinned);
+  if (s->host_st_pinned) hipHostFree(s->host_st_pinned);
   for (hipEvent_t e : {s->ev_sim, s->ev_done[0], s->ev_done[1]})
     if (e) hipEventDestroy(e);
   if (s->sst) hipStreamDestroy(s->sst);
@@ -205,6 +213,10 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
         return EKF_E_ARG;
     }
   if (int rc = handle_info(s->h, &s->info)) return rc;  // host-planned work first, bulk joined
+  // Joseph form on the HBM pipeline takes one marker per chunk (ekf_api.cpp plan_known); the
+  // device planner writes one chunk per message, so it cannot honour it: refuse rather than run
+  // the simple form silently (the resident path carries the form in its own kernel)
+  if (s->info.joseph && !s->info.resident) return EKF_E_ARG;
   hipSetDevice(s->info.device);
   if (int rc = reserve(s, T)) return rc;
   const int b = s->buf;
@@ -260,18 +272,23 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
   a.radius = s->cfg.wheel_radius;
   a.track = s->cfg.track_width;
   if (launch_sim(a, st) != hipSuccess) return EKF_E_HIP;
-  // each filter's final parity (its inactive messages do not flip it): the host mirror
+  // each filter's final parity (its inactive messages do not flip it) and odometry: the host mirror
   if (hipMemcpyAsync(s->host_par_pinned, s->par, F * sizeof(int), hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipMemcpyAsync(s->host_st_pinned, s->st, F * sizeof(SimState), hipMemcpyDeviceToHost, st) !=
           hipSuccess ||
       hipEventRecord(s->ev_sim, st) != hipSuccess || hipEventSynchronize(s->ev_sim) != hipSuccess)
     return EKF_E_HIP;
   std::memcpy(s->host_par.data(), s->host_par_pinned, F * sizeof(int));
+  for (size_t f = 0; f < F; ++f)
+    for (int k = 0; k < 3; ++k) s->host_odom[3 * f + k] = s->host_st_pinned[f].odom[k];
   s->tick += static_cast<long long>(ticks);
   s->msg += T;
   s->last_T = T;
   // the filter's kernels behind the simulation (their descriptors), then release buffer b
   if (hipStreamWaitEvent(s->info.stream, s->ev_sim, 0) != hipSuccess) return EKF_E_HIP;
-  const int rc = run_device_plan(s->h, s->desc[b], s->plan, T, s->host_par.data());
+  const int rc = run_device_plan(s->h, s->desc[b], s->plan, T, s->host_par.data(),
+                                 s->host_odom.data());
   if (rc) return rc;
   if (int r2 = handle_info(s->h, &s->info)) return r2;  // joins the bulk stream into main
   return hipEventRecord(s->ev_done[b], s->info.stream) == hipSuccess ? EKF_OK : EKF_E_HIP;

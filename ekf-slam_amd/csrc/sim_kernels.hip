@@ -92,6 +92,7 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
   const double* lm = A.lm + static_cast<size_t>(f) * L * 2;
   const int words = (L + 31) / 32;
   for (int w = lane; w < words; w += 64) sh.sighted[w] = A.sighted[static_cast<size_t>(f) * words + w];
+  __syncthreads();  // (one wave: order the lanes' LDS writes before any lane reads another's word)
   // the true pose (slipping wheels) and the odometry (commanded encoder angles), wave-uniform
   Pose2 truth{S.truth[0], S.truth[1], S.truth[2]};
   Pose2 odo{S.odom[0], S.odom[1], S.odom[2]};
@@ -150,6 +151,7 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
         if (mode == kSenseAll) key[j] = d;  // (the ADD / DELETE test below)
       }
     }
+    __syncthreads();  // sh.bx / sh.by of every lane before the survey fallback reads them
     int k = 0;
     if (mode == kSenseAll) {
       k = L;  // every landmark, in id order (L ≤ kMaxChunk, checked on the host)

@@ -8,7 +8,12 @@
  *                                                      DiffDrive::FKin(true wheel angles)
  *                                                      (turtlelib/src/diff_drive.cpp:10-28)
  *   slam jointStateCallback nuslam/src/slam.cpp:599-634 t_odom_robot = FKin(encoder angles): the
- *                                                      encoders report the commanded angles
+ *                                                      encoders report the COMMANDED angles — a
+ *                                                      deliberate change from nusim, whose encoders
+ *                                                      publish the slipped wheel_pos_l/r
+ *                                                      (nusim.cpp:272-273), so its odometry follows
+ *                                                      the truth; here odometry drifts from the
+ *                                                      truth and the filter has work to do
  *   nusim sensor_timer_callback nusim.cpp:317-346      marker = landmark in the true body frame
  *                                                      + N(0, σ²) on x and y; ADD within range,
  *                                                      DELETE beyond (mode ALL) or the m nearest
@@ -63,7 +68,11 @@ int ekf_sim_destroy(ekf_sim_t s);
  * right; every filter's), sense[T] EKF_SENSE_* per message (NULL: NEAREST). Simulates, senses and
  * plans on the device, then runs the filter over the T messages (asynchronous like ekf_replay; the
  * call waits only for the device planning). A filter with no marker in a message gets no message
- * (as ekf_replay with counts 0). */
+ * (as ekf_replay with counts 0). Afterwards the handle's t_odom_robot is the run's last odometry
+ * pose, as if ekf_set_odom had been called with it (the next host-planned call predicts from it).
+ * EKF_E_ARG when ekf_set_joseph is on and the handle runs the HBM pipeline (fp32, or n > 128): the
+ * device planner writes one multi-marker chunk per message, the Joseph form there needs one marker
+ * per chunk (the resident path honours it). */
 int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense);
 
 /* With cfg.record: the last run's inputs as ekf_replay would take them — counts[T][F],

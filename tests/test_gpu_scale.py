@@ -18,8 +18,8 @@ differ by 1.8e-8 in Σ on the N=256 populated drive (152 survey + 25 circle mess
 sightings), so 1e-7 is 5× that floor. The chunked update also carries a chunk's first-sighting
 prior into its later corrections' factor products (K_c = r₀·Z_c, x += r₀·Zx), each rounding at
 ~1e7·ε: the state lands ≈1e-8 from the oracle after a survey (1.0e-9 between the two CPU
-restatements), hence 5e-8. fp32 Σ: poses within 2e-4 of the fp64 oracle. Measured errors go to
-gpurun_out/scale_errors.json.
+restatements), hence 5e-8. fp32 Σ: poses 1e-6, state 1e-5 and Σ 5e-5 absolute against the fp64
+oracle (20–40× the measured errors). Measured errors go to gpurun_out/scale_errors.json.
 """
 import json
 import os
@@ -36,6 +36,12 @@ pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-8
 STATE_TOL = 5e-8
 SIGMA_TOL = 1e-7
+# fp32 Σ (configs[2]) against the fp64 oracle from the same warm state: Σ entries are O(1) or
+# below on the populated map, so fp32's 6e-8 relative rounding over 16 rank-2 terms per pass and
+# 40 passes lands ≈1e-6 absolute (measured, gpurun_out/scale_errors.json)
+F32_POSE_TOL = 1e-6
+F32_STATE_TOL = 1e-5
+F32_SIGMA_TOL = 5e-5
 ERRORS = {}
 
 
@@ -174,9 +180,11 @@ def test_n1024_fp32_populated_against_oracle(n1024, env, monkeypatch):
     ERRORS["n1024_fp32_" + ("devsync" if env["EKF_DEVSYNC"] == "1" else "events")] = {
         "pose": err, "state": float(np.abs(x32 - xr).max()),
         "sigma": float(np.abs(S32 - Sr).max())}
-    assert err < 2e-4
+    # measured (round 2): pose 2.8e-8, state 5.0e-7, Σ 1.3e-6 — bounds ≈ 20–40× above
+    assert err < F32_POSE_TOL
     assert np.all(np.isfinite(S32))
-    assert np.abs(x32 - xr).max() < 2e-4
+    assert np.abs(x32 - xr).max() < F32_STATE_TOL
+    assert np.abs(S32 - Sr).max() < F32_SIGMA_TOL
 
 
 @pytest.mark.parametrize("devsync", ["1", "0"], ids=["devsync", "events"])
@@ -232,8 +240,8 @@ def test_n1024_helper_rebuild_bit_identical(n1024, dtype, monkeypatch):
 def test_n1024_joseph_populated_against_oracle(n1024, dtype):
     """configs[2]'s populated map with the Joseph form (BASELINE.json north_star; ekf_set_joseph)
     on the HBM pipeline: 6 circle messages (96 corrections, one Σ pass each) from the fp64 survey's
-    state against the oracle's Joseph mode. fp32 poses within 2e-4 (as the simple form), fp64 state
-    5e-8 and Σ 1e-7 (the populated-map tolerances above)."""
+    state against the oracle's Joseph mode. fp32 within the fp32 tolerances above (poses 1e-6,
+    state 1e-5, Σ 5e-5), fp64 state 5e-8 and Σ 1e-7 (the populated-map tolerances above)."""
     sc, odom, ws = n1024
     w, T = sc.n_warm, 6
     e = pyekf.EKF(n_landmarks=1024, dtype=dtype)
@@ -255,9 +263,11 @@ def test_n1024_joseph_populated_against_oracle(n1024, dtype):
     xr, Sr, _, _ = ref.get()
     ERRORS["n1024_joseph_" + ("f32" if dtype == pyekf.EKF_F32 else "f64")] = {
         "pose": err, "state": float(np.abs(xg - xr).max()), "sigma": float(np.abs(Sg - Sr).max())}
-    if dtype == pyekf.EKF_F32:
-        assert err < 2e-4
+    if dtype == pyekf.EKF_F32:  # measured (round 2): pose 4.2e-8, Σ 1.8e-6
+        assert err < F32_POSE_TOL
         assert np.all(np.isfinite(Sg))
+        assert np.abs(xg - xr).max() < F32_STATE_TOL
+        assert np.abs(Sg - Sr).max() < F32_SIGMA_TOL
     else:
         assert err < POSE_TOL
         assert np.abs(xg - xr).max() < STATE_TOL

@@ -139,3 +139,52 @@ def test_sim_schedules_and_host_replay_agree(monkeypatch):
         assert np.abs(x - out[0][f][0]).max() < 1e-9
         assert np.abs(S - out[0][f][1]).max() < 1e-8
     e.close()
+
+
+def test_sim_then_host_call_predicts_from_the_sims_odometry():
+    """After ekf_sim_run the handle's t_odom_robot is the run's last odometry pose (the device
+    integrated the encoders, slam.cpp:599-634): a host ekf_batch_sensor with odom = NULL then
+    predicts from it, as the oracle fed the same odometry does (fp64 pipeline, N = 64)."""
+    N, F, T = 64, 2, 10
+    sw = synth.swarm(N, F, T + 1)
+    Tw = sw.count.shape[0] - 1  # the sim runs all but the last message; the host sends that one
+    e = pyekf.EKF(n_landmarks=N, n_filters=F)
+    sim = _sim_for(e, sw)
+    tpm = sw.wheel.shape[1]
+    sim.run(sw.cmd[:Tw * tpm], sw.sense[:Tw])
+    cnt, ids, act, rel = sim.markers()
+    odom = sim.poses()[0]
+    t = Tw
+    assert e.batch_sensor(sw.count[t], sw.rel[t], None, ids=sw.ids[t], actions=sw.actions[t]) == 0
+    for f in range(F):
+        ref = orc.OracleEKF(n_landmarks=N)
+        for k in range(Tw):
+            ref.set_odom(odom[k])
+            c = int(cnt[k, f])
+            ref.fake_sensor_cb(ids[k, f, :c], act[k, f, :c], rel[k, f, :c])
+        c = int(sw.count[t, f])  # odometry unchanged since the run: t_odom_robot = odom[Tw - 1]
+        ref.fake_sensor_cb(sw.ids[t, f, :c], sw.actions[t, f, :c], sw.rel[t, f, :c])
+        x, S, _ = e.state(f)
+        xr, Sr, _, _ = ref.get()
+        assert e.status(f) == 0
+        assert np.abs(x - xr).max() < STATE_TOL_POPULATED, f
+        assert np.abs(S - Sr).max() < SIGMA_TOL, f
+    sim.close()
+    e.close()
+
+
+def test_sim_refuses_joseph_on_the_pipeline():
+    """ekf_set_joseph on an HBM-pipeline handle (fp32): the device planner cannot write the
+    one-marker chunks the form needs there, so ekf_sim_run returns EKF_E_ARG instead of running
+    the simple form; with the form off again the same run goes through."""
+    N, F = 64, 2
+    sw = synth.swarm(N, F, 4)
+    e = pyekf.EKF(n_landmarks=N, n_filters=F, dtype=pyekf.EKF_F32)
+    sim = _sim_for(e, sw)
+    assert e.set_joseph(True) == pyekf.EKF_OK
+    with pytest.raises(pyekf.EkfError) as ei:
+        sim.run(sw.cmd[:sw.wheel.shape[1]], sw.sense[:1])
+    assert ei.value.rc == pyekf.EKF_E_ARG
+    assert e.set_joseph(False) == pyekf.EKF_OK
+    sim.close()
+    e.close()
