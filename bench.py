@@ -48,7 +48,20 @@ WORKLOADS = {
     # per workgroup): configs[0]'s filter × 1024 seeded runs per GPU
     "swarm_basic_world": (50, "f64", 1024, 4,
                           "configs[0] x 1024 Monte-Carlo runs per GPU (basic_world, fp64)"),
+    # configs[2] at the reference's own precision (slam.cpp is fp64 throughout)
+    "n1024_fp64": (1024, "f64", 1, 16, "configs[2] at fp64: N=1024 synthetic landmarks, 1 filter"),
+    # unknown association (sensor_cb, slam.cpp:318-530): ids stripped, every marker scored against
+    # the 960 mapped landmarks (64 slots left for new ones)
+    "n1024_fp32_assoc": (1024, "f32", 1, 16, "configs[2] with unknown association (sensor_cb): "
+                                              "N=1024 slots, 960 mapped landmarks, fp32"),
+    "n1024_fp64_assoc": (1024, "f64", 1, 16, "configs[2] with unknown association (sensor_cb): "
+                                              "N=1024 slots, 960 mapped landmarks, fp64"),
 }
+ASSOC_FREE_SLOTS = 64  # association workloads map N − 64 landmarks (room for new ones)
+
+
+def is_assoc(workload):
+    return workload.endswith("_assoc")
 
 
 def parse(argv=None):
@@ -329,12 +342,13 @@ class HipBackend:
         self.torch.cuda.synchronize()
 
 
-def build_inputs(N, F, T, seed, m, rank):
+def build_inputs(N, F, T, seed, m, rank, n_map=None):
     """SURVEY.md §8d inputs for this rank's F filters: global filter g = rank·F + f is seeded
     seed + g (its own map, slip and sensor noise); the survey warm-up (every landmark sighted)
     precedes T messages of the circle drive. N = 50 is configs[0]'s basic_world (4 landmarks,
-    every one in view, no survey needed). Returns the synth.Swarm (its drive, maps and the host
-    restatement of every marker) and the odometry."""
+    every one in view, no survey needed). n_map < N landmarks are placed (association workloads:
+    the rest of the slots stay free for new landmarks). Returns the synth.Swarm (its drive, maps and
+    the host restatement of every marker) and the odometry."""
     from pyekf import synth
     import pyekf
     if N == 50:
@@ -344,8 +358,9 @@ def build_inputs(N, F, T, seed, m, rank):
                              start_pose=(synth.BASIC_WORLD_THETA0, 0.0, 0.0))
         n_target = 4
     else:
-        sw = synth.swarm(N, F, T, seed=seed + rank * F, max_markers=m)
-        n_target = N
+        sw = synth.swarm(N, F, T, seed=seed + rank * F, max_markers=m,
+                         **({} if n_map is None else {"n_map": n_map}))
+        n_target = N if n_map is None else n_map
     odo = pyekf.odometry(sw.scenario(0))  # encoders report the commanded drive: every filter's
     return sw, np.repeat(odo[:, None], F, 1), n_target
 
@@ -373,6 +388,8 @@ def run(args, rank, world, local, backend=None):
     messages between barriers, the slowest rank's time (MAX), corrections of all ranks (SUM), one
     all_gather of the final poses (the path's only collective)."""
     N, dt, F, m, cfgname = WORKLOADS[args.workload]
+    assoc = is_assoc(args.workload)
+    n_map = N - ASSOC_FREE_SLOTS if assoc else None
     traffic, traffic_err = None, "not measured (--traffic off or N>1)"
     resident = dt == "f64" and 3 + 2 * N <= 128 and os.environ.get("EKF_RESIDENT") != "0"
     if resident:
@@ -386,14 +403,15 @@ def run(args, rank, world, local, backend=None):
     dtype = be.F32 if dt == "f32" else be.F64
     W, K = args.warmup, args.steps
     t_gen = time.perf_counter()
-    sw, odom, n_init_target = build_inputs(N, F, W + 2 * K, args.seed, m, rank)
+    sw, odom, n_init_target = build_inputs(N, F, W + 2 * K, args.seed, m, rank, n_map)
     n_warm, counts, ids, act, rel = sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel
     t_gen = time.perf_counter() - t_gen
     inputs = args.inputs
     if inputs == "auto":
         inputs = "device" if (F > 1 and dt == "f64" and backend is None) else "host"
-    if inputs == "device" and dt != "f64":
-        raise SystemExit("--inputs device: fp64 workloads (fp32 takes its survey on an fp64 handle)")
+    if inputs == "device" and (dt != "f64" or assoc):
+        raise SystemExit("--inputs device: fp64 known-id workloads (fp32 takes its survey on an "
+                         "fp64 handle; the device planner writes known-id chunks)")
     ekf = be.EKF(n_landmarks=N, n_filters=F, dtype=dtype, device=local)
     sim = None
     if inputs == "device":
@@ -404,24 +422,29 @@ def run(args, rank, world, local, backend=None):
                         start_theta=sw.start_pose[0], start_x=sw.start_pose[1],
                         start_y=sw.start_pose[2])
 
-    def msgs(a, b, e=None):
+    def msgs(a, b, e=None, known=False):
         if sim is not None and e is None:  # the GPU simulates, senses and plans these messages
             sim.run(sw.cmd[a * tpm:b * tpm], sw.sense[a:b])
             return
         sl = slice(a, b)
-        (e or ekf).replay(counts[sl], rel[sl], odom[sl], ids=ids[sl], actions=act[sl])
+        un = assoc and not known  # the survey sights with known ids; the drive's ids are stripped
+        (e or ekf).replay(counts[sl], rel[sl], odom[sl], ids=None if un else ids[sl],
+                          actions=act[sl], assoc=un)
 
     # ---- untimed warm-up: the survey (every landmark initialised), then W messages ----
     # fp32 cannot take first sightings against the 1e7 prior (slam.cpp:130): the survey runs on an
     # fp64 handle whose state seeds the fp32 one
+    # (association: the survey sights with known ids on an fp64 handle, then counter_obstacles =
+    # the mapped landmarks, numbered 0..n_map−1 as slam.cpp:351-356 would have numbered them)
     warm_state = None
-    if dtype == be.F32 and n_warm:
+    if (dtype == be.F32 or assoc) and n_warm:
         e64 = be.EKF(n_landmarks=N, n_filters=F, device=local)
-        msgs(0, n_warm, e64)
+        msgs(0, n_warm, e64, known=True)
         warm_state = []
         for f in range(F):
             x, S, cnt = e64.state(f)
             tmo = e64.map_odom(f)
+            cnt = n_map if assoc else cnt
             ekf.set_state(x, S, tmo=tmo, counter=cnt, f=f)
             warm_state.append((x, S, tmo, cnt))
         e64.close()
@@ -477,6 +500,7 @@ def run(args, rank, world, local, backend=None):
     n_gain, ms_gain = ekf.profile_read(1)
     n_fac, ms_fac = ekf.profile_read(3)
     n_res, ms_res = ekf.profile_read(4)
+    n_asc, ms_asc = ekf.profile_read(2)
     ekf.profile(False)
     live = np.arange(act.shape[2]) < counts[ps][..., None]
     res_corr = int(np.count_nonzero(live & (act[ps] != 2)))
@@ -515,7 +539,8 @@ def run(args, rank, world, local, backend=None):
             "config": {"workload": args.workload, "baseline_config": cfgname,
                        "n_landmarks": N, "state_dim": n, "filters_per_gpu": F,
                        "filters_total": F * world, "markers_per_message": m,
-                       "association": "known", "seeds": f"{args.seed} + global filter index",
+                       "association": "unknown (sensor_cb)" if assoc else "known",
+                       "seeds": f"{args.seed} + global filter index",
                        "survey_messages": n_warm,
                        "landmarks_initialised_min": n_init,
                        "landmarks_initialised_target": n_init_target,
@@ -539,8 +564,21 @@ def run(args, rank, world, local, backend=None):
                          "pmc": traffic.get("mfma_busy") if traffic else traffic_err},
                 "chain_kernel_avg_us": ms_gain / max(n_gain, 1) * 1e3,
                 "factor_kernel_avg_us": ms_fac / max(n_fac, 1) * 1e3,
+                # the whole step against the rank-2m ceiling: one Σ pass per
+                # message is the algorithmic minimum, 2·n²·w·F bytes per step
+                "end_to_end": {
+                    "bytes_per_step": bytes_per_launch,
+                    "achieved": bytes_per_launch / (elapsed / K) / 1e9,
+                    "frac": bytes_per_launch / (elapsed / K) / 1e9 / HBM_PEAK_GBS,
+                    "ceiling_corrections_per_s": (HBM_PEAK_GBS * 1e9 / bytes_per_launch * (
+                        total_corr / world / K)) if bytes_per_launch else None,
+                },
             },
         }
+        result["roofline"]["end_to_end_frac"] = result["roofline"]["end_to_end"]["frac"]
+        if n_asc:
+            result["roofline"]["assoc_kernel_avg_us"] = ms_asc / n_asc * 1e3
+            result["roofline"]["assoc_launches"] = n_asc
         if world > 1:
             result["gathered_poses"] = {"filters": int(all_poses.shape[0]),
                                         "all_finite": bool(np.all(np.isfinite(all_poses)))}
@@ -605,8 +643,9 @@ def ekf_first_poses(args, be, N, dtype, ws, counts, ids, act, rel, odom, t0s, de
     e = be.EKF(n_landmarks=N, dtype=dtype, device=device)
     e.set_state(x, S, tmo=tmo, counter=cnt)
     sl = slice(t0s, t0s + k)
-    p = e.replay(counts[sl, :1], rel[sl, :1], odom[sl, :1], ids=ids[sl, :1], actions=act[sl, :1],
-                 poses=True)[:, 0]
+    un = is_assoc(args.workload)
+    p = e.replay(counts[sl, :1], rel[sl, :1], odom[sl, :1], ids=None if un else ids[sl, :1],
+                 actions=act[sl, :1], poses=True, assoc=un)[:, 0]
     e.close()
     return p
 
@@ -657,9 +696,14 @@ def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
     d.state, d.sigma, d.counter = x.copy(), S.copy(), int(cnt)
     d.t_map_odom, d.prev = tuple(tmo), tuple(x[:3])
 
+    un = is_assoc(args.workload)
+
     def np_step(t, c):
         d.t_odom_robot = tuple(odom[t, 0])
-        d.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
+        if un:
+            d.sensor_cb(rel[t, 0, :c])
+        else:
+            d.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
     nb, kb, tb = timed(np_step, 1, 10.0)
     out = {}
     for literal, k_min, budget in ((True, 1, 10.0), (False, args.steps, 0.0)):
@@ -668,13 +712,17 @@ def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
 
         def c_step(t, c, ref=ref):
             ref.set_odom(odom[t, 0])
-            ref.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
+            if un:
+                ref.sensor_cb(rel[t, 0, :c])
+            else:
+                ref.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
         out[literal] = timed(c_step, k_min, budget)
     lc, lk, lt = out[True]
     sc_, sk, st = out[False]
     return {"value": nb / tb, "unit": "corrections/s", "cores": _blas_threads() or cores,
             "kind": "port",
-            "sample": f"literal dense restatement of slam.cpp (numpy + OpenBLAS dgemm, fp64, "
+            "sample": f"literal dense restatement of slam.cpp{' sensor_cb' if un else ''} "
+                      f"(numpy + OpenBLAS dgemm, fp64, "
                       f"oracle/ekf_numpy.py): {kb} message(s) = {nb} corrections in {tb:.2f} s",
             "c_literal": {"value": lc / lt, "cores": cores,
                           "sample": f"C oracle, dense O(n^3) with a blocked OpenMP GEMM: {lk} "
@@ -694,7 +742,10 @@ def parity(args, N, gpu_poses, ws, counts, ids, act, rel, odom, t0s):
     for i, t in enumerate(range(t0s, t0s + k)):
         ref.set_odom(odom[t, 0])
         c = int(counts[t, 0])
-        ref.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
+        if is_assoc(args.workload):
+            ref.sensor_cb(rel[t, 0, :c])
+        else:
+            ref.fake_sensor_cb(ids[t, 0, :c], act[t, 0, :c], rel[t, 0, :c])
         ref_p[i] = ref.get(sigma=False)[0][:3]
     d = gpu_poses - ref_p
     dth = np.arctan2(np.sin(d[:, 0]), np.cos(d[:, 0]))

@@ -102,6 +102,7 @@ struct orc_ekf {
   double* H;      /* 2×n dense (literal mode) */
   double* PH0;    /* n×2 : Σ·Hᵀ kept for the Joseph form (PHt is overwritten by K) */
   unsigned counter;      /* counter_obstacles, slam.cpp:670 */
+  double last_dmin;      /* the last association's smallest existing d_k (test diagnostics) */
   double tmo[3];         /* t_map_odom, slam.cpp:659 */
   double prev[3];        /* filter_previous_configuration, slam.cpp:660 */
   double todom[3];       /* t_odom_robot, slam.cpp:650 */
@@ -428,10 +429,13 @@ int orc_ekf_associate_correct(orc_ekf* f, double rel_x, double rel_y, int* jout,
   int best = -1;
   double bestd = INFINITY;
   double dnew = f->gate;                                   /* :406-408 */
+  double dm = INFINITY; /* the smallest existing d_k (test diagnostics, orc_ekf_last_dmin) */
   for (unsigned k = 0; k < f->counter; ++k) {
     const double d = (k == f->counter - 1) ? dnew : mahalanobis(f, (int)k, zr, zb);
     if (d < bestd) { bestd = d; best = (int)k; }
+    if (k + 1 < f->counter && d < dm) dm = d;
   }
+  f->last_dmin = dm;
   int jsel = best;
   int nw = 0;
   if (best == (int)f->counter - 1 && bestd >= f->gate) {  /* :421 new landmark */
@@ -507,6 +511,8 @@ void orc_ekf_get(const orc_ekf* f, double* state, double* sigma, double* tmo, un
 }
 
 void orc_ekf_get_prev(const orc_ekf* f, double* prev) { memcpy(prev, f->prev, sizeof(double) * 3); }
+
+double orc_ekf_last_dmin(const orc_ekf* f) { return f->last_dmin; }
 
 void orc_ekf_set(orc_ekf* f, const double* state, const double* sigma, const double* tmo,
                  const double* prev, unsigned counter) {

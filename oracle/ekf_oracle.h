@@ -55,6 +55,9 @@ void orc_ekf_get(const orc_ekf* f, double* state, double* sigma, double* tmo, un
 void orc_ekf_set(orc_ekf* f, const double* state, const double* sigma, const double* tmo,
                  const double* prev, unsigned counter);
 void orc_ekf_get_prev(const orc_ekf* f, double* prev);
+/* test diagnostics: the smallest existing Mahalanobis distance of the last association (INFINITY
+ * when there was no existing landmark), to build decisions near the gate */
+double orc_ekf_last_dmin(const orc_ekf* f);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,8 @@ def lib():
                                   C.c_uint]
         L.orc_ekf_get_prev.argtypes = [C.c_void_p, _dp]
         L.orc_ekf_set_joseph.argtypes = [C.c_void_p, C.c_int]
+        L.orc_ekf_last_dmin.restype = C.c_double
+        L.orc_ekf_last_dmin.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -133,6 +135,28 @@ class OracleEKF:
         nw = np.zeros(max(m, 1), dtype=np.int32)
         rc = lib().orc_ekf_sensor_cb(self.h, m, rel, j, nw)
         return rc, j[:m], nw[:m]
+
+    def sensor_cb_dmin(self, rel_xy):
+        """sensor_cb (slam.cpp:318-530) marker by marker, as orc_ekf_sensor_cb runs it, also
+        returning each marker's smallest existing Mahalanobis distance (tests near the gate)."""
+        rel = np.ascontiguousarray(rel_xy, dtype=np.float64).reshape(-1, 2)
+        m = rel.shape[0]
+        j = np.zeros(m, dtype=np.int32)
+        nw = np.zeros(m, dtype=np.int32)
+        dmin = np.zeros(m)
+        rc = -3 if m == 0 else 0
+        if m:
+            lib().orc_ekf_predict(self.h)
+            for i in range(m):
+                jj, nn = C.c_int(-1), C.c_int(0)
+                e = lib().orc_ekf_associate_correct(self.h, float(rel[i, 0]), float(rel[i, 1]),
+                                                    C.byref(jj), C.byref(nn))
+                j[i], nw[i] = jj.value, nn.value
+                dmin[i] = lib().orc_ekf_last_dmin(self.h)
+                if e and not rc:
+                    rc = e
+            lib().orc_ekf_posterior(self.h)
+        return rc, j, nw, dmin
 
     def get(self, sigma=True):
         x = np.zeros(self.n)

@@ -392,3 +392,125 @@ def test_association_at_scale_batched_replay(known_map):
     assert cg == cr
     assert np.abs(xg - xr).max() < POSE_TOL
     assert np.abs(Sg - Sr).max() < SIGMA_TOL
+
+
+def _open_map_scenario():
+    """512 slots, 320 landmarks. Half of the landmarks the circle messages will see are relabelled
+    to the top slots and forgotten after the known-id survey, so unknown association meets both
+    mapped landmarks and unmapped ones (new-landmark commits at counter ≥ 256, slam.cpp:421-422)."""
+    sc = synth.populated(512, 12, n_map=320, shuffle=True)
+    w = sc.n_warm
+    live = np.arange(sc.ids.shape[1])[None, :] < sc.count[w:, None]
+    seen = np.unique(sc.ids[w:][live])
+    unmapped = seen[::2]
+    mapped = np.setdiff1d(np.arange(320), unmapped)
+    perm = np.empty(512, np.int32)
+    perm[mapped] = np.arange(mapped.size)
+    perm[unmapped] = mapped.size + np.arange(unmapped.size)
+    perm[320:] = np.arange(320, 512)
+    ids = np.where(sc.ids >= 0, perm[np.maximum(sc.ids, 0)], -1).astype(np.int32)
+    sc = synth.Scenario(sc.n_landmarks, sc.landmarks, sc.wheel, ids, sc.actions, sc.rel,
+                        sc.count, sc.truth, sc.track, sc.radius, sc.n_warm)
+    return sc, int(mapped.size)
+
+
+@pytest.fixture(scope="module")
+def open_map():
+    """The survey on the GPU (fp64), then the unmapped slots reset to the prior (slam.cpp:127-132):
+    state (0, 0), no cross covariance, 1e7 on the diagonal; counter = the mapped count (≥ 256)."""
+    sc, counter = _open_map_scenario()
+    assert counter >= 256
+    odom = pyekf.odometry(sc)
+    e = pyekf.EKF(n_landmarks=512)
+    _replay(e, slice(0, sc.n_warm), sc, odom)
+    x, S, _ = e.state()
+    tmo = e.map_odom()
+    e.close()
+    k = 3 + 2 * counter
+    x[k:] = 0.0
+    S[k:, :] = 0.0
+    S[:, k:] = 0.0
+    S[np.arange(k, S.shape[0]), np.arange(k, S.shape[0])] = 10e6
+    return sc, odom, (x, S, tmo, counter)
+
+
+def _assoc_oracle_run(sc, odom, ws, gate=2.0):
+    x, S, tmo, cnt = ws
+    ref = orc.OracleEKF(n_landmarks=512, mah_gate=gate)
+    ref.set(x, S, tmo, x[:3], cnt)
+    out = []
+    for t in range(sc.n_warm, sc.n_messages):
+        ref.set_odom(odom[t])
+        out.append(ref.sensor_cb_dmin(sc.rel[t, :int(sc.count[t])]) + (ref.get(sigma=False)[0][:3],))
+    return ref, out
+
+
+def _assoc_gpu_against(sc, odom, ws, ref_out, dtype=pyekf.EKF_F64, gate=2.0):
+    x, S, tmo, cnt = ws
+    e = pyekf.EKF(n_landmarks=512, dtype=dtype, mah_gate=gate)
+    e.set_state(x, S, tmo=tmo, counter=cnt)
+    perr = 0.0
+    n_new = n_old = 0
+    for i, t in enumerate(range(sc.n_warm, sc.n_messages)):
+        e.set_odom(odom[t])
+        rc, j, nw = e.sensor(sc.rel[t, :int(sc.count[t])])
+        rr, jr, nr, _, pr = ref_out[i]
+        assert rc == rr == 0
+        assert np.array_equal(j, jr) and np.array_equal(nw, nr), (t, j, jr, nw, nr)
+        n_new += int(nr.sum())
+        n_old += int(nr.size - nr.sum())
+        perr = max(perr, float(np.abs(e.pose() - pr).max()))
+    xg, Sg, cg = e.state()
+    assert e.status() == 0
+    e.close()
+    return perr, xg, Sg, cg, n_new, n_old
+
+
+@pytest.mark.parametrize("dtype", [pyekf.EKF_F64, pyekf.EKF_F32], ids=["f64", "f32"])
+def test_association_open_map_new_and_known(open_map, dtype):
+    """sensor_cb against ≥ 256 mapped landmarks with unmapped ones in view: both branches of
+    slam.cpp:421-440 (commit at counter ≥ 256, roll back) with every decision equal to the
+    oracle's; poses 1e-8 (fp64) / 1e-6 (fp32 Σ)."""
+    sc, odom, ws = open_map
+    ref, out = _assoc_oracle_run(sc, odom, ws)
+    perr, xg, Sg, cg, n_new, n_old = _assoc_gpu_against(sc, odom, ws, out, dtype)
+    xr, Sr, _, cr = ref.get()
+    key = "assoc_open_" + ("f64" if dtype == pyekf.EKF_F64 else "f32")
+    ERRORS[key] = {"new": n_new, "associated": n_old, "counter": int(cg), "pose": perr,
+                   "state": float(np.abs(xg - xr).max()), "sigma": float(np.abs(Sg - Sr).max())}
+    assert n_new > 0 and n_old > 0
+    assert cg == cr and cr > ws[3] >= 256
+    if dtype == pyekf.EKF_F64:
+        assert perr < POSE_TOL
+        assert np.abs(xg - xr).max() < STATE_TOL
+        assert np.abs(Sg - Sr).max() < SIGMA_TOL
+    else:
+        assert perr < F32_POSE_TOL
+        assert np.abs(xg - xr).max() < F32_STATE_TOL
+        assert np.abs(Sg - Sr).max() < F32_SIGMA_TOL
+
+
+def test_association_near_the_gate(open_map):
+    """A gate placed 3e-4 below the first known-landmark distance in (0.5, 2): that marker's
+    smallest d sits just above the gate (slam.cpp:401-408; the new slot, index counter, wins only
+    over a strictly larger existing minimum), every earlier decision unchanged. Every decision,
+    the near-gate one included, equals the oracle's."""
+    sc, odom, ws = open_map
+    _, out = _assoc_oracle_run(sc, odom, ws)
+    d = np.concatenate([o[3] for o in out])
+    i0 = int(np.argmax((d > 0.5) & (d < 2.0)))
+    assert 0.5 < d[i0] < 2.0
+    gate = float(d[i0]) - 3e-4
+    ref, out = _assoc_oracle_run(sc, odom, ws, gate)
+    d2 = np.concatenate([o[3] for o in out])
+    near = np.flatnonzero(np.abs(d2 - gate) < 1e-3)
+    assert near.size > 0 and i0 in near
+    perr, xg, Sg, cg, n_new, n_old = _assoc_gpu_against(sc, odom, ws, out, gate=gate)
+    xr, Sr, _, cr = ref.get()
+    ERRORS["assoc_near_gate"] = {"gate": gate, "near": near.tolist(), "new": n_new,
+                                 "associated": n_old, "pose": perr,
+                                 "state": float(np.abs(xg - xr).max())}
+    assert cg == cr
+    assert perr < POSE_TOL
+    assert np.abs(xg - xr).max() < STATE_TOL
+    assert np.abs(Sg - Sr).max() < SIGMA_TOL

@@ -32,14 +32,17 @@ class OracleSwarm:
         self.N, self.F = n_landmarks, n_filters
         self.f = [orc.OracleEKF(n_landmarks=n_landmarks) for _ in range(n_filters)]
 
-    def replay(self, counts, rel, odom, ids=None, actions=None, poses=False):
+    def replay(self, counts, rel, odom, ids=None, actions=None, poses=False, assoc=False):
         T = counts.shape[0]
         out = np.zeros((T, self.F, 3))
         for t in range(T):
             for f, e in enumerate(self.f):
                 c = int(counts[t, f])
                 e.set_odom(odom[t, f])
-                e.fake_sensor_cb(ids[t, f, :c], actions[t, f, :c], rel[t, f, :c])
+                if assoc:
+                    e.sensor_cb(rel[t, f, :c])
+                else:
+                    e.fake_sensor_cb(ids[t, f, :c], actions[t, f, :c], rel[t, f, :c])
                 out[t, f] = e.get(sigma=False)[0][:3]
         return out if poses else None
 
@@ -94,7 +97,11 @@ def _worker(rank, world, port, q):
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     args = bench.parse(["--workload", "tiny", "--gpus", str(world), "--steps", "3",
                         "--warmup", "2", "--traffic", "off", "--parity-messages", "2"])
-    result, poses = bench.run(args, rank, world, 0, CpuBackend())
+    try:
+        result, poses = bench.run(args, rank, world, 0, CpuBackend())
+    except BaseException as e:  # report at once instead of leaving the parent to time out
+        q.put((rank, repr(e), None))
+        raise
     q.put((rank, result, poses))
 
 
@@ -107,6 +114,8 @@ def test_bench_run_gloo_world2():
     for p in procs:
         p.start()
     out = {r: (res, poses) for r, res, poses in (q.get(timeout=300) for _ in procs)}
+    for r, (res, _) in out.items():
+        assert not isinstance(res, str), f"rank {r}: {res}"
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
