@@ -30,7 +30,8 @@ struct Marker {
 };
 
 struct Launch {
-  int kind;    // 0 = gain + Σ pass, 1 = association + gain + Σ pass, 2 = posterior only
+  int kind;    // 0 = gain + Σ pass, 1 = association + gain + Σ pass (one marker), 2 = posterior
+               // only, 3 = a chunk of associated markers (k_assoc_msg) + Σ pass
   size_t off;  // first descriptor
   int f0, nf, kw;
 };
@@ -61,6 +62,10 @@ struct ekf_ctx {
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
   bool defer = false;            // ekf_defer: plan now, upload and launch later
   bool joseph = false;           // ekf_set_joseph (resident: its own kernel; pipeline: kJoseph chunks)
+  bool assoc_msg = true;         // unknown association by chunks (k_assoc_msg); EKF_ASSOC_MSG=0:
+                                 // one association kernel + launch pair per marker
+  bool main_dirty = false;       // work on the main stream since the bulk stream last joined it
+  AmArgs am{};                   // k_assoc_msg scratch (allocated at the first association chunk)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
   hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
   bool devsync = false;                   // streams synchronise through device epochs
@@ -464,6 +469,115 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
   }
 }
 
+// k_assoc_msg's tables and granules for every filter (once; zeroed so no stale tag matches)
+int ensure_am(ekf_ctx* h) {
+  if (h->am.hist) return EKF_OK;
+  const int G = (h->cfg.n_landmarks + kAmSlots - 1) / kAmSlots;
+  const size_t Np = static_cast<size_t>(G) * kAmSlots, F = static_cast<size_t>(h->F);
+  AmArgs b{};
+  b.G = G;
+  b.hist_stride = kMaxChunk * Np;
+  b.cur_stride = (kMaxChunk + 1) * Np;
+  b.gran_stride = static_cast<size_t>(kMaxChunk + 1) * G * 4;
+  if (hipMalloc(&b.hist, sizeof(AmHist) * b.hist_stride * F) != hipSuccess ||
+      hipMalloc(&b.cur, sizeof(AmCur) * b.cur_stride * F) != hipSuccess ||
+      hipMalloc(&b.gran, sizeof(unsigned long long) * b.gran_stride * F) != hipSuccess) {
+    if (b.hist) hipFree(b.hist);
+    if (b.cur) hipFree(b.cur);
+    return EKF_E_NOMEM;
+  }
+  if (hipMemset(b.gran, 0, sizeof(unsigned long long) * b.gran_stride * F) != hipSuccess)
+    return EKF_E_HIP;
+  h->am = b;
+  return EKF_OK;
+}
+
+// Unknown association by chunks (k_assoc_msg): markers [i0, i1) of each filter's message in chunks
+// of ≤ kMaxChunk, each chunk one association launch + one Σ pass. Decisions land in
+// FilterCtl::assoc_j/new at slot i % kMaxAssoc, as plan_assoc's.
+void plan_assoc_msg(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0, int i1,
+                    const char* absent = nullptr) {
+  int chunks = 1;
+  for (int k = 0; k < nf; ++k) {
+    const int mf = std::min(static_cast<int>(h->msgs[k].size()), i1);
+    chunks = std::max(chunks, (mf - i0 + kMaxChunk - 1) / kMaxChunk);
+  }
+  for (int chunk = 0; chunk < chunks; ++chunk) {
+    const size_t off = h->plan_d.size();
+    h->plan_d.resize(off + nf);
+    for (int k = 0; k < nf; ++k) {
+      const int f = f0 + k;
+      const auto& mk = h->msgs[k];
+      const int mf = std::min(static_cast<int>(mk.size()), i1);
+      const int nch = std::max(1, (mf - i0 + kMaxChunk - 1) / kMaxChunk);
+      MsgDesc* d = &h->plan_d[off + k];
+      if (chunk >= nch || (absent && absent[k]) || (mf <= i0 && i0 > 0)) {
+        std::memset(d, 0, sizeof(MsgDesc));
+        continue;
+      }
+      const int b = i0 + chunk * kMaxChunk;
+      const int m = std::max(0, std::min(kMaxChunk, mf - b));
+      int flags = kActive | kNoInit;
+      h->prev_m[f] = -1;  // association chunks run unpipelined
+      forget_desc(h, f);
+      if (b == 0 && (predict || h->pending[f])) flags |= kFirst;
+      if (chunk == nch - 1 && posterior) flags |= kLast;
+      fill_desc(d, m, flags, h->parity[f], h->odom[f]);
+      d->assoc_slot = b % kMaxAssoc;
+      for (int i = 0; i < m; ++i) {
+        d->ids[i] = -1;
+        d->z[i][0] = mk[b + i].zr;
+        d->z[i][1] = mk[b + i].zb;
+      }
+      h->parity[f] ^= 1;
+      if (b == 0) h->pending[f] = 0;
+    }
+    h->plan_l.push_back(Launch{3, off, f0, nf, 4});
+  }
+}
+
+// Route unknown association: whole chunks through k_assoc_msg on the HBM pipeline (simple form);
+// the resident path, the Joseph form and EKF_ASSOC_MSG=0 take one marker per launch.
+void plan_unknown(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0, int i1,
+                  const char* absent = nullptr) {
+  if (!h->resident && !h->joseph && h->assoc_msg)
+    plan_assoc_msg(h, f0, nf, predict, posterior, i0, i1, absent);
+  else
+    plan_assoc(h, f0, nf, predict, posterior, i0, i1, absent);
+}
+
+// One association chunk per filter of [f0, f0+nf) (descriptors dptr), then its Σ pass, both on the
+// bulk stream (the pass's CUs; the main stream's chains are not involved). The bulk stream joins
+// the main stream first if the latter ran anything since (a chain wrote t_map_odom there).
+int assoc_msg_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
+  if (int rc = ensure_am(h)) return rc;
+  hipStream_t bs = h->serial ? h->stream : h->bulk;
+  if (!h->serial && h->main_dirty) {
+    HIPCHK(hipEventRecord(h->ev_chain, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
+    h->main_dirty = false;
+  }
+  const unsigned seq = static_cast<unsigned>(h->seq);
+  auto run = [&](auto tag) -> int {
+    using T = decltype(tag);
+    PassArgs<T> a = args<T>(h, dptr, f0);
+    a.seq = seq;
+    a.polls = h->devsync && !h->serial ? 1 : 0;
+    int rc = timed(h, 2, bs, [&](hipEvent_t e0, hipEvent_t e1) {
+      return launch_assoc_msg<T>(a, h->am, nf, bs, e0, e1);
+    });
+    if (rc) return rc;
+    return timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
+      return launch_sigma_pass<T>(a, nf, true, false, bs, e0, e1);
+    });
+  };
+  const int rc = h->cfg.dtype == EKF_F32 ? run(float{}) : run(double{});
+  if (rc) return rc;
+  if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[seq & 1], bs));
+  h->seq += 1;
+  return EKF_OK;
+}
+
 void plan_posterior(ekf_ctx* h, int f) {
   h->prev_m[f] = -1;
   forget_desc(h, f);
@@ -571,6 +685,7 @@ int flush(ekf_ctx* h) {
   // the bulk stream reads these descriptors too: one main → bulk hop per upload
   HIPCHK(hipEventRecord(h->ev_chain, h->stream));
   HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
+  h->main_dirty = false;
   HIPCHK(hipEventRecord(sl.ev, h->stream));
   sl.used = true;
   int rc = EKF_OK;
@@ -591,7 +706,13 @@ int flush(ekf_ctx* h) {
       }
       rc = group(h, dp, h->plan_d.data() + L.off, L.f0, L.nf, static_cast<int>(lj - li), true,
                  nolook);
+      h->main_dirty = true;
       li = lj;
+      continue;
+    }
+    if (L.kind == 3) {
+      rc = assoc_msg_group(h, dp, L.f0, L.nf);
+      ++li;
       continue;
     }
     if (L.kind == 1) {
@@ -602,10 +723,12 @@ int flush(ekf_ctx* h) {
       // has 4 CUs per XCD: a pass there took 33 µs against 9 at N = 1024 fp32); the next
       // association joins the bulk stream first
       if (!rc) rc = group(h, dp, h->plan_d.data() + L.off, L.f0, L.nf, 1, true);
+      h->main_dirty = true;
     }
     if (!rc && L.kind == 2) {
       if (join_bulk(h)) return EKF_E_HIP;
       rc = posterior_launch(h, dp, L.f0, L.nf);
+      h->main_dirty = true;
     }
     ++li;
   }
@@ -636,7 +759,7 @@ int assoc_sync(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int m_m
   for (int k = 0; k < nf; ++k) mm = std::max(mm, static_cast<int>(h->msgs[k].size()));
   for (int i0 = 0; i0 < mm; i0 += kMaxAssoc) {
     const int i1 = std::min(mm, i0 + kMaxAssoc);
-    plan_assoc(h, f0, nf, predict, posterior && i1 == mm, i0, i1);
+    plan_unknown(h, f0, nf, predict, posterior && i1 == mm, i0, i1);
     int rc = flush(h);
     if (rc) return rc;
     if (drain(h)) return EKF_E_HIP;
@@ -734,6 +857,7 @@ int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
         for (int t = 0; t < T && !rc; ++t)
           rc = group(h, dd + t * F, nullptr, 0, h->F, 1, true, t == 0);
       }
+      h->main_dirty = true;
     }
   }
   for (int f = 0; f < h->F; ++f) {
@@ -812,6 +936,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
   if (const char* e = std::getenv("EKF_SERIAL")) h->serial = std::atoi(e) != 0;
   if (const char* e = std::getenv("EKF_NB")) h->nb = std::atoi(e) != 0;
+  if (const char* e = std::getenv("EKF_ASSOC_MSG")) h->assoc_msg = std::atoi(e) != 0;
   {  // EKF_RESIDENT=0: the HBM pipeline at every size (tests compare the two)
     const char* e = std::getenv("EKF_RESIDENT");
     h->resident = cfg.dtype == EKF_F64 && h->n <= kResidentMaxN && !(e && std::atoi(e) == 0);
@@ -897,6 +1022,9 @@ int ekf_destroy(ekf_t h) {
   if (h->rows) hipFree(h->rows);
   if (h->stage) hipFree(h->stage);
   if (h->ddesc) hipFree(h->ddesc);
+  if (h->am.hist) hipFree(h->am.hist);
+  if (h->am.cur) hipFree(h->am.cur);
+  if (h->am.gran) hipFree(h->am.gran);
   for (int i = 0; i < kRing; ++i) {
     if (h->ring[i].p) hipHostFree(h->ring[i].p);
     if (h->ring[i].ev) hipEventDestroy(h->ring[i].ev);
@@ -969,7 +1097,7 @@ int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int*
   }
   hipSetDevice(h->cfg.device);
   if (!assoc_out && !is_new_out) {
-    plan_assoc(h, f, 1, true, true, 0, m);
+    plan_unknown(h, f, 1, true, true, 0, m);
     return submit(h);
   }
   const int rc = assoc_sync(h, f, 1, true, true, m, assoc_out, is_new_out);
@@ -993,7 +1121,7 @@ int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, cons
   if (assoc_mode) {
     int mm = 1;
     for (int f = 0; f < h->F; ++f) mm = std::max(mm, static_cast<int>(h->msgs[f].size()));
-    plan_assoc(h, 0, h->F, true, true, 0, mm, h->absent.data());
+    plan_unknown(h, 0, h->F, true, true, 0, mm, h->absent.data());
   } else {
     plan_known(h, 0, h->F, true, h->absent.data());
   }
@@ -1018,7 +1146,7 @@ int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, con
     if (assoc_mode) {
       int mm = 1;
       for (size_t f = 0; f < F; ++f) mm = std::max(mm, static_cast<int>(h->msgs[f].size()));
-      plan_assoc(h, 0, h->F, true, true, 0, mm, h->absent.data());
+      plan_unknown(h, 0, h->F, true, true, 0, mm, h->absent.data());
     } else {
       plan_known(h, 0, h->F, true, h->absent.data());
     }

@@ -1,0 +1,779 @@
+// Unknown association (Slam::sensor_cb, nuslam/src/slam.cpp:318-530) for a whole chunk of markers
+// in ONE launch, followed by a single Σ pass — instead of an association kernel, a chain, a factor
+// kernel and a Σ pass per marker.
+//
+// Why it works. A chunk's corrections are Σ_{c+1} = Σ_c − K_c·M_c (slam.cpp:264-265, rank 2 each)
+// on the predicted Σ_p (slam.cpp:321-335). Marker c's association (slam.cpp:358-440) reads, for every
+// known landmark k, only the 5 × 5 block of Σ_c over {θ, x, y, kx, ky} and x_c at those indices. Those
+// 16 entries per landmark evolve by the same rank-2 terms, so each landmark can carry its own block:
+//   Σ_{c+1}[k, k] = Σ_c[k, k] − K_c[k]·M_c[:, k],  Σ_{c+1}[k, p] = Σ_c[k, p] − K_c[k]·M_c[:, p], …
+// with K_c[k] = Σ_c[k, pA]·Hᵀ·S⁻¹ and M_c[:, k] = H·Σ_c[pA, k] over pA = {θ, x, y, jx, jy}. The only
+// entries of Σ_c outside the blocks that a step needs are the crosses with its landmark j:
+//   Σ_c[k, j] = Σ_p[k, j] − Σ_{c'<c} K_{c'}[k]·M_{c'}[:, j],   Σ_c[j, k] likewise,
+// i.e. Σ_in (no predict term between landmarks) and the factor histories of k and of j. So:
+//   * one lane per landmark slot, 64 slots per workgroup (one wave), G = ⌈N / 64⌉ workgroups per
+//     filter; a lane keeps its slot's block and state in registers and its K / M history in LDS;
+//   * per marker: every lane scores its landmark (k_assoc's expression, ekf_math.hpp assoc_dist),
+//     a wave argmin (first index on ties, arma::index_min), then the G workgroups exchange their
+//     (d, k) as tagged 8-byte granules (cdna_hip_programming.md Guideline 16, R2) and every one
+//     takes the same decision: commit a new landmark (slam.cpp:421-422) or the argmin;
+//   * the chosen landmark's block, state and history are read from write-through tables (every
+//     lane publishes its slot's K, M and next block each step, drained before the granule), its
+//     crosses with each lane's landmark are gathered from Σ_in; every workgroup then forms the same
+//     S, S⁻¹, ν, K[pose], M[pose] and each lane its own K[k], M[k] — the chunk's Kcat / Mcat rows
+//     for the Σ pass — and applies the step to its block and state.
+// The Σ pass (k_sigma_pass, ekf_kernels.hip) then applies Σ_out = Σ_in + Q̄ − Kcatᵀ·Mcat once.
+// fp32 Σ: a chunk that commits a new landmark also writes the final Σ[U, U] in fp64 (ChunkRec::Pend,
+// the first sighting's 1e7 − (1e7 − δ), slam.cpp:130) for k_patch_stage, after a last exchange.
+//
+// In exact arithmetic this equals the reference's sequential dense algebra; the decisions are the
+// reference's (tests/test_gpu_scale.py: every decision equal to the oracle's, new and known
+// landmarks, a marker 3e-4 from the gate).
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "ekf_device.hpp"
+#include "ekf_launch.hpp"
+#include "ekf_math.hpp"
+#include "geom.hpp"
+
+namespace ekfslam {
+
+#include "ekf_sync.hpp"
+
+namespace {
+
+constexpr unsigned kAmSpin = 1u << 22;  // bounded granule polls (EKF_FLAG_TIMEOUT)
+
+struct AmShared {
+  double hk[kMaxChunk][4][kAmSlots];  // this wave's K_c[k], by lane
+  double hm[kMaxChunk][4][kAmSlots];  // this wave's M_c[:, k], by lane
+  double jh[kMaxChunk][8];            // the step's landmark: K (0..3) and M (4..7) of every step
+  double jc[18];                      // its block and state (AmCur, x included)
+  double pb[kMaxChunk][18];           // fp32 patch: every marker's landmark's final block
+  double pp[9];                       // fp32 patch: the final pose block
+  int jl[kMaxChunk];                  // the chunk's landmark per marker (−1: skipped)
+};
+
+// The lane's predicted block of slot entries: Σ_p[k][b] = Σ[k][b] + Σ[k][0]·α_b,
+// Σ_p[a][k] = Σ[a][k] + α_a·Σ[0][k] (k_assoc's expressions; At has α only in rows 1, 2).
+template <typename T>
+__device__ __forceinline__ void slot_block(const T* S, int ld, int ix, double a1, double a2,
+                                           double (&kk)[4], double (&kp)[6], double (&pk)[6],
+                                           double (&c0)[2], double (&r0)[2]) {
+  const T* q0 = S + static_cast<size_t>(ix) * ld;
+  const T* q1 = q0 + ld;
+  double rk[2][3], rp[3][2];
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    rk[0][b] = static_cast<double>(q0[b]);
+    rk[1][b] = static_cast<double>(q1[b]);
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    rp[a][0] = static_cast<double>(S[a * ld + ix]);
+    rp[a][1] = static_cast<double>(S[a * ld + ix + 1]);
+  }
+  kk[0] = static_cast<double>(q0[ix]);
+  kk[1] = static_cast<double>(q0[ix + 1]);
+  kk[2] = static_cast<double>(q1[ix]);
+  kk[3] = static_cast<double>(q1[ix + 1]);
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) kp[3 * e + b] = rk[e][b] + rk[e][0] * alpha_of(b, a1, a2);
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) pk[2 * a + e] = rp[a][e] + alpha_of(a, a1, a2) * rp[0][e];
+  c0[0] = rk[0][0];
+  c0[1] = rk[1][0];
+  r0[0] = rp[0][0];
+  r0[1] = rp[0][1];
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long* p) {
+  return __hip_atomic_load((const gu64*)(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1_f64(const double* p) {
+  return __longlong_as_double(static_cast<long long>(
+      ld_sc1_u64(reinterpret_cast<const unsigned long long*>(p))));
+}
+
+// wave argmin of (d, k): the smaller d, ties (and two +inf) to the lower k
+__device__ __forceinline__ void wave_argmin(double& d, int& k) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double od = __shfl_xor(d, o, 64);
+    const int ok = __shfl_xor(k, o, 64);
+    if (od < d || (od == d && ok < k)) {
+      d = od;
+      k = ok;
+    }
+  }
+}
+
+// The G workgroups of a filter publish their (d, k) for exchange `c` and wait for everyone's:
+// three 8-byte {tag, value} granules per workgroup (d's two halves, k), stored by lane 0 after the
+// wave's write-through table stores have drained; lanes < G poll one workgroup's each. Returns the
+// filter-wide argmin (the same in every workgroup), or (inf, INT_MAX) and *timeout on a stuck poll.
+__device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g, int c,
+                                         unsigned tag, double& d, int& k, bool* timeout) {
+  drain_stores();  // R1: this wave's sc1 table stores of the step are complete before its granule
+  const int lane = threadIdx.x;
+  unsigned long long* mine = gran + (static_cast<size_t>(c) * G + g) * 4;
+  const unsigned long long hi = static_cast<unsigned long long>(tag) << 32;
+  const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(d));
+  if (lane == 0) {
+    __hip_atomic_store((gu64*)(mine + 0), hi | (bits & 0xffffffffull),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64*)(mine + 1), hi | (bits >> 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64*)(mine + 2), hi | static_cast<unsigned>(k),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  double od = INFINITY;
+  int ok = INT_MAX;
+  for (int base = 0; base < G; base += 64) {
+    const int w = base + lane;
+    const unsigned long long* src = gran + (static_cast<size_t>(c) * G + (w < G ? w : 0)) * 4;
+    for (unsigned spins = 0;; ++spins) {
+      bool got = true;
+      unsigned long long v0 = 0, v1 = 0, v2 = 0;
+      if (w < G) {
+        v0 = ld_sc1_u64(src + 0);
+        v1 = ld_sc1_u64(src + 1);
+        v2 = ld_sc1_u64(src + 2);
+        got = (v0 >> 32) == tag && (v1 >> 32) == tag && (v2 >> 32) == tag;
+      }
+      if (__all(got)) {
+        if (w < G) {
+          const double dv = __longlong_as_double(
+              static_cast<long long>(((v1 & 0xffffffffull) << 32) | (v0 & 0xffffffffull)));
+          const int kv = static_cast<int>(static_cast<unsigned>(v2));
+          if (dv < od || (dv == od && kv < ok)) {
+            od = dv;
+            ok = kv;
+          }
+        }
+        break;
+      }
+      if (spins >= kAmSpin) {
+        *timeout = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  // loads of the published tables come after the poll (sc1 loads: they bypass this CU's L1)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_argmin(od, ok);
+  d = od;
+  k = ok;
+}
+
+}  // namespace
+
+template <typename T>
+__global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B) {
+  __shared__ AmShared sh;
+  const int g = blockIdx.x, G = B.G, fy = blockIdx.y;
+  const MsgDesc& d = A.desc[fy];
+  const int flags = d.flags;
+  if (!(flags & kActive)) return;  // (every workgroup of the filter)
+  const int f = A.f0 + fy;
+  const int lane = threadIdx.x;
+  const int N = A.N, ld = A.ld, ldk = A.ldk;
+  const int Np = G * kAmSlots;
+  const int k = g * kAmSlots + lane;  // this lane's landmark slot
+  const bool valid = k < N;
+  const int ix = 3 + 2 * (valid ? k : N - 1);  // its state index (clamped for the loads)
+  const T* S = A.sig[d.parity] + f * A.sig_stride;
+  const double* xin = A.x[d.parity] + f * A.x_stride;
+  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
+  T* kc = A.kcat + f * A.km_stride;
+  T* mc = A.mcat + f * A.km_stride;
+  FilterCtl* ctl = A.ctl + f;
+  AmHist* hist = B.hist + f * B.hist_stride;
+  AmCur* cur = B.cur + f * B.cur_stride;
+  unsigned long long* gran = B.gran + f * B.gran_stride;
+  const int m = d.m;
+  const double r_noise = A.r, gate = A.gate;
+  const unsigned tagbase = (A.seq & 0x07ffffffu) << 5;
+  bool timeout = false;
+  unsigned status = 0;
+
+  // ---- predict (slam.cpp:321-335): the pose, At's two entries, the pose block (every lane) ----
+  double pose[3], a1, a2;
+  predicted_pose(ctl->tmo, d, xin, pose, &a1, &a2);
+  const bool first = (flags & kFirst) != 0;
+  double Pp[3][3], raw[3][3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) raw[a][b] = static_cast<double>(S[a * ld + b]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const double aa = alpha_of(a, a1, a2), ab = alpha_of(b, a1, a2);
+      double v = raw[a][b] + aa * raw[0][b];
+      v = v + (raw[a][0] + aa * raw[0][0]) * ab;
+      if (first && a == b) v += A.q;
+      Pp[a][b] = v;
+    }
+  // the lane's slot: its predicted block and state
+  double kk[4], kp[6], pk[6], c0[2], r0[2];
+  slot_block(S, ld, ix, a1, a2, kk, kp, pk, c0, r0);
+  double xk[2] = {xin[ix], xin[ix + 1]};
+  unsigned s = ctl->counter;
+
+  // the state at the chunk's start, for the first step's exchange
+  if (valid && G > 1) {
+    AmCur* o = cur + k;
+    const auto rc = buf_rsrc(o, sizeof(AmCur));
+    st_wt2(rc, 0, kk[0], kk[1]);
+    st_wt2(rc, 16, kk[2], kk[3]);
+    st_wt2(rc, 32, kp[0], kp[1]);
+    st_wt2(rc, 48, kp[2], kp[3]);
+    st_wt2(rc, 64, kp[4], kp[5]);
+    st_wt2(rc, 80, pk[0], pk[1]);
+    st_wt2(rc, 96, pk[2], pk[3]);
+    st_wt2(rc, 112, pk[4], pk[5]);
+    st_wt2(rc, 128, xk[0], xk[1]);
+  }
+  bool any_new = false;
+
+  for (int c = 0; c < m; ++c) {
+    const double z0 = d.z[c][0], z1 = d.z[c][1];
+    // ---- marker c's distance to this lane's landmark (slam.cpp:361-416) ----
+    double key = INFINITY;
+    if (valid && k < static_cast<int>(s)) {
+      double P[5][5];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) P[a][b] = Pp[a][b];
+        P[a][3] = pk[2 * a];
+        P[a][4] = pk[2 * a + 1];
+        P[3][a] = kp[a];
+        P[4][a] = kp[3 + a];
+      }
+      P[3][3] = kk[0];
+      P[3][4] = kk[1];
+      P[4][3] = kk[2];
+      P[4][4] = kk[3];
+      const double dist = assoc_dist(P, pose, xk[0], xk[1], z0, z1, r_noise);
+      key = dist < INFINITY ? dist : INFINITY;  // NaN never wins (strict <, k_assoc)
+    }
+    int kbest = valid ? k : INT_MAX;
+    wave_argmin(key, kbest);
+    if (G > 1) exchange(gran, G, g, c, tagbase | static_cast<unsigned>(c + 1), key, kbest, &timeout);
+    key = __longlong_as_double(static_cast<long long>(__builtin_amdgcn_readfirstlane(
+              static_cast<int>(__double_as_longlong(key))) & 0xffffffffull) |
+          (static_cast<long long>(__builtin_amdgcn_readfirstlane(
+               static_cast<int>(__double_as_longlong(key) >> 32))) << 32));
+    kbest = __builtin_amdgcn_readfirstlane(kbest);  // (every lane holds the same argmin)
+    // ---- decision (slam.cpp:418-440): the new slot (index s, d = gate) wins only over a strictly
+    // larger existing minimum; a full map is the reference's out-of-range state index ----
+    int j;
+    bool isnew = false;
+    if (!(key <= gate)) {
+      if (s >= static_cast<unsigned>(N)) {
+        j = -1;
+        status |= EKF_FLAG_RANGE_D;
+      } else {
+        j = static_cast<int>(s);
+        isnew = true;
+        ++s;
+        any_new = true;
+      }
+    } else {
+      j = kbest;
+    }
+    if (lane == 0) {
+      sh.jl[c] = j;
+      if (g == 0) {
+        const int slot = (d.assoc_slot + c) & (kMaxAssoc - 1);
+        ctl->assoc_j[slot] = j;
+        ctl->assoc_new[slot] = isnew ? 1 : 0;
+      }
+    }
+    double Kk[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, Mk[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    double Kp[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}}, Mp[2][3] = {{0.0, 0.0, 0.0},
+                                                                         {0.0, 0.0, 0.0}};
+    if (j >= 0) {
+      const int jx = 3 + 2 * j;
+      // the new landmark's state (slam.cpp:351-354, the pose before this marker's correction)
+      const double nx = pose[1] + z0 * cos(z1 + pose[0]);
+      const double ny = pose[2] + z0 * sin(z1 + pose[0]);
+      if (isnew && k == j) {
+        xk[0] = nx;
+        xk[1] = ny;
+      }
+      // ---- j's block, state and history (one round of sc1 loads), crosses from Σ_in ----
+      double v[3];
+      const AmCur* jc = cur + static_cast<size_t>(c) * Np + j;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int e = lane + 64 * i;  // 0..17: the AmCur fields; then 8 per earlier step
+        v[i] = 0.0;
+        if (G > 1 && e < 18) {
+          v[i] = ld_sc1_f64(&jc->kk[0] + e);
+        } else if (G > 1 && e < 18 + 8 * c) {
+          const int cc = (e - 18) >> 3, t = (e - 18) & 7;
+          const AmHist* hh = hist + static_cast<size_t>(cc) * Np + j;
+          v[i] = ld_sc1_f64((t < 4 ? hh->k : hh->m) + (t & 3));
+        }
+      }
+      // Σ_in crosses of this lane's slot with j (no predict term between landmarks)
+      const T* q0 = S + static_cast<size_t>(ix) * ld;
+      const T* p0 = S + static_cast<size_t>(jx) * ld;
+      double rkj[4], rjk[4];
+      rkj[0] = static_cast<double>(q0[jx]);
+      rkj[1] = static_cast<double>(q0[jx + 1]);
+      rkj[2] = static_cast<double>(q0[ld + jx]);
+      rkj[3] = static_cast<double>(q0[ld + jx + 1]);
+      rjk[0] = static_cast<double>(p0[ix]);
+      rjk[1] = static_cast<double>(p0[ix + 1]);
+      rjk[2] = static_cast<double>(p0[ld + ix]);
+      rjk[3] = static_cast<double>(p0[ld + ix + 1]);
+      if (G > 1) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int e = lane + 64 * i;
+          if (e < 18) sh.jc[e] = v[i];
+          else if (e < 18 + 8 * c) sh.jh[(e - 18) >> 3][(e - 18) & 7] = v[i];
+        }
+      } else {  // one workgroup: j's lane holds its block (v_readlane), its history is in LDS
+        const int lj = j;
+        double jv[18];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) jv[t] = readlane_f64(kk[t], lj);
+#pragma unroll
+        for (int t = 0; t < 6; ++t) jv[4 + t] = readlane_f64(kp[t], lj);
+#pragma unroll
+        for (int t = 0; t < 6; ++t) jv[10 + t] = readlane_f64(pk[t], lj);
+        jv[16] = readlane_f64(xk[0], lj);
+        jv[17] = readlane_f64(xk[1], lj);
+        if (lane == 0) {
+#pragma unroll
+          for (int t = 0; t < 18; ++t) sh.jc[t] = jv[t];
+        }
+        for (int e = lane; e < 8 * c; e += 64) {
+          const int cc = e >> 3, t = e & 7;
+          sh.jh[cc][t] = t < 4 ? sh.hk[cc][t][lj] : sh.hm[cc][t - 4][lj];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      double jkk[4], jkp[6], jpk[6], xj[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) jkk[t] = sh.jc[t];
+#pragma unroll
+      for (int t = 0; t < 6; ++t) jkp[t] = sh.jc[4 + t];
+#pragma unroll
+      for (int t = 0; t < 6; ++t) jpk[t] = sh.jc[10 + t];
+      xj[0] = isnew ? nx : sh.jc[16];
+      xj[1] = isnew ? ny : sh.jc[17];
+      // ---- the step (slam.cpp:443-488), every lane the same: ẑ, H, S, S⁻¹, ν, K / M at the pose ----
+      double zhat[2], H0[5], H1[5], braw;
+      bool bok;
+      range_bearing(pose, xj[0], xj[1], zhat, H0, H1, &braw, &bok);
+      if (!bok) zhat[1] = normalize_angle(braw);
+      double P5[5][5];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) P5[a][b] = Pp[a][b];
+        P5[a][3] = jpk[2 * a];
+        P5[a][4] = jpk[2 * a + 1];
+        P5[3][a] = jkp[a];
+        P5[4][a] = jkp[3 + a];
+      }
+      P5[3][3] = jkk[0];
+      P5[3][4] = jkk[1];
+      P5[4][3] = jkk[2];
+      P5[4][4] = jkk[3];
+      double Gt[5][2];  // (Σ·Hᵀ)[pA]
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        double g0 = 0.0, g1 = 0.0;
+#pragma unroll
+        for (int b = 0; b < 5; ++b) {
+          g0 += P5[a][b] * H0[b];
+          g1 += P5[a][b] * H1[b];
+        }
+        Gt[a][0] = g0;
+        Gt[a][1] = g1;
+      }
+      double Sm[4] = {0.0, 0.0, 0.0, 0.0};  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:476)
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        Sm[0] += H0[a] * Gt[a][0];
+        Sm[1] += H0[a] * Gt[a][1];
+        Sm[2] += H1[a] * Gt[a][0];
+        Sm[3] += H1[a] * Gt[a][1];
+      }
+      Sm[0] += r_noise;
+      Sm[3] += r_noise;
+      double Si[4];
+      if (!inv2(Sm, Si)) {
+        status |= EKF_FLAG_NUMERIC_D;  // Armadillo's inv throws; this marker is skipped
+      } else {
+        const double nu0 = z0 - zhat[0];
+        const double nu1 = normalize_angle(z1 - zhat[1]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          Kp[a][0] = Gt[a][0] * Si[0] + Gt[a][1] * Si[2];
+          Kp[a][1] = Gt[a][0] * Si[1] + Gt[a][1] * Si[3];
+        }
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+          for (int a = 0; a < 5; ++a) {
+            m0 += H0[a] * P5[a][b];
+            m1 += H1[a] * P5[a][b];
+          }
+          Mp[0][b] = m0;
+          Mp[1][b] = m1;
+        }
+        // ---- this lane's slot: the crosses with j at step c, K[k], M[:, k] ----
+        if (k == j) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            rkj[t] = kk[t];
+            rjk[t] = kk[t];
+          }
+        } else {
+          for (int cc = 0; cc < c; ++cc) {
+            const double* jk = sh.jh[cc];
+            const double* jm = sh.jh[cc] + 4;
+            const double ok0 = sh.hk[cc][0][lane], ok1 = sh.hk[cc][1][lane];
+            const double ok2 = sh.hk[cc][2][lane], ok3 = sh.hk[cc][3][lane];
+            const double om0 = sh.hm[cc][0][lane], om1 = sh.hm[cc][1][lane];
+            const double om2 = sh.hm[cc][2][lane], om3 = sh.hm[cc][3][lane];
+            // Σ_c[k, j] −= K[k]·M[:, j];  Σ_c[j, k] −= K[j]·M[:, k]
+            rkj[0] = rank2_sub(rkj[0], ok0, ok1, jm[0], jm[2]);
+            rkj[1] = rank2_sub(rkj[1], ok0, ok1, jm[1], jm[3]);
+            rkj[2] = rank2_sub(rkj[2], ok2, ok3, jm[0], jm[2]);
+            rkj[3] = rank2_sub(rkj[3], ok2, ok3, jm[1], jm[3]);
+            rjk[0] = rank2_sub(rjk[0], jk[0], jk[1], om0, om2);
+            rjk[1] = rank2_sub(rjk[1], jk[0], jk[1], om1, om3);
+            rjk[2] = rank2_sub(rjk[2], jk[2], jk[3], om0, om2);
+            rjk[3] = rank2_sub(rjk[3], jk[2], jk[3], om1, om3);
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          double g0 = 0.0, g1 = 0.0;  // (Σ·Hᵀ)[k_a] over pA
+#pragma unroll
+          for (int b = 0; b < 3; ++b) {
+            g0 += kp[3 * a + b] * H0[b];
+            g1 += kp[3 * a + b] * H1[b];
+          }
+          g0 += rkj[2 * a] * H0[3];
+          g0 += rkj[2 * a + 1] * H0[4];
+          g1 += rkj[2 * a] * H1[3];
+          g1 += rkj[2 * a + 1] * H1[4];
+          Kk[a][0] = g0 * Si[0] + g1 * Si[2];
+          Kk[a][1] = g0 * Si[1] + g1 * Si[3];
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          double m0 = 0.0, m1 = 0.0;  // (H·Σ)[:, k_b]
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            m0 += H0[a] * pk[2 * a + b];
+            m1 += H1[a] * pk[2 * a + b];
+          }
+          m0 += H0[3] * rjk[b];
+          m0 += H0[4] * rjk[2 + b];
+          m1 += H1[3] * rjk[b];
+          m1 += H1[4] * rjk[2 + b];
+          Mk[0][b] = m0;
+          Mk[1][b] = m1;
+        }
+        // ---- Σ ← Σ − K·M on the lane's block and the pose block; x += K·ν (slam.cpp:482-488) ----
+        double nkk[4], nkp[6], npk[6];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            nkk[2 * a + b] = rank2_sub(kk[2 * a + b], Kk[a][0], Kk[a][1], Mk[0][b], Mk[1][b]);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 3; ++b)
+            nkp[3 * a + b] = rank2_sub(kp[3 * a + b], Kk[a][0], Kk[a][1], Mp[0][b], Mp[1][b]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            npk[2 * a + b] = rank2_sub(pk[2 * a + b], Kp[a][0], Kp[a][1], Mk[0][b], Mk[1][b]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) kk[t] = nkk[t];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          kp[t] = nkp[t];
+          pk[t] = npk[t];
+        }
+        xk[0] = xk[0] + (Kk[0][0] * nu0 + Kk[0][1] * nu1);
+        xk[1] = xk[1] + (Kk[1][0] * nu0 + Kk[1][1] * nu1);
+        double nP[3][3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+          for (int b = 0; b < 3; ++b) nP[a][b] = rank2_sub(Pp[a][b], Kp[a][0], Kp[a][1], Mp[0][b], Mp[1][b]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+#pragma unroll
+          for (int b = 0; b < 3; ++b) Pp[a][b] = nP[a][b];
+          pose[a] = pose[a] + (Kp[a][0] * nu0 + Kp[a][1] * nu1);
+        }
+        pose[0] = normalize_angle(pose[0]);  // slam.cpp:488
+      }
+    }
+    // ---- the step's factors: history (LDS + write-through table), Kcat / Mcat rows ----
+    sh.hk[c][0][lane] = Kk[0][0];
+    sh.hk[c][1][lane] = Kk[0][1];
+    sh.hk[c][2][lane] = Kk[1][0];
+    sh.hk[c][3][lane] = Kk[1][1];
+    sh.hm[c][0][lane] = Mk[0][0];
+    sh.hm[c][1][lane] = Mk[0][1];
+    sh.hm[c][2][lane] = Mk[1][0];
+    sh.hm[c][3][lane] = Mk[1][1];
+    if (valid) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        kc[(2 + 2 * c + e) * ldk + ix] = static_cast<T>(Kk[0][e]);
+        kc[(2 + 2 * c + e) * ldk + ix + 1] = static_cast<T>(Kk[1][e]);
+        mc[(2 + 2 * c + e) * ldk + ix] = static_cast<T>(Mk[e][0]);
+        mc[(2 + 2 * c + e) * ldk + ix + 1] = static_cast<T>(Mk[e][1]);
+      }
+      if (G > 1 && c + 1 < m) {
+        const auto rh = buf_rsrc(hist + static_cast<size_t>(c) * Np + k, sizeof(AmHist));
+        st_wt2(rh, 0, Kk[0][0], Kk[0][1]);
+        st_wt2(rh, 16, Kk[1][0], Kk[1][1]);
+        st_wt2(rh, 32, Mk[0][0], Mk[0][1]);
+        st_wt2(rh, 48, Mk[1][0], Mk[1][1]);
+      }
+    }
+    if (g == 0 && lane < 3) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double kv = lane == 0 ? Kp[0][e] : (lane == 1 ? Kp[1][e] : Kp[2][e]);
+        const double mv = lane == 0 ? Mp[e][0] : (lane == 1 ? Mp[e][1] : Mp[e][2]);
+        kc[(2 + 2 * c + e) * ldk + lane] = static_cast<T>(kv);
+        mc[(2 + 2 * c + e) * ldk + lane] = static_cast<T>(mv);
+      }
+    }
+    if (valid && G > 1 && c + 1 < m) {  // the slot's block and state as step c + 1 starts
+      const auto rc = buf_rsrc(cur + static_cast<size_t>(c + 1) * Np + k, sizeof(AmCur));
+      st_wt2(rc, 0, kk[0], kk[1]);
+      st_wt2(rc, 16, kk[2], kk[3]);
+      st_wt2(rc, 32, kp[0], kp[1]);
+      st_wt2(rc, 48, kp[2], kp[3]);
+      st_wt2(rc, 64, kp[4], kp[5]);
+      st_wt2(rc, 80, pk[0], pk[1]);
+      st_wt2(rc, 96, pk[2], pk[3]);
+      st_wt2(rc, 112, pk[4], pk[5]);
+      st_wt2(rc, 128, xk[0], xk[1]);
+    }
+  }
+
+  // ---- the chunk's remaining factor rows: the predict's two rank-1 terms (slam.cpp:198, as
+  // k_factors writes them), zero rows up to the pass's rank kw ----
+  const int kw = ((2 + 2 * m + 3) / 4) * 4;
+  if (valid) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      kc[0 * ldk + ix + e] = static_cast<T>(0.0);                  // −α_i = 0 for landmark rows
+      kc[1 * ldk + ix + e] = static_cast<T>(first ? -c0[e] : 0.0);  // −(Σ[i][0] + α_i·Σ[0][0])
+      mc[0 * ldk + ix + e] = static_cast<T>(first ? r0[e] : 0.0);   // Σ[0][j]
+      mc[1 * ldk + ix + e] = static_cast<T>(0.0);                  // α_j = 0
+      for (int rr = 2 + 2 * m; rr < kw; ++rr) {
+        kc[rr * ldk + ix + e] = static_cast<T>(0.0);
+        mc[rr * ldk + ix + e] = static_cast<T>(0.0);
+      }
+    }
+    xout[ix] = xk[0];
+    xout[ix + 1] = xk[1];
+  }
+  if (g == 0 && lane < 3) {
+    const double al = alpha_of(lane, a1, a2);
+    const double rc0 = lane == 0 ? raw[0][0] : (lane == 1 ? raw[1][0] : raw[2][0]);
+    const double r0c = lane == 0 ? raw[0][0] : (lane == 1 ? raw[0][1] : raw[0][2]);
+    kc[0 * ldk + lane] = static_cast<T>(first ? -al : 0.0);
+    kc[1 * ldk + lane] = static_cast<T>(first ? -(rc0 + al * raw[0][0]) : 0.0);
+    mc[0 * ldk + lane] = static_cast<T>(first ? r0c : 0.0);
+    mc[1 * ldk + lane] = static_cast<T>(first ? al : 0.0);
+    for (int rr = 2 + 2 * m; rr < kw; ++rr) {
+      kc[rr * ldk + lane] = static_cast<T>(0.0);
+      mc[rr * ldk + lane] = static_cast<T>(0.0);
+    }
+    xout[lane] = pose[lane];
+  }
+  if (g == 0 && lane == 0) {
+    ctl->counter = s;
+    if (flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:490-494)
+      const Pose2 tmo = compose(Pose2{pose[0], pose[1], pose[2]},
+                                inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
+      ctl->tmo[0] = tmo.theta;
+      ctl->tmo[1] = tmo.x;
+      ctl->tmo[2] = tmo.y;
+    }
+  }
+  if (lane == 0 && (status || timeout) && (g == 0 || timeout))
+    atomicOr(&ctl->status, (g == 0 ? status : 0u) | (timeout ? EKF_FLAG_TIMEOUT_D : 0u));
+
+  // ---- fp32 Σ: the final Σ[U, U] in fp64 over the pass's block when a landmark was committed
+  // (k_patch_stage; its first sighting cancels 1e7 − (1e7 − δ) in fp32) ----
+  if (sizeof(T) != 4) return;
+  ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+  if (!any_new) {
+    if (g == 0 && lane == 0) rec->flags = 0;
+    return;
+  }
+  if (G > 1) {  // the final blocks (cur[m]) and every history row published; then workgroup 0 only
+    if (valid) {
+      const auto rh = buf_rsrc(hist + static_cast<size_t>(m - 1) * Np + k, sizeof(AmHist));
+      st_wt2(rh, 0, sh.hk[m - 1][0][lane], sh.hk[m - 1][1][lane]);
+      st_wt2(rh, 16, sh.hk[m - 1][2][lane], sh.hk[m - 1][3][lane]);
+      st_wt2(rh, 32, sh.hm[m - 1][0][lane], sh.hm[m - 1][1][lane]);
+      st_wt2(rh, 48, sh.hm[m - 1][2][lane], sh.hm[m - 1][3][lane]);
+      const auto rc = buf_rsrc(cur + static_cast<size_t>(m) * Np + k, sizeof(AmCur));
+      st_wt2(rc, 0, kk[0], kk[1]);
+      st_wt2(rc, 16, kk[2], kk[3]);
+      st_wt2(rc, 32, kp[0], kp[1]);
+      st_wt2(rc, 48, kp[2], kp[3]);
+      st_wt2(rc, 64, kp[4], kp[5]);
+      st_wt2(rc, 80, pk[0], pk[1]);
+      st_wt2(rc, 96, pk[2], pk[3]);
+      st_wt2(rc, 112, pk[4], pk[5]);
+      st_wt2(rc, 128, xk[0], xk[1]);
+    }
+    double dd = 0.0;
+    int kd = 0;
+    exchange(gran, G, g, m, tagbase | static_cast<unsigned>(m + 1), dd, kd, &timeout);
+    if (timeout && lane == 0) atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+    if (g != 0) return;
+  }
+  // workgroup 0: U = {θ, x, y, jx, jy per marker} (a skipped marker maps onto θ: never a first
+  // position, never patched); every marker's landmark's final block (pb) and, with G > 1, its
+  // factor history staged into the no longer needed own-history LDS (ph[c][cc][8])
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  const int nu = 3 + 2 * m;
+  double* ph = &sh.hk[0][0][0];  // G > 1: [m][m][8] ≤ 2 048 doubles (the hk region holds 4 096)
+  if (G > 1) {
+    for (int e = lane; e < m * 18; e += 64) {
+      const int c = e / 18, t = e - c * 18;
+      sh.pb[c][t] = ld_sc1_f64(&cur[static_cast<size_t>(m) * Np + max(sh.jl[c], 0)].kk[0] + t);
+    }
+    for (int e = lane; e < m * m * 8; e += 64) {
+      const int c = e / (8 * m), cc = (e >> 3) % m, t = e & 7;
+      const AmHist& hh = hist[static_cast<size_t>(cc) * Np + max(sh.jl[c], 0)];
+      const double v = ld_sc1_f64((t < 4 ? hh.k : hh.m) + (t & 3));
+      __builtin_amdgcn_wave_barrier();  // every lane's loads issued before any lane overwrites
+      ph[e] = v;
+    }
+  } else {
+    for (int c = 0; c < m; ++c) {
+      const int j = __builtin_amdgcn_readfirstlane(max(sh.jl[c], 0));
+      double jv[18];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) jv[t] = readlane_f64(kk[t], j);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) jv[4 + t] = readlane_f64(kp[t], j);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) jv[10 + t] = readlane_f64(pk[t], j);
+      jv[16] = readlane_f64(xk[0], j);
+      jv[17] = readlane_f64(xk[1], j);
+      if (lane == 0) {
+#pragma unroll
+        for (int t = 0; t < 18; ++t) sh.pb[c][t] = jv[t];
+      }
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) sh.pp[3 * a + b] = Pp[a][b];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  // the history of marker position c's landmark at step cc: K (t < 4) and M (t ≥ 4)
+  auto hv = [&](int c, int cc, int t) -> double {
+    if (G > 1) return ph[(c * m + cc) * 8 + t];
+    const int j = max(sh.jl[c], 0);
+    return t < 4 ? sh.hk[cc][t][j] : sh.hm[cc][t - 4][j];
+  };
+  for (int e = lane; e < nu * nu; e += 64) {
+    const int a = e / nu, b = e - a * nu;
+    const int ca = a < 3 ? -1 : (a - 3) >> 1, ea = (a - 3) & 1;
+    const int cb = b < 3 ? -1 : (b - 3) >> 1, eb = (b - 3) & 1;
+    const bool sa = ca >= 0 && sh.jl[ca] < 0, sb = cb >= 0 && sh.jl[cb] < 0;
+    double v;
+    if (sa || sb) {
+      v = 0.0;  // a skipped marker's position (its column maps onto θ and is never patched)
+    } else if (ca < 0 && cb < 0) {
+      v = sh.pp[3 * a + b];
+    } else if (ca < 0) {  // Σ[pose a][landmark]: pk
+      v = sh.pb[cb][10 + 2 * a + eb];
+    } else if (cb < 0) {  // Σ[landmark][pose b]: kp
+      v = sh.pb[ca][4 + 3 * ea + b];
+    } else if (sh.jl[ca] == sh.jl[cb]) {
+      v = sh.pb[ca][2 * ea + eb];
+    } else {  // two landmarks: Σ_in minus the chunk's rank-2 terms, as the lanes' crosses
+      const int ja = 3 + 2 * sh.jl[ca] + ea, jb = 3 + 2 * sh.jl[cb] + eb;
+      v = static_cast<double>(S[static_cast<size_t>(ja) * ld + jb]);
+      for (int cc = 0; cc < m; ++cc)
+        v = rank2_sub(v, hv(ca, cc, 2 * ea), hv(ca, cc, 2 * ea + 1), hv(cb, cc, 4 + eb),
+                      hv(cb, cc, 4 + 2 + eb));
+    }
+    rec->Pend[a][b] = v;
+  }
+  for (int a = lane; a < kMaxU + 1; a += 64) {
+    int u = 0;
+    if (a < 3) {
+      u = a;
+    } else if (a < nu) {
+      const int jj = sh.jl[(a - 3) >> 1];
+      u = jj < 0 ? 0 : 3 + 2 * jj + ((a - 3) & 1);
+    }
+    rec->u[a] = u;
+  }
+  if (lane == 0) {
+    rec->nu = nu;
+    rec->m = m;
+    rec->flags = kPendValid;
+  }
+}
+
+template <typename T>
+hipError_t launch_assoc_msg(const PassArgs<T>& a, const AmArgs& b, int nf, hipStream_t s,
+                            hipEvent_t e0, hipEvent_t e1) {
+  const dim3 grid(b.G, nf);
+  if (e0 && e1)
+    hipExtLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmSlots), 0, s, e0, e1, 0, a, b);
+  else
+    hipLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmSlots), 0, s, a, b);
+  return hipGetLastError();
+}
+
+template hipError_t launch_assoc_msg<double>(const PassArgs<double>&, const AmArgs&, int,
+                                             hipStream_t, hipEvent_t, hipEvent_t);
+template hipError_t launch_assoc_msg<float>(const PassArgs<float>&, const AmArgs&, int, hipStream_t,
+                                            hipEvent_t, hipEvent_t);
+
+}  // namespace ekfslam

@@ -187,70 +187,7 @@ struct ChainShared {
 };
 
 
-// ---- cross-queue hand-offs (chain on the main stream, factors + Σ pass on the bulk stream) ----
-// Protocol of cdna_hip_programming.md §6 Guideline 16: the producer stores its payload write-through
-// (sc1), every storing wave drains (s_waitcnt vmcnt(0)), a workgroup barrier, then ONE lane stores
-// or adds to an agent-scope epoch word; the consumer polls that word relaxed, takes ONE agent
-// acquire, drains, barriers, then loads plainly. Polls are bounded (EKF_FLAG_TIMEOUT).
-#define EKF_FLAG_TIMEOUT_D 4u
-typedef __attribute__((address_space(1))) unsigned gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-
-__device__ __forceinline__ unsigned epoch_load(const unsigned* p) {
-  return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void epoch_store(unsigned* p, unsigned v) {
-  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// One lane: wait until the epoch word reaches v (wrap-safe), then acquire. false on timeout.
-__device__ __noinline__ bool epoch_wait_acquire(const unsigned* p, unsigned v) {
-  bool ok = false;
-  for (unsigned i = 0; i < (1u << 22); ++i) {
-    if (static_cast<int>(epoch_load(p) - v) >= 0) {
-      ok = true;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return ok;
-}
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// write-through stores of hand-off payload
-__device__ __forceinline__ void st_wt(double* p, double v) {
-  __hip_atomic_store((gu64*)p, static_cast<unsigned long long>(__double_as_longlong(v)),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store((gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 16-byte write-through store (buffer store, cache policy sc1) at byte offset `off` of `r`
-__device__ __forceinline__ void st_wt2(__amdgpu_buffer_rsrc_t r, int off, double a, double b) {
-  typedef int i4 __attribute__((ext_vector_type(4)));
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4, make_double2(a, b)), r, off, 0, 16);
-}
-__device__ __forceinline__ void st_wt(int* p, int v) {
-  __hip_atomic_store((gu32*)p, static_cast<unsigned>(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Buffer loads (32-bit offsets; a load past the descriptor's size returns 0 and touches nothing)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
-}
-__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
-}
-typedef unsigned u2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ double ld_f64(__amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
-}
-__device__ __forceinline__ float ld_t(__amdgpu_buffer_rsrc_t r, unsigned vo, float) {
-  return ld_f32(r, vo, 0);
-}
-__device__ __forceinline__ double ld_t(__amdgpu_buffer_rsrc_t r, unsigned vo, double) {
-  return ld_f64(r, vo, 0);
-}
+#include "ekf_sync.hpp"  // (hand-off protocol and buffer-descriptor helpers)
 
 // A workgroup barrier that orders LDS only: global loads in flight stay in flight across it
 // (__syncthreads waits vmcnt(0), and vmcnt counts loads too).
@@ -2369,44 +2306,7 @@ __global__ __launch_bounds__(kAssocThreads) void k_assoc(PassArgs<T> A) {
       P[3 + e][3] = static_cast<double>(row[j]);
       P[3 + e][4] = static_cast<double>(row[j + 1]);
     }
-    double zhat[2], H0[5], H1[5];
-    double braw;
-    bool bok;
-    range_bearing(s_pose, x[j], x[j + 1], zhat, H0, H1, &braw, &bok);
-    if (!bok) zhat[1] = normalize_angle(braw);
-    double HP0[5], HP1[5];
-    for (int bb = 0; bb < 5; ++bb) {
-      double s0 = 0.0, s1 = 0.0;
-      for (int a = 0; a < 5; ++a) {
-        s0 += H0[a] * P[a][bb];
-        s1 += H1[a] * P[a][bb];
-      }
-      HP0[bb] = s0;
-      HP1[bb] = s1;
-    }
-    double psi[4] = {0, 0, 0, 0};
-    for (int b = 0; b < 5; ++b) {
-      psi[0] += HP0[b] * H0[b];
-      psi[1] += HP0[b] * H1[b];
-      psi[2] += HP1[b] * H0[b];
-      psi[3] += HP1[b] * H1[b];
-    }
-    psi[0] += A.r;
-    psi[3] += A.r;
-    const double nu0 = z0 - zhat[0];
-    const double nu1 = normalize_angle(z1 - zhat[1]);
-    double pi[4];
-    double dist = NAN;
-    const double det = psi[0] * psi[3] - psi[1] * psi[2];
-    if (fabs(det) > 0.0) {
-      pi[0] = psi[3] / det;
-      pi[1] = -psi[1] / det;
-      pi[2] = -psi[2] / det;
-      pi[3] = psi[0] / det;
-      const double t0 = nu0 * pi[0] + nu1 * pi[2];
-      const double t1 = nu0 * pi[1] + nu1 * pi[3];
-      dist = t0 * nu0 + t1 * nu1;
-    }
+    const double dist = assoc_dist(P, s_pose, x[j], x[j + 1], z0, z1, A.r);
     if (dist < bestd) {  // strict: first index kept, NaN never selected
       bestd = dist;
       bestk = static_cast<int>(k);

@@ -68,6 +68,24 @@ template <typename T>
 hipError_t launch_assoc(const PassArgs<T>& a, int n_filters, hipStream_t s,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
+// Unknown association, a whole chunk of ≤ kMaxChunk markers in one launch (ekf_assoc.hip): the
+// scratch of the handle's k_assoc_msg (per filter: hist [kMaxChunk][Np], cur [kMaxChunk + 1][Np],
+// granules [kMaxChunk + 1][G][4], Np = G·kAmSlots ≥ N).
+struct AmArgs {
+  AmHist* hist;
+  AmCur* cur;
+  unsigned long long* gran;
+  size_t hist_stride, cur_stride, gran_stride;  // elements between filters
+  int G;                                        // workgroups per filter
+};
+// Scores, decides and corrects every marker of the chunk (slam.cpp:338-488) and writes the chunk's
+// Kcat / Mcat, the new state, t_map_odom and the decisions; the Σ pass then runs as for a known-id
+// chunk. One grid (G, n_filters) of 64-lane workgroups; a filter's G workgroups exchange each
+// step's argmin through granules.
+template <typename T>
+hipError_t launch_assoc_msg(const PassArgs<T>& a, const AmArgs& b, int n_filters, hipStream_t s,
+                            hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+
 // Posterior t_map_odom for filters with no pending Σ pass.
 template <typename T>
 hipError_t launch_posterior(const PassArgs<T>& a, int n_filters, hipStream_t s);

@@ -92,6 +92,54 @@ __device__ __forceinline__ bool inv2(const double* A, double* o) {
   return isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
 }
 
+// slam.cpp:364-401: d_k = νᵀ ψ⁻¹ ν for a landmark at (lx, ly) with P the 5×5 block of Σ over
+// {θ, x, y, kx, ky}: ψ = (H·P)·Hᵀ + R (arma's left-to-right triple product), ν = z − ẑ with the
+// bearing normalised; NaN when ψ is singular (never selected by the strict argmin). One expression
+// for every association kernel (k_assoc, k_assoc_msg), so they decide alike.
+__device__ __forceinline__ double assoc_dist(const double (&P)[5][5], const double* pose,
+                                             double lx, double ly, double z0, double z1,
+                                             double r_noise) {
+  double zhat[2], H0[5], H1[5];
+  double braw;
+  bool bok;
+  range_bearing(pose, lx, ly, zhat, H0, H1, &braw, &bok);
+  if (!bok) zhat[1] = normalize_angle(braw);
+  double HP0[5], HP1[5];
+  for (int bb = 0; bb < 5; ++bb) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int a = 0; a < 5; ++a) {
+      s0 += H0[a] * P[a][bb];
+      s1 += H1[a] * P[a][bb];
+    }
+    HP0[bb] = s0;
+    HP1[bb] = s1;
+  }
+  double psi[4] = {0, 0, 0, 0};
+  for (int b = 0; b < 5; ++b) {
+    psi[0] += HP0[b] * H0[b];
+    psi[1] += HP0[b] * H1[b];
+    psi[2] += HP1[b] * H0[b];
+    psi[3] += HP1[b] * H1[b];
+  }
+  psi[0] += r_noise;
+  psi[3] += r_noise;
+  const double nu0 = z0 - zhat[0];
+  const double nu1 = normalize_angle(z1 - zhat[1]);
+  double dist = NAN;
+  const double det = psi[0] * psi[3] - psi[1] * psi[2];
+  if (fabs(det) > 0.0) {
+    double pi[4];
+    pi[0] = psi[3] / det;
+    pi[1] = -psi[1] / det;
+    pi[2] = -psi[2] / det;
+    pi[3] = psi[0] / det;
+    const double t0 = nu0 * pi[0] + nu1 * pi[2];
+    const double t1 = nu0 * pi[1] + nu1 * pi[3];
+    dist = t0 * nu0 + t1 * nu1;
+  }
+  return dist;
+}
+
 // v − k0·m0 − k1·m1 with one fixed evaluation order (two FMAs), so a value rebuilt on the fly
 // from the previous buffer is bit-identical to the one the block update stores.
 __device__ __forceinline__ double rank2_sub(double v, double k0, double k1, double m0, double m1) {
