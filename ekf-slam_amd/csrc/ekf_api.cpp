@@ -1396,6 +1396,9 @@ int ekf_diag_nb(double* out, unsigned* info) { return ekfslam_diag_read_nb(out, 
 int ekfslam_res_read_stamps(unsigned long long* out, int n);  // ekf_resident.hip
 // dev only: the resident kernel's stamps (filter flo, thread 0): 6 per correction
 int ekf_diag_res_stamps(unsigned long long* out, int n) { return ekfslam_res_read_stamps(out, n); }
+extern "C" int ekfslam_diag_read_am_stamps(unsigned long long* out);  // ekf_assoc.hip
+// dev only: k_assoc_msg's s_memrealtime stamps, [2 workgroups][kMaxChunk + 1][8]
+int ekf_diag_am_stamps(unsigned long long* out) { return ekfslam_diag_read_am_stamps(out); }
 #endif
 
 double ekf_sigma_pass_bytes(ekf_t h, int nf) {

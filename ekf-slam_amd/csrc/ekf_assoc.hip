@@ -44,6 +44,21 @@ namespace ekfslam {
 
 #include "ekf_sync.hpp"
 
+// Diagnostic build only (tools/assoc_stamps.py): s_memrealtime (100 MHz) of workgroup 0 / the last
+// workgroup, lane 0, per step and phase, of the last launch.
+#ifdef EKF_DIAG_STAMPS
+__device__ unsigned long long g_am_stamps[2][kMaxChunk + 1][8];
+#define AM_STAMP(c, i)                                                                    \
+  do {                                                                                    \
+    if (blockIdx.y == 0 && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
+      g_am_stamps[blockIdx.x == 0 ? 0 : 1][c][i] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+#else
+#define AM_STAMP(c, i) \
+  do {                 \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr unsigned kAmSpin = 1u << 22;  // bounded granule polls (EKF_FLAG_TIMEOUT)
@@ -102,6 +117,35 @@ __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long lon
 __device__ __forceinline__ double ld_sc1_f64(const double* p) {
   return __longlong_as_double(static_cast<long long>(
       ld_sc1_u64(reinterpret_cast<const unsigned long long*>(p))));
+}
+
+// This lane's rows of the write-through tables. The buffer descriptor is built from the
+// workgroup's block of 64 rows (wave-uniform, so it stays in SGPRs); the lane's row is the voffset.
+// (A per-lane descriptor made hipcc wrap every store in a 64-iteration waterfall loop: ≈ 30 µs per
+// step.)
+__device__ __forceinline__ void put_cur(AmCur* blk, int lane, const double (&kk)[4],
+                                        const double (&kp)[6], const double (&pk)[6],
+                                        const double (&xk)[2]) {
+  const auto r = buf_rsrc(blk, kAmSlots * sizeof(AmCur));
+  const int o = lane * static_cast<int>(sizeof(AmCur));
+  st_wt2(r, o + 0, kk[0], kk[1]);
+  st_wt2(r, o + 16, kk[2], kk[3]);
+  st_wt2(r, o + 32, kp[0], kp[1]);
+  st_wt2(r, o + 48, kp[2], kp[3]);
+  st_wt2(r, o + 64, kp[4], kp[5]);
+  st_wt2(r, o + 80, pk[0], pk[1]);
+  st_wt2(r, o + 96, pk[2], pk[3]);
+  st_wt2(r, o + 112, pk[4], pk[5]);
+  st_wt2(r, o + 128, xk[0], xk[1]);
+}
+__device__ __forceinline__ void put_hist(AmHist* blk, int lane, double k0, double k1, double k2,
+                                         double k3, double m0, double m1, double m2, double m3) {
+  const auto r = buf_rsrc(blk, kAmSlots * sizeof(AmHist));
+  const int o = lane * static_cast<int>(sizeof(AmHist));
+  st_wt2(r, o + 0, k0, k1);
+  st_wt2(r, o + 16, k2, k3);
+  st_wt2(r, o + 32, m0, m1);
+  st_wt2(r, o + 48, m2, m3);
 }
 
 // wave argmin of (d, k): the smaller d, ties (and two +inf) to the lower k
@@ -233,26 +277,19 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   unsigned s = ctl->counter;
 
   // the state at the chunk's start, for the first step's exchange
-  if (valid && G > 1) {
-    AmCur* o = cur + k;
-    const auto rc = buf_rsrc(o, sizeof(AmCur));
-    st_wt2(rc, 0, kk[0], kk[1]);
-    st_wt2(rc, 16, kk[2], kk[3]);
-    st_wt2(rc, 32, kp[0], kp[1]);
-    st_wt2(rc, 48, kp[2], kp[3]);
-    st_wt2(rc, 64, kp[4], kp[5]);
-    st_wt2(rc, 80, pk[0], pk[1]);
-    st_wt2(rc, 96, pk[2], pk[3]);
-    st_wt2(rc, 112, pk[4], pk[5]);
-    st_wt2(rc, 128, xk[0], xk[1]);
-  }
+  if (valid && G > 1) put_cur(cur + g * kAmSlots, lane, kk, kp, pk, xk);
   bool any_new = false;
 
+  AM_STAMP(kMaxChunk, 0);
   for (int c = 0; c < m; ++c) {
+    AM_STAMP(c, 0);
     const double z0 = d.z[c][0], z1 = d.z[c][1];
+    // a full map: the reference's temporary landmark (slam.cpp:351-356) indexes the state out of
+    // range and throws before any association; the marker is skipped (uniform: no exchange)
+    const bool full = s >= static_cast<unsigned>(N);
     // ---- marker c's distance to this lane's landmark (slam.cpp:361-416) ----
     double key = INFINITY;
-    if (valid && k < static_cast<int>(s)) {
+    if (!full && valid && k < static_cast<int>(s)) {
       double P[5][5];
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
@@ -272,21 +309,24 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     }
     int kbest = valid ? k : INT_MAX;
     wave_argmin(key, kbest);
-    if (G > 1) exchange(gran, G, g, c, tagbase | static_cast<unsigned>(c + 1), key, kbest, &timeout);
+    AM_STAMP(c, 1);
+    if (G > 1 && !full)
+      exchange(gran, G, g, c, tagbase | static_cast<unsigned>(c + 1), key, kbest, &timeout);
     key = __longlong_as_double(static_cast<long long>(__builtin_amdgcn_readfirstlane(
               static_cast<int>(__double_as_longlong(key))) & 0xffffffffull) |
           (static_cast<long long>(__builtin_amdgcn_readfirstlane(
                static_cast<int>(__double_as_longlong(key) >> 32))) << 32));
     kbest = __builtin_amdgcn_readfirstlane(kbest);  // (every lane holds the same argmin)
+    AM_STAMP(c, 2);
     // ---- decision (slam.cpp:418-440): the new slot (index s, d = gate) wins only over a strictly
     // larger existing minimum; a full map is the reference's out-of-range state index ----
     int j;
     bool isnew = false;
-    if (!(key <= gate)) {
-      if (s >= static_cast<unsigned>(N)) {
-        j = -1;
-        status |= EKF_FLAG_RANGE_D;
-      } else {
+    if (full) {
+      j = -1;
+      status |= EKF_FLAG_RANGE_D;
+    } else if (!(key <= gate)) {
+      {
         j = static_cast<int>(s);
         isnew = true;
         ++s;
@@ -373,6 +413,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
       double jkk[4], jkp[6], jpk[6], xj[2];
+      AM_STAMP(c, 3);
 #pragma unroll
       for (int t = 0; t < 4; ++t) jkk[t] = sh.jc[t];
 #pragma unroll
@@ -540,6 +581,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
         pose[0] = normalize_angle(pose[0]);  // slam.cpp:488
       }
     }
+    AM_STAMP(c, 4);
     // ---- the step's factors: history (LDS + write-through table), Kcat / Mcat rows ----
     sh.hk[c][0][lane] = Kk[0][0];
     sh.hk[c][1][lane] = Kk[0][1];
@@ -557,13 +599,9 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
         mc[(2 + 2 * c + e) * ldk + ix] = static_cast<T>(Mk[e][0]);
         mc[(2 + 2 * c + e) * ldk + ix + 1] = static_cast<T>(Mk[e][1]);
       }
-      if (G > 1 && c + 1 < m) {
-        const auto rh = buf_rsrc(hist + static_cast<size_t>(c) * Np + k, sizeof(AmHist));
-        st_wt2(rh, 0, Kk[0][0], Kk[0][1]);
-        st_wt2(rh, 16, Kk[1][0], Kk[1][1]);
-        st_wt2(rh, 32, Mk[0][0], Mk[0][1]);
-        st_wt2(rh, 48, Mk[1][0], Mk[1][1]);
-      }
+      if (G > 1 && c + 1 < m)
+        put_hist(hist + static_cast<size_t>(c) * Np + g * kAmSlots, lane, Kk[0][0], Kk[0][1],
+                 Kk[1][0], Kk[1][1], Mk[0][0], Mk[0][1], Mk[1][0], Mk[1][1]);
     }
     if (g == 0 && lane < 3) {
 #pragma unroll
@@ -574,20 +612,11 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
         mc[(2 + 2 * c + e) * ldk + lane] = static_cast<T>(mv);
       }
     }
-    if (valid && G > 1 && c + 1 < m) {  // the slot's block and state as step c + 1 starts
-      const auto rc = buf_rsrc(cur + static_cast<size_t>(c + 1) * Np + k, sizeof(AmCur));
-      st_wt2(rc, 0, kk[0], kk[1]);
-      st_wt2(rc, 16, kk[2], kk[3]);
-      st_wt2(rc, 32, kp[0], kp[1]);
-      st_wt2(rc, 48, kp[2], kp[3]);
-      st_wt2(rc, 64, kp[4], kp[5]);
-      st_wt2(rc, 80, pk[0], pk[1]);
-      st_wt2(rc, 96, pk[2], pk[3]);
-      st_wt2(rc, 112, pk[4], pk[5]);
-      st_wt2(rc, 128, xk[0], xk[1]);
-    }
+    if (valid && G > 1 && c + 1 < m)  // the slot's block and state as step c + 1 starts
+      put_cur(cur + static_cast<size_t>(c + 1) * Np + g * kAmSlots, lane, kk, kp, pk, xk);
   }
 
+  AM_STAMP(kMaxChunk, 1);
   // ---- the chunk's remaining factor rows: the predict's two rank-1 terms (slam.cpp:198, as
   // k_factors writes them), zero rows up to the pass's rank kw ----
   const int kw = ((2 + 2 * m + 3) / 4) * 4;
@@ -643,21 +672,11 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   }
   if (G > 1) {  // the final blocks (cur[m]) and every history row published; then workgroup 0 only
     if (valid) {
-      const auto rh = buf_rsrc(hist + static_cast<size_t>(m - 1) * Np + k, sizeof(AmHist));
-      st_wt2(rh, 0, sh.hk[m - 1][0][lane], sh.hk[m - 1][1][lane]);
-      st_wt2(rh, 16, sh.hk[m - 1][2][lane], sh.hk[m - 1][3][lane]);
-      st_wt2(rh, 32, sh.hm[m - 1][0][lane], sh.hm[m - 1][1][lane]);
-      st_wt2(rh, 48, sh.hm[m - 1][2][lane], sh.hm[m - 1][3][lane]);
-      const auto rc = buf_rsrc(cur + static_cast<size_t>(m) * Np + k, sizeof(AmCur));
-      st_wt2(rc, 0, kk[0], kk[1]);
-      st_wt2(rc, 16, kk[2], kk[3]);
-      st_wt2(rc, 32, kp[0], kp[1]);
-      st_wt2(rc, 48, kp[2], kp[3]);
-      st_wt2(rc, 64, kp[4], kp[5]);
-      st_wt2(rc, 80, pk[0], pk[1]);
-      st_wt2(rc, 96, pk[2], pk[3]);
-      st_wt2(rc, 112, pk[4], pk[5]);
-      st_wt2(rc, 128, xk[0], xk[1]);
+      put_hist(hist + static_cast<size_t>(m - 1) * Np + g * kAmSlots, lane, sh.hk[m - 1][0][lane],
+               sh.hk[m - 1][1][lane], sh.hk[m - 1][2][lane], sh.hk[m - 1][3][lane],
+               sh.hm[m - 1][0][lane], sh.hm[m - 1][1][lane], sh.hm[m - 1][2][lane],
+               sh.hm[m - 1][3][lane]);
+      put_cur(cur + static_cast<size_t>(m) * Np + g * kAmSlots, lane, kk, kp, pk, xk);
     }
     double dd = 0.0;
     int kd = 0;
@@ -759,6 +778,15 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     rec->flags = kPendValid;
   }
 }
+
+#ifdef EKF_DIAG_STAMPS
+}  // namespace ekfslam
+extern "C" int ekfslam_diag_read_am_stamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(ekfslam::g_am_stamps), sizeof(ekfslam::g_am_stamps)) ==
+                 hipSuccess ? 0 : -5;
+}
+namespace ekfslam {
+#endif
 
 template <typename T>
 hipError_t launch_assoc_msg(const PassArgs<T>& a, const AmArgs& b, int nf, hipStream_t s,
