@@ -422,6 +422,47 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       for (int t = 0; t < 6; ++t) jpk[t] = sh.jc[10 + t];
       xj[0] = isnew ? nx : sh.jc[16];
       xj[1] = isnew ? ny : sh.jc[17];
+      // ---- this lane's slot: its crosses with j at step c (before the step's math, while few
+      // registers are live: the history sums then keep their LDS reads in flight) ----
+      if (k == j) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          rkj[t] = kk[t];
+          rjk[t] = kk[t];
+        }
+      } else {
+        // Σ_c[k, j] = Σ_p[k, j] − Σ_cc K_cc[k]·M_cc[:, j] and Σ_c[j, k] likewise, each sum in
+        // two interleaved fma chains (even / odd steps): half the dependent chain length
+        double ea[8] = {0, 0, 0, 0, 0, 0, 0, 0}, eb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        auto term = [&](int cc, double (&acc)[8]) __attribute__((always_inline)) {
+          const double* jk = sh.jh[cc];
+          const double* jm = sh.jh[cc] + 4;
+          const double ok0 = sh.hk[cc][0][lane], ok1 = sh.hk[cc][1][lane];
+          const double ok2 = sh.hk[cc][2][lane], ok3 = sh.hk[cc][3][lane];
+          const double om0 = sh.hm[cc][0][lane], om1 = sh.hm[cc][1][lane];
+          const double om2 = sh.hm[cc][2][lane], om3 = sh.hm[cc][3][lane];
+          acc[0] = fma(ok1, jm[2], fma(ok0, jm[0], acc[0]));
+          acc[1] = fma(ok1, jm[3], fma(ok0, jm[1], acc[1]));
+          acc[2] = fma(ok3, jm[2], fma(ok2, jm[0], acc[2]));
+          acc[3] = fma(ok3, jm[3], fma(ok2, jm[1], acc[3]));
+          acc[4] = fma(jk[1], om2, fma(jk[0], om0, acc[4]));
+          acc[5] = fma(jk[1], om3, fma(jk[0], om1, acc[5]));
+          acc[6] = fma(jk[3], om2, fma(jk[2], om0, acc[6]));
+          acc[7] = fma(jk[3], om3, fma(jk[2], om1, acc[7]));
+        };
+        int cc = 0;
+        for (; cc + 1 < c; cc += 2) {
+          term(cc, ea);
+          term(cc + 1, eb);
+        }
+        if (cc < c) term(cc, ea);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          rkj[t] = rkj[t] - (ea[t] + eb[t]);
+          rjk[t] = rjk[t] - (ea[4 + t] + eb[4 + t]);
+        }
+      }
+
       // ---- the step (slam.cpp:443-488), every lane the same: ẑ, H, S, S⁻¹, ν, K / M at the pose ----
       double zhat[2], H0[5], H1[5], braw;
       bool bok;
@@ -485,32 +526,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
           Mp[0][b] = m0;
           Mp[1][b] = m1;
         }
-        // ---- this lane's slot: the crosses with j at step c, K[k], M[:, k] ----
-        if (k == j) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            rkj[t] = kk[t];
-            rjk[t] = kk[t];
-          }
-        } else {
-          for (int cc = 0; cc < c; ++cc) {
-            const double* jk = sh.jh[cc];
-            const double* jm = sh.jh[cc] + 4;
-            const double ok0 = sh.hk[cc][0][lane], ok1 = sh.hk[cc][1][lane];
-            const double ok2 = sh.hk[cc][2][lane], ok3 = sh.hk[cc][3][lane];
-            const double om0 = sh.hm[cc][0][lane], om1 = sh.hm[cc][1][lane];
-            const double om2 = sh.hm[cc][2][lane], om3 = sh.hm[cc][3][lane];
-            // Σ_c[k, j] −= K[k]·M[:, j];  Σ_c[j, k] −= K[j]·M[:, k]
-            rkj[0] = rank2_sub(rkj[0], ok0, ok1, jm[0], jm[2]);
-            rkj[1] = rank2_sub(rkj[1], ok0, ok1, jm[1], jm[3]);
-            rkj[2] = rank2_sub(rkj[2], ok2, ok3, jm[0], jm[2]);
-            rkj[3] = rank2_sub(rkj[3], ok2, ok3, jm[1], jm[3]);
-            rjk[0] = rank2_sub(rjk[0], jk[0], jk[1], om0, om2);
-            rjk[1] = rank2_sub(rjk[1], jk[0], jk[1], om1, om3);
-            rjk[2] = rank2_sub(rjk[2], jk[2], jk[3], om0, om2);
-            rjk[3] = rank2_sub(rjk[3], jk[2], jk[3], om1, om3);
-          }
-        }
+        // ---- this lane's slot: K[k], M[:, k] from its crosses with j ----
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           double g0 = 0.0, g1 = 0.0;  // (Σ·Hᵀ)[k_a] over pA

@@ -125,17 +125,13 @@ __device__ __forceinline__ double assoc_dist(const double (&P)[5][5], const doub
   psi[3] += r_noise;
   const double nu0 = z0 - zhat[0];
   const double nu1 = normalize_angle(z1 - zhat[1]);
+  // νᵀ·adj(ψ)·ν / det(ψ): arma's inv (adjugate / det) with the one division taken last
   double dist = NAN;
   const double det = psi[0] * psi[3] - psi[1] * psi[2];
   if (fabs(det) > 0.0) {
-    double pi[4];
-    pi[0] = psi[3] / det;
-    pi[1] = -psi[1] / det;
-    pi[2] = -psi[2] / det;
-    pi[3] = psi[0] / det;
-    const double t0 = nu0 * pi[0] + nu1 * pi[2];
-    const double t1 = nu0 * pi[1] + nu1 * pi[3];
-    dist = t0 * nu0 + t1 * nu1;
+    const double t0 = nu0 * psi[3] - nu1 * psi[2];
+    const double t1 = nu1 * psi[0] - nu0 * psi[1];
+    dist = (t0 * nu0 + t1 * nu1) / det;
   }
   return dist;
 }

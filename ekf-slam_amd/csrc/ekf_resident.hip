@@ -504,12 +504,10 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
               const double nu1 = normalize_angle(z1 - zhat[1]);
               double dist = NAN;
               const double det = psi[0] * psi[3] - psi[1] * psi[2];
-              if (fabs(det) > 0.0) {  // (z_diffᵀ·ψ⁻¹)·z_diff, slam.cpp:401
-                const double p0 = psi[3] / det, p1 = -psi[1] / det;
-                const double p2 = -psi[2] / det, p3 = psi[0] / det;
-                const double t0 = nu0 * p0 + nu1 * p2;
-                const double t1 = nu0 * p1 + nu1 * p3;
-                dist = t0 * nu0 + t1 * nu1;
+              if (fabs(det) > 0.0) {  // (z_diffᵀ·ψ⁻¹)·z_diff, slam.cpp:401 (assoc_dist's form)
+                const double t0 = nu0 * psi[3] - nu1 * psi[2];
+                const double t1 = nu1 * psi[0] - nu0 * psi[1];
+                dist = (t0 * nu0 + t1 * nu1) / det;
               }
               if (dist < bestd) {  // strict: first index kept, NaN never selected
                 bestd = dist;
