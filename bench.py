@@ -474,8 +474,9 @@ def run(args, rank, world, local, backend=None):
     if trace:
         clk.append(("enqueued", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                     time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
-    ekf.sync()
-    be.sync()
+    if backend is not None:
+        ekf.sync()  # (a CPU stand-in backend: its own sync; on the GPU the device-wide sync below
+    be.sync()       # waits for every stream of the library — ekf_replay has enqueued everything)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

@@ -65,6 +65,8 @@ struct ekf_ctx {
   bool assoc_msg = true;         // unknown association by chunks (k_assoc_msg); EKF_ASSOC_MSG=0:
                                  // one association kernel + launch pair per marker
   bool main_dirty = false;       // work on the main stream since the bulk stream last joined it
+  bool epoch_owed = false;       // the last Σ pass published no device epoch (the flush's last
+                                 // launch: the next flush joins the bulk stream on the host)
   AmArgs am{};                   // k_assoc_msg scratch (allocated at the first association chunk)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
   hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
@@ -225,7 +227,7 @@ int join_bulk(ekf_ctx* h) {
 // hd: the host copy of the group's descriptors (nullptr: written on the device, no kStageOut).
 template <typename T>
 int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
-                 bool pipelined, bool nolook) {
+                 bool pipelined, bool nolook, bool publish_end) {
   PassArgs<T> a = args<T>(h, dptr, f0);
   a.desc_stride = nf;
   const unsigned s0 = static_cast<unsigned>(h->seq);
@@ -233,6 +235,7 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
   const bool two = pipelined && !h->serial;
   hipStream_t ms = h->stream, bs = two ? h->bulk : h->stream;
   a.polls = two && h->devsync ? 1 : 0;
+  a.first_ready = h->epoch_owed ? 1 : 0;  // (the host joined the bulk stream since that pass)
   a.nb = a.polls && h->nb ? 1 : 0;
   if (pipelined && !nolook) {
     // events: a rebuilding (kLook) chain needs the Σ pass two launches back
@@ -269,22 +272,26 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
       const int fl = hd[static_cast<size_t>(i) * nf + k].flags;
       stage = stage || ((fl & kActive) && (fl & kStageOut));
     }
+    const bool last = i + 1 == nchunks;
     rc = timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
-      return launch_sigma_pass<T>(ai, nf, !(in_group && i + 1 < nchunks), stage, bs, e0, e1);
+      return launch_sigma_pass<T>(ai, nf, last ? publish_end : !in_group, stage, bs, e0, e1);
     });
     if (rc) return rc;
     if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[(s0 + i) & 1], bs));
   }
   h->seq += nchunks;
+  h->epoch_owed = a.polls && !publish_end;
   return EKF_OK;
 }
 
 // nolook: some active filter's first chunk gathers its own Σ_in (no kLook rebuild)
+// publish_end: the group's last Σ pass publishes its device epoch (false only for a flush's last
+// launch, whose successor the next flush orders on the host: one kernel less on the stream's tail)
 int group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
-          bool pipelined, bool nolook = true) {
+          bool pipelined, bool nolook = true, bool publish_end = true) {
   return h->cfg.dtype == EKF_F32
-             ? launch_group<float>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook)
-             : launch_group<double>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook);
+             ? launch_group<float>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook, publish_end)
+             : launch_group<double>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook, publish_end);
 }
 
 // The chain → factors kernels of a message are a latency-bound critical path; the Σ pass of the
@@ -549,7 +556,7 @@ void plan_unknown(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int 
 // One association chunk per filter of [f0, f0+nf) (descriptors dptr), then its Σ pass, both on the
 // bulk stream (the pass's CUs; the main stream's chains are not involved). The bulk stream joins
 // the main stream first if the latter ran anything since (a chain wrote t_map_odom there).
-int assoc_msg_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
+int assoc_msg_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, bool publish_end) {
   if (int rc = ensure_am(h)) return rc;
   hipStream_t bs = h->serial ? h->stream : h->bulk;
   if (!h->serial && h->main_dirty) {
@@ -568,13 +575,14 @@ int assoc_msg_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf) {
     });
     if (rc) return rc;
     return timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
-      return launch_sigma_pass<T>(a, nf, true, false, bs, e0, e1);
+      return launch_sigma_pass<T>(a, nf, publish_end, false, bs, e0, e1);
     });
   };
   const int rc = h->cfg.dtype == EKF_F32 ? run(float{}) : run(double{});
   if (rc) return rc;
   if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[seq & 1], bs));
   h->seq += 1;
+  h->epoch_owed = h->devsync && !h->serial && !publish_end;
   return EKF_OK;
 }
 
@@ -705,18 +713,19 @@ int flush(ekf_ctx* h) {
         nolook = nolook || ((fl & kActive) && !(fl & kLook));
       }
       rc = group(h, dp, h->plan_d.data() + L.off, L.f0, L.nf, static_cast<int>(lj - li), true,
-                 nolook);
+                 nolook, lj < nl);
       h->main_dirty = true;
       li = lj;
       continue;
     }
     if (L.kind == 3) {
-      rc = assoc_msg_group(h, dp, L.f0, L.nf);
+      rc = assoc_msg_group(h, dp, L.f0, L.nf, li + 1 < nl);
       ++li;
       continue;
     }
     if (L.kind == 1) {
-      const bool poll = h->devsync && !h->serial;
+      // (an owed epoch: k_assoc cannot poll it; the flush's start joined the bulk stream anyway)
+      const bool poll = h->devsync && !h->serial && !h->epoch_owed;
       if (!poll && join_bulk(h)) return EKF_E_HIP;
       rc = assoc(h, dp, L.f0, L.nf, poll);
       // the chunk's factors and Σ pass on the bulk stream (with split CU masks the main stream

@@ -776,7 +776,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // vmcnt(0), together with every early load below
   const int cA = tid >= 3 && tid < 3 + 2 * d.m ? (tid - 3) >> 1 : 0;
   const int aj = ctl->assoc_j[min(max(d.assoc_slot + cA, 0), kMaxAssoc - 1)];
-  if (A.polls && need && tid == 0 && !built && !epoch_wait_acquire(A.sync + kSyncSigma, need))
+  if (A.polls && need && tid == 0 && !built && !(ci == 0 && A.first_ready) &&
+      !epoch_wait_acquire(A.sync + kSyncSigma, need))
     atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
   if (tid == 0) sh.status = 0;

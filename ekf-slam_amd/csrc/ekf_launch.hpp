@@ -31,6 +31,8 @@ struct PassArgs {
   unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
   unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
   unsigned pub_sigma;   // factors: publish this Σ-pass epoch first (the previous chunk's pass, 0 = none)
+  int first_ready;      // chain: the launch's first chunk skips its Σ-epoch poll (the host joined
+                        // the bulk stream before it, and the last pass published no epoch)
   int polls;            // 1: the streams hand off through device epochs (kernels poll them);
                         // 0: stream order / events order everything, no poll and no epoch kernel
   int nb;               // chain (polls only): waves 1–2 rebuild the next chunk's block during the
