@@ -318,8 +318,12 @@ int create_streams(ekf_ctx* h) {
         hipExtStreamCreateWithCUMask(&h->bulk, words, mbulk.data()) == hipSuccess) {
       // device-epoch hand-offs by default; EKF_DEVSYNC=0 synchronises the streams with events
       // (same kernels, one chain launch per chunk: bit-identical to the single-stream order)
+      // A persistent multi-chunk chain launch needs every filter's chain resident at once (a
+      // chain's chunk i+2 waits for the Σ pass of chunk i over ALL filters, whose factor kernels
+      // wait for every chain): with more filters than main-stream CUs it would spin into its
+      // timeouts, so such a split synchronises with events.
       const char* e = std::getenv("EKF_DEVSYNC");
-      h->devsync = !(e && std::atoi(e) == 0);
+      h->devsync = !(e && std::atoi(e) == 0) && h->F <= split * kXcd;
       return EKF_OK;
     }
     if (h->stream) hipStreamDestroy(h->stream);
