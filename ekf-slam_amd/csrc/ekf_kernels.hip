@@ -2037,8 +2037,13 @@ constexpr int kRegRows = 2, kRegCols = 4;
 __host__ __device__ inline int region_tiles(int trows, int tcols) {  // the largest region's tiles
   return ((trows + kRegRows - 1) / kRegRows) * ((tcols + kRegCols - 1) / kRegCols);
 }
+// An explicit occupancy target (the one the registers allowed anyway: 2 waves/SIMD for the wide
+// fp64 tile, 4–5 for the narrow one, 6–7 for fp32) makes the allocator keep the MFMA accumulators
+// in VGPRs instead of AGPRs (no v_accvgpr_read before the Σ_in subtraction and the stores): swarm
+// message 0.719 → 0.703 ms, N = 1024 fp64 pass 16.4 → 15.9 µs, fp32 unchanged
+// (profiles/r3/p3r_vgpr_acc_ab.txt, two alternating runs each)
 template <typename T, bool WIDE>
-__global__ __launch_bounds__(256) void k_sigma_pass(PassArgs<T> A, int tcols, int xcd_b, int nf) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : (sizeof(T) == 8 ? 4 : 6)))) void k_sigma_pass(PassArgs<T> A, int tcols, int xcd_b, int nf) {
   using Tile = PassTile<T, WIDE>;
   SIG_STAMP(0);
   int fb = blockIdx.y, bx = blockIdx.x;
