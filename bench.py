@@ -76,11 +76,14 @@ def parse(argv=None):
     p.add_argument("--seed", type=int, default=20240317,
                    help="filter g (global index over ranks) uses seed + g (SURVEY.md §8d)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and parity legs")
-    p.add_argument("--inputs", choices=["auto", "host", "device"], default="auto",
-                   help="device: odometry, slip and the fake sensor simulated on the GPU inside the "
-                        "timed region, descriptors written there too (include/ekf_sim.h); host: "
-                        "marker arrays from pyekf.synth replayed through ekf_replay; auto: device "
-                        "for the fp64 swarm workloads, host otherwise")
+    p.add_argument("--inputs", choices=["auto", "host", "hbm", "device"], default="auto",
+                   help="hbm: the pyekf.synth marker arrays uploaded to HBM before the timed region "
+                        "and planned on the GPU (ekf_replay_device); device: odometry, slip and the "
+                        "fake sensor simulated on the GPU inside the timed region, descriptors "
+                        "written there too (include/ekf_sim.h); host: the marker arrays replayed "
+                        "through ekf_replay (host planning + PCIe inside the timed region); auto: "
+                        "device for the fp64 swarm workloads, hbm for the other known-id pipeline "
+                        "workloads, host otherwise (association, the resident N = 50)")
     p.add_argument("--parity-messages", type=int, default=10)
     p.add_argument("--traffic", choices=["auto", "off"], default="auto",
                    help="auto: measure the Σ pass's HBM bytes with two rocprofv3 --pmc child runs")
@@ -403,15 +406,24 @@ def run(args, rank, world, local, backend=None):
     dtype = be.F32 if dt == "f32" else be.F64
     W, K = args.warmup, args.steps
     t_gen = time.perf_counter()
-    sw, odom, n_init_target = build_inputs(N, F, W + 2 * K, args.seed, m, rank, n_map)
-    n_warm, counts, ids, act, rel = sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel
-    t_gen = time.perf_counter() - t_gen
     inputs = args.inputs
     if inputs == "auto":
-        inputs = "device" if (F > 1 and dt == "f64" and backend is None) else "host"
+        if F > 1 and dt == "f64" and backend is None:
+            inputs = "device"
+        elif not assoc and not resident and backend is None:
+            inputs = "hbm"
+        else:
+            inputs = "host"
     if inputs == "device" and (dt != "f64" or assoc):
         raise SystemExit("--inputs device: fp64 known-id workloads (fp32 takes its survey on an "
                          "fp64 handle; the device planner writes known-id chunks)")
+    if inputs == "hbm" and (assoc or resident or backend is not None):
+        raise SystemExit("--inputs hbm: known-id workloads on the HBM pipeline (ekf_replay_device)")
+    # hbm: a third span of K messages times the same path with host inputs (PCIe-inclusive)
+    sw, odom, n_init_target = build_inputs(N, F, W + (3 if inputs == "hbm" else 2) * K, args.seed,
+                                           m, rank, n_map)
+    n_warm, counts, ids, act, rel = sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel
+    t_gen = time.perf_counter() - t_gen
     ekf = be.EKF(n_landmarks=N, n_filters=F, dtype=dtype, device=local)
     sim = None
     if inputs == "device":
@@ -422,9 +434,22 @@ def run(args, rank, world, local, backend=None):
                         start_theta=sw.start_pose[0], start_x=sw.start_pose[1],
                         start_y=sw.start_pose[2])
 
-    def msgs(a, b, e=None, known=False):
+    gpu_in = None
+    if inputs == "hbm":  # every message's markers in HBM before anything is timed
+        import torch
+        dev = torch.device("cuda", local)
+        gpu_in = [torch.from_numpy(np.ascontiguousarray(a, dtype=d)).to(dev) for a, d in
+                  ((counts, np.int32), (ids, np.int32), (act, np.int32), (rel, np.float64),
+                   (odom, np.float64))]
+        torch.cuda.synchronize()
+
+    def msgs(a, b, e=None, known=False, host=False):
         if sim is not None and e is None:  # the GPU simulates, senses and plans these messages
             sim.run(sw.cmd[a * tpm:b * tpm], sw.sense[a:b])
+            return
+        if gpu_in is not None and e is None and not host:  # planned on the GPU from HBM
+            gc, gi, ga, gr, go = (g[a:b] for g in gpu_in)
+            ekf.replay_device(gc, gr, go, gi, ga)
             return
         sl = slice(a, b)
         un = assoc and not known  # the survey sights with known ids; the drive's ids are stripped
@@ -450,15 +475,21 @@ def run(args, rank, world, local, backend=None):
         e64.close()
     elif n_warm:
         msgs(0, n_warm)
-    if W:
-        msgs(n_warm, n_warm + W)
+    # the state reads below leave the GPU idle for milliseconds (a whole Σ crosses PCIe), and an idle
+    # GPU enters the timed region at low clocks: the last two warm-up messages run after them
+    W1 = max(W - 2, 0)
+    if W1:
+        msgs(n_warm, n_warm + W1)
     ekf.sync()
     # landmarks initialised (state slot ≠ (0, 0), slam.cpp:213) in every filter of this rank
     n_init = min(int(np.count_nonzero(np.any(ekf.state(f, sigma=False)[0][3:].reshape(-1, 2)
                                              != 0.0, 1))) for f in range(F))
     status = [ekf.status(f) for f in range(F)]
     x0, S0, c0 = ekf.state(0)
-    ws0 = (x0, S0, ekf.map_odom(0), c0)
+    ws0 = (x0, S0, ekf.map_odom(0), c0)  # the state before message t_ws (parity's start)
+    t_ws = n_warm + W1
+    if W > W1:
+        msgs(n_warm + W1, n_warm + W)
 
     # ---- timed region: exactly K messages ----
     t0s = n_warm + W
@@ -505,6 +536,27 @@ def run(args, rank, world, local, backend=None):
     ekf.profile(False)
     live = np.arange(act.shape[2]) < counts[ps][..., None]
     res_corr = int(np.count_nonzero(live & (act[ps] != 2)))
+    host_rate = None
+    if inputs == "hbm":  # the same path fed host arrays (ekf_replay): host planning and PCIe timed
+        hs = slice(t0s + 2 * K, t0s + 3 * K)
+        ekf.sync()  # (the planning state comes back from the device first: not this span's cost)
+        if world > 1:
+            dist.barrier()
+        be.sync()
+        t1 = time.perf_counter()
+        msgs(hs.start, hs.stop, host=True)
+        be.sync()
+        if world > 1:
+            dist.barrier()
+        el_h = time.perf_counter() - t1
+        live_h = np.arange(act.shape[2]) < counts[hs][..., None]
+        corr_h = int(np.count_nonzero(live_h & (act[hs] != 2)))
+        if world > 1:
+            el_h, corr_h, _ = reduce_ranks(el_h, corr_h, poses, be.device)
+        host_rate = {"value": corr_h / el_h, "unit": "corrections/s", "ms_per_step": el_h / K * 1e3,
+                     "note": "PCIe-inclusive: the same messages handed over as host arrays "
+                             "(ekf_replay: host planning, one descriptor upload, launches), "
+                             f"messages {hs.start}..{hs.stop - 1}; not the value"}
     bytes_per_launch = ekf.sigma_pass_bytes()
     avg_sig_s = ms_sig / max(n_sig, 1) / 1e3
     achieved = bytes_per_launch / avg_sig_s / 1e9 if n_sig else 0.0
@@ -536,6 +588,8 @@ def run(args, rank, world, local, backend=None):
                     "then the circle drive with a nusim-style fake sensor)" + (
                         "; odometry, slip and sensing simulated on the GPU inside the timed "
                         "region (ekf_sim)" if inputs == "device" else
+                        "; host-generated markers uploaded to HBM before the timed region, planned "
+                        "on the GPU (ekf_replay_device)" if inputs == "hbm" else
                         "; host-generated markers replayed through ekf_replay"),
             "config": {"workload": args.workload, "baseline_config": cfgname,
                        "n_landmarks": N, "state_dim": n, "filters_per_gpu": F,
@@ -577,6 +631,8 @@ def run(args, rank, world, local, backend=None):
             },
         }
         result["roofline"]["end_to_end_frac"] = result["roofline"]["end_to_end"]["frac"]
+        if host_rate is not None:
+            result["host_inputs"] = host_rate
         if n_asc:
             result["roofline"]["assoc_kernel_avg_us"] = ms_asc / n_asc * 1e3
             result["roofline"]["assoc_launches"] = n_asc
@@ -603,13 +659,17 @@ def run(args, rank, world, local, backend=None):
             }
             result["config"]["device_path"] = "resident"
     # ---- parity (rank 0) and the CPU baseline (rank 0, N=1 only) ----
+    # parity and the CPU leg start from a state the host holds: the survey's (fp32 / association
+    # handles, then messages t0s..) or the one read before the last warm-up messages (t_ws..)
     ws = warm_state[0] if warm_state else ws0
+    tp = t0s if warm_state else t_ws
     if rank == 0 and not args.no_cpu:
         result["parity"] = parity(args, N, ekf_first_poses(args, be, N, dtype, ws, counts, ids,
-                                                           act, rel, odom, t0s, local),
-                                  ws, counts, ids, act, rel, odom, t0s)
+                                                           act, rel, odom, tp, local,
+                                                           gpu_in=gpu_in),
+                                  ws, counts, ids, act, rel, odom, tp)
         if world == 1:
-            result["cpu_baseline"] = cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s)
+            result["cpu_baseline"] = cpu_baseline(args, N, ws, counts, ids, act, rel, odom, tp)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if sim is not None:
@@ -637,14 +697,25 @@ def reduce_ranks(elapsed, corrections, poses, device):
     return float(t.item()), float(c.item()), np.concatenate([g.cpu().numpy() for g in gathered])
 
 
-def ekf_first_poses(args, be, N, dtype, ws, counts, ids, act, rel, odom, t0s, device):
-    """Posterior poses of the first timed messages of filter 0 from the same warm state."""
+def ekf_first_poses(args, be, N, dtype, ws, counts, ids, act, rel, odom, t0s, device,
+                    gpu_in=None):
+    """Posterior poses of the first timed messages of filter 0 from the same warm state, through
+    the path the timed region took (gpu_in: ekf_replay_device on the HBM inputs, a message at a
+    time)."""
     k = args.parity_messages
     x, S, tmo, cnt = ws
     e = be.EKF(n_landmarks=N, dtype=dtype, device=device)
     e.set_state(x, S, tmo=tmo, counter=cnt)
     sl = slice(t0s, t0s + k)
     un = is_assoc(args.workload)
+    if gpu_in is not None:
+        p = []
+        for t in range(t0s, t0s + k):
+            gc, gi, ga, gr, go = (g[t:t + 1, :1].contiguous() for g in gpu_in)
+            e.replay_device(gc, gr, go, gi, ga)
+            p.append(e.pose(0))
+        e.close()
+        return np.stack(p)
     p = e.replay(counts[sl, :1], rel[sl, :1], odom[sl, :1], ids=None if un else ids[sl, :1],
                  actions=act[sl, :1], poses=True, assoc=un)[:, 0]
     e.close()

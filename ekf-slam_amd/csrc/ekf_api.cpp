@@ -84,6 +84,12 @@ struct ekf_ctx {
   void* stage = nullptr; // StageRec<T>[2][F]: a kLook chain's rebuild operands (kStageIn)
   MsgDesc* ddesc = nullptr;
   size_t sig_stride = 0, x_stride = 0, km_stride = 0;
+  // ekf_replay_device: the planning state lives on the device while dev_plan (ping-pong by
+  // dstate_cur); the host mirror below adopts it (adopt_device_plan) before it is used again
+  PlanState* dstate[2] = {nullptr, nullptr};
+  PlanState* hstate = nullptr;  // pinned: host → device and back
+  int dstate_cur = 0;
+  bool dev_plan = false;
   // host mirror
   std::vector<Pose2> odom;
   std::vector<int> parity;
@@ -227,7 +233,7 @@ int join_bulk(ekf_ctx* h) {
 // hd: the host copy of the group's descriptors (nullptr: written on the device, no kStageOut).
 template <typename T>
 int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
-                 bool pipelined, bool nolook, bool publish_end) {
+                 bool pipelined, bool nolook, bool publish_end, bool stage_hint) {
   PassArgs<T> a = args<T>(h, dptr, f0);
   a.desc_stride = nf;
   const unsigned s0 = static_cast<unsigned>(h->seq);
@@ -267,7 +273,9 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
       return launch_factors<T>(ai, nf, bs, e0, e1);
     });
     if (rc) return rc;
-    bool stage = false;  // some filter stages the rebuild operands of its chunk after next
+    // some filter stages the rebuild operands of its chunk after next (device-written descriptors:
+    // the caller's hint, the staging kernel reads every descriptor's own flags)
+    bool stage = !hd && stage_hint;
     for (int k = 0; hd && k < nf; ++k) {
       const int fl = hd[static_cast<size_t>(i) * nf + k].flags;
       stage = stage || ((fl & kActive) && (fl & kStageOut));
@@ -288,10 +296,12 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
 // publish_end: the group's last Σ pass publishes its device epoch (false only for a flush's last
 // launch, whose successor the next flush orders on the host: one kernel less on the stream's tail)
 int group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
-          bool pipelined, bool nolook = true, bool publish_end = true) {
+          bool pipelined, bool nolook = true, bool publish_end = true, bool stage_hint = false) {
   return h->cfg.dtype == EKF_F32
-             ? launch_group<float>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook, publish_end)
-             : launch_group<double>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook, publish_end);
+             ? launch_group<float>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook, publish_end,
+                                   stage_hint)
+             : launch_group<double>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook, publish_end,
+                                    stage_hint);
 }
 
 // The chain → factors kernels of a message are a latency-bound critical path; the Σ pass of the
@@ -760,9 +770,31 @@ int submit(ekf_ctx* h) {
 }
 
 // Before any host access to device state: run what is planned, then wait for it.
+// ekf_replay_device left the planning state on the device: bring it into the host mirror (behind
+// everything enqueued so far) before the host plans or reads per-filter state again.
+int adopt_device_plan(ekf_ctx* h) {
+  if (!h->dev_plan) return EKF_OK;
+  hipSetDevice(h->cfg.device);
+  HIPCHK(hipMemcpyAsync(h->hstate, h->dstate[h->dstate_cur], h->F * sizeof(PlanState),
+                        hipMemcpyDeviceToHost, h->stream));
+  if (drain(h)) return EKF_E_HIP;
+  for (int f = 0; f < h->F; ++f) {
+    const PlanState& ps = h->hstate[f];
+    h->parity[f] = ps.parity;
+    h->prev_m[f] = ps.prev_m;
+    h->pending[f] = static_cast<char>(ps.pending);
+    for (int i = 0; i < kMaxChunk; ++i) h->prev_ids[f][i] = ps.prev_ids[i];
+    h->odom[f] = Pose2{ps.odom[0], ps.odom[1], ps.odom[2]};
+    forget_desc(h, f);
+  }
+  h->dev_plan = false;
+  return EKF_OK;
+}
+
 int settle(ekf_ctx* h) {
   if (int rc = flush(h)) return rc;
-  return drain(h) ? EKF_E_HIP : EKF_OK;
+  if (drain(h)) return EKF_E_HIP;
+  return adopt_device_plan(h);
 }
 
 // Association with the decisions read back (synchronous), kMaxAssoc markers per upload.
@@ -844,6 +876,7 @@ int handle_info(ekf_t h, HandleInfo* out) {
 
 int handle_parity(ekf_t h, int* parity) {
   if (!h || !parity) return EKF_E_ARG;
+  if (int rc = adopt_device_plan(h)) return rc;
   for (int f = 0; f < h->F; ++f) parity[f] = h->parity[f];
   return EKF_OK;
 }
@@ -852,6 +885,7 @@ int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
                     const int* parity_after, const double* odom_after) {
   if (!h || T < 0 || !dd || !parity_after || !odom_after) return EKF_E_ARG;
   hipSetDevice(h->cfg.device);
+  if (int r0 = adopt_device_plan(h)) return r0;
   int rc = EKF_OK;
   if (T > 0) {
     if (h->resident) {
@@ -1035,6 +1069,9 @@ int ekf_destroy(ekf_t h) {
   if (h->rows) hipFree(h->rows);
   if (h->stage) hipFree(h->stage);
   if (h->ddesc) hipFree(h->ddesc);
+  for (PlanState* p : h->dstate)
+    if (p) hipFree(p);
+  if (h->hstate) hipHostFree(h->hstate);
   if (h->am.hist) hipFree(h->am.hist);
   if (h->am.cur) hipFree(h->am.cur);
   if (h->am.gran) hipFree(h->am.gran);
@@ -1074,6 +1111,7 @@ int ekf_get_path(ekf_t h, int* path) {
 
 int ekf_set_odom(ekf_t h, int f, double theta, double x, double y) {
   if (!valid(h, f)) return EKF_E_ARG;
+  if (int rc = adopt_device_plan(h)) return rc;
   h->odom[f] = Pose2{theta, x, y};
   return EKF_OK;
 }
@@ -1082,6 +1120,7 @@ int ekf_fake_sensor(ekf_t h, int f, int m, const int* ids, const int* actions,
                     const double* rel_xy) {
   if (!valid(h, f) || m < 0 || (m > 0 && (!ids || !rel_xy))) return EKF_E_ARG;
   if (m == 0) return EKF_E_EMPTY;
+  if (int rc = adopt_device_plan(h)) return rc;
   auto& mk = h->msgs[0];
   mk.clear();
   for (int i = 0; i < m; ++i) {
@@ -1100,6 +1139,7 @@ int ekf_fake_sensor(ekf_t h, int f, int m, const int* ids, const int* actions,
 int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int* is_new_out) {
   if (!valid(h, f) || m < 0 || (m > 0 && !rel_xy)) return EKF_E_ARG;
   if (m == 0) return EKF_E_EMPTY;
+  if (int rc = adopt_device_plan(h)) return rc;
   auto& mk = h->msgs[0];
   mk.clear();
   for (int i = 0; i < m; ++i) {
@@ -1128,6 +1168,7 @@ int ekf_batch_sensor(ekf_t h, int assoc_mode, int m_max, const int* counts, cons
                      const int* actions, const double* rel_xy, const double* odom) {
   if (!h || m_max < 0 || !counts || (m_max > 0 && !rel_xy) || (!assoc_mode && m_max > 0 && !ids))
     return EKF_E_ARG;
+  if (int r0 = adopt_device_plan(h)) return r0;
   const int rc = load_batch(h, assoc_mode, m_max, counts, ids, actions, rel_xy, odom);
   if (rc) return rc;
   hipSetDevice(h->cfg.device);
@@ -1148,6 +1189,7 @@ int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, con
     return EKF_E_ARG;
   const size_t F = static_cast<size_t>(h->F);
   hipSetDevice(h->cfg.device);
+  if (int rc = adopt_device_plan(h)) return rc;
   for (int t = 0; t < T; ++t) {
     const size_t o = static_cast<size_t>(t) * F * m_max;
     int rc = load_batch(h, assoc_mode, m_max, counts + t * F, ids ? ids + o : nullptr,
@@ -1182,8 +1224,81 @@ int ekf_replay(ekf_t h, int assoc_mode, int T, int m_max, const int* counts, con
   return submit(h);
 }
 
+// Known-association replay whose inputs are already in device memory: the descriptors are planned
+// on the GPU (plan_kernels.hip) into the upload buffer, then the same launch groups as a flush.
+// The planning state (parity, previous chunk, odometry) stays on the device between such calls.
+int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int* d_ids,
+                      const int* d_actions, const double* d_rel_xy, const double* d_odom) {
+  if (!h || T < 0 || m_max < 0 || m_max > kMaxChunk || !d_counts || !d_odom ||
+      (m_max > 0 && (!d_ids || !d_rel_xy)))
+    return EKF_E_ARG;
+  if (h->resident || h->joseph) return EKF_E_ARG;
+  if (T == 0) return EKF_OK;
+  hipSetDevice(h->cfg.device);
+  if (int rc = flush(h)) return rc;  // what the host planned before runs first
+  const size_t F = static_cast<size_t>(h->F);
+  if (!h->dstate[0]) {
+    for (PlanState*& p : h->dstate)
+      if (hipMalloc(&p, F * sizeof(PlanState)) != hipSuccess) return EKF_E_NOMEM;
+    if (hipHostMalloc(reinterpret_cast<void**>(&h->hstate), F * sizeof(PlanState),
+                      hipHostMallocDefault) != hipSuccess)
+      return EKF_E_NOMEM;
+  }
+  if (int rc = reserve_upload(h, static_cast<size_t>(T) * F)) return rc;
+  if (join_bulk(h)) return EKF_E_HIP;  // the bulk stream may still read the last descriptors
+  if (!h->dev_plan) {  // the host mirror goes down once; later device replays chain on the device
+    for (size_t f = 0; f < F; ++f) {
+      PlanState& ps = h->hstate[f];
+      ps = PlanState{};
+      ps.parity = h->parity[f];
+      ps.prev_m = h->prev_m[f];
+      ps.pending = h->pending[f];
+      for (int i = 0; i < kMaxChunk; ++i) ps.prev_ids[i] = h->prev_ids[f][i];
+      ps.odom[0] = h->odom[f].theta;
+      ps.odom[1] = h->odom[f].x;
+      ps.odom[2] = h->odom[f].y;
+    }
+    HIPCHK(hipMemcpyAsync(h->dstate[h->dstate_cur], h->hstate, F * sizeof(PlanState),
+                          hipMemcpyHostToDevice, h->stream));
+    h->dev_plan = true;
+  }
+  ReplayArgs a{};
+  a.counts = d_counts;
+  a.ids = d_ids;
+  a.actions = d_actions;
+  a.rel = d_rel_xy;
+  a.odom = d_odom;
+  a.st_in = h->dstate[h->dstate_cur];
+  a.st_out = h->dstate[h->dstate_cur ^ 1];
+  a.desc = h->ddesc;
+  a.T = T;
+  a.F = h->F;
+  a.M = m_max;
+  a.N = h->cfg.n_landmarks;
+  a.rows = h->rows != nullptr;
+  a.stage = h->stage != nullptr;
+  HIPCHK(launch_plan_replay(a, h->stream));
+  h->dstate_cur ^= 1;
+  // the bulk stream reads these descriptors too: one main → bulk hop
+  HIPCHK(hipEventRecord(h->ev_chain, h->stream));
+  HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
+  h->main_dirty = false;
+  const bool stg = h->stage != nullptr;
+  int rc = EKF_OK;
+  if (h->devsync && !h->serial) {
+    rc = group(h, h->ddesc, nullptr, 0, h->F, T, true, true, false, stg);
+  } else {
+    for (int t = 0; t < T && !rc; ++t)
+      rc = group(h, h->ddesc + static_cast<size_t>(t) * F, nullptr, 0, h->F, 1, true, true, true,
+                 stg);
+  }
+  h->main_dirty = true;
+  return rc;
+}
+
 int ekf_predict(ekf_t h, int f) {
   if (!valid(h, f)) return EKF_E_ARG;
+  if (int rc = adopt_device_plan(h)) return rc;
   h->pending[f] = 1;
   return EKF_OK;
 }
@@ -1191,6 +1306,7 @@ int ekf_predict(ekf_t h, int f) {
 int ekf_correct(ekf_t h, int f, int id, double rx, double ry) {
   if (!valid(h, f)) return EKF_E_ARG;
   if (id < 0 || id >= h->cfg.n_landmarks) return EKF_E_RANGE;
+  if (int rc = adopt_device_plan(h)) return rc;
   auto& mk = h->msgs[0];
   mk.clear();
   Marker k;
@@ -1204,6 +1320,7 @@ int ekf_correct(ekf_t h, int f, int id, double rx, double ry) {
 
 int ekf_associate_correct(ekf_t h, int f, double rx, double ry, int* j, int* is_new) {
   if (!valid(h, f)) return EKF_E_ARG;
+  if (int rc = adopt_device_plan(h)) return rc;
   auto& mk = h->msgs[0];
   mk.clear();
   Marker k;
@@ -1222,6 +1339,7 @@ int ekf_associate_correct(ekf_t h, int f, double rx, double ry, int* j, int* is_
 
 int ekf_posterior(ekf_t h, int f) {
   if (!valid(h, f)) return EKF_E_ARG;
+  if (int rc = adopt_device_plan(h)) return rc;
   hipSetDevice(h->cfg.device);
   if (h->pending[f]) {  // fold the pending predict into a zero-marker pass, then the posterior
     h->msgs[0].clear();

@@ -104,6 +104,32 @@ hipError_t launch_resident(const PassArgs<double>& a, const PlanEntry* plan, int
                            int nfil, hipStream_t s, hipEvent_t e0 = nullptr,
                            hipEvent_t e1 = nullptr);
 
+// Known-association replay planned on the GPU (plan_kernels.hip, ekf_replay_device): a filter's
+// planning state between messages — ekf_api.cpp's host mirror of it — before and after a replay.
+struct alignas(16) PlanState {
+  int parity;    // Σ / x copy that is "in"
+  int prev_m;    // markers of the filter's last pipelined chunk (−1: none, the next one gathers)
+  int pending;   // a predict is pending (folded into the next chunk)
+  int pad;
+  int prev_ids[kMaxChunk];
+  double odom[3];  // t_odom_robot of the last message
+  double pad2;
+};
+struct ReplayArgs {
+  const int* counts;      // [T][F]
+  const int* ids;         // [T][F][M]
+  const int* actions;     // [T][F][M] or null
+  const double* rel;      // [T][F][M][2]
+  const double* odom;     // [T][F][3]
+  const PlanState* st_in; // [F]
+  PlanState* st_out;      // [F]
+  MsgDesc* desc;          // [T][F]
+  int T, F, M, N;
+  int rows;               // fp64 pipeline: kRowsOut / kRowsIn hand-offs
+  int stage;              // staged rebuild operands (kStageOut / kStageIn)
+};
+hipError_t launch_plan_replay(const ReplayArgs& a, hipStream_t s);
+
 // Σ₀ diagonal: Σ[i][i] = v for i ≥ 3 (the rest is zero-filled by the caller).
 template <typename T>
 hipError_t launch_init_diag(T* sig, size_t stride, int n, int ld, double v, int nf, hipStream_t s);

@@ -26,7 +26,8 @@ SOURCE_SIM, SOURCE_ASSOC = 0, 1
 EXPORTS = [
     "ekf_config_default", "ekf_strerror", "ekf_create", "ekf_destroy", "ekf_dims", "ekf_get_path",
     "ekf_set_odom",
-    "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_predict",
+    "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_replay_device",
+    "ekf_predict",
     "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_get_pose",
     "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status", "ekf_defer",
     "ekf_set_joseph",
@@ -87,6 +88,7 @@ def lib():
             "ekf_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
             "ekf_batch_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
             "ekf_replay": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+            "ekf_replay_device": (_i, [_vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
             "ekf_predict": (_i, [_vp, _i]),
             "ekf_correct": (_i, [_vp, _i, _i, _d, _d]),
             "ekf_associate_correct": (_i, [_vp, _i, _d, _d, _ip, _ip]),
@@ -139,6 +141,16 @@ def lib():
 
 def _ptr(a):
     return None if a is None else a.ctypes.data
+
+
+def _dptr(x, dtype):
+    """A device buffer for ekf_replay_device: None, an int address, or a contiguous torch tensor
+    of the given dtype on the GPU."""
+    if x is None or isinstance(x, int):
+        return x
+    if not (x.is_cuda and x.is_contiguous() and x.dtype == dtype):
+        raise ValueError(f"device input must be a contiguous {dtype} GPU tensor")
+    return x.data_ptr()
 
 
 def _f64(a):
@@ -225,6 +237,17 @@ class EKF:
                               _ptr(rel), _ptr(odom), _ptr(out))
         _check(rc, "ekf_replay")
         return out
+
+    def replay_device(self, counts, rel_xy, odom, ids, actions=None):
+        """ekf_replay_device: known-id replay whose inputs are GPU tensors already on this handle's
+        device — counts [T,F] int32, rel_xy [T,F,M,2] float64, odom [T,F,3] float64, ids / actions
+        [T,F,M] int32 (M <= EKF_MAX_CHUNK). Asynchronous; keep the tensors alive until a sync."""
+        import torch
+        T, M = int(rel_xy.shape[0]), int(rel_xy.shape[2])
+        rc = lib().ekf_replay_device(self.h, T, M, _dptr(counts, torch.int32),
+                                     _dptr(ids, torch.int32), _dptr(actions, torch.int32),
+                                     _dptr(rel_xy, torch.float64), _dptr(odom, torch.float64))
+        _check(rc, "ekf_replay_device")
 
     # fine-grained
     def predict(self, f=0):

@@ -107,6 +107,18 @@ int ekf_batch_sensor(ekf_t h, int assoc, int m_max, const int* counts, const int
 int ekf_replay(ekf_t h, int assoc, int T, int m_max, const int* counts, const int* ids,
                const int* actions, const double* rel_xy, const double* odom, double* out_pose);
 
+/* ekf_replay with known ids (assoc = 0) whose inputs already live in device memory of the
+ * handle's GPU (same layouts; d_actions nullable): the descriptors are planned on the GPU (one
+ * chunk per message, so m_max <= EKF_MAX_CHUNK; no Joseph form, no resident handle: EKF_E_ARG)
+ * and no input crosses PCIe. The measurement (range, bearing) of slam.cpp:208-210 is computed on
+ * the GPU (correctly rounded sqrt; the bearing's atan2 may differ from glibc's in the last bit).
+ * Inputs are not validated on the host: an id outside [0, N) is skipped by the correction and
+ * sets EKF_FLAG_RANGE in the filter's status. Asynchronous; the inputs must stay valid until the
+ * next synchronising call (ekf_sync, a state read). The handle's planning state comes back to the
+ * host at the next host-planned call or state access. */
+int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int* d_ids,
+                      const int* d_actions, const double* d_rel_xy, const double* d_odom);
+
 /* ---- the finer-grained surface (north_star: predict()/update()/associate()) ---- */
 
 /* Predict (slam.cpp:184-198): deferred and folded into the next Σ pass. */

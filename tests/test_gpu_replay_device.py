@@ -1,0 +1,162 @@
+"""ekf_replay_device (include/ekf.h): a known-id replay whose inputs already live on the GPU, its
+descriptors planned by k_plan_replay (plan_kernels.hip). Parity: the same replay through the
+host planner (ekf_replay, plan_known in ekf_api.cpp) — the reference's fake_sensor_cb
+(nuslam/src/slam.cpp:180-316) message by message — and the CPU oracle."""
+import numpy as np
+import pytest
+
+import pyekf
+from pyekf import synth
+import orc
+
+pytestmark = pytest.mark.gpu
+
+# fp64, against the host planner. The two differ only in the bearing's atan2 (ocml on the device,
+# glibc on the host, ≤ 1 ulp apart); a first sighting's 1e7 − (1e7 − δ) (the reference's prior,
+# slam.cpp:130) amplifies that to ≈ 1e-11 on the new landmark's Σ entries, ≈ 2e-9 at most seen.
+STATE_TOL = 1e-9
+SIGMA_TOL = 1e-8
+
+
+def _inputs(scs, F, T0, T1, holes=False):
+    """counts/ids/actions/rel/odom [T][F](...) for messages [T0, T1) of scenario f % len(scs)."""
+    T = T1 - T0
+    M = max(s.ids.shape[1] for s in scs)
+    cnt = np.zeros((T, F), np.int32)
+    ids = np.zeros((T, F, M), np.int32)
+    act = np.zeros((T, F, M), np.int32)
+    rel = np.zeros((T, F, M, 2))
+    od = np.zeros((T, F, 3))
+    for f in range(F):
+        s = scs[f % len(scs)]
+        k = s.ids.shape[1]
+        cnt[:, f] = s.count[T0:T1]
+        ids[:, f, :k] = s.ids[T0:T1]
+        act[:, f, :k] = s.actions[T0:T1]
+        rel[:, f, :k] = s.rel[T0:T1]
+        od[:, f] = pyekf.odometry(s)[T0:T1]
+    if holes and F > 1:
+        cnt[1::3, 1] = 0                   # filter 1: every 3rd message missing
+        act[2::4, F - 1] = synth.DELETE    # the last filter: every 4th message all DELETE
+    return cnt, ids, act, rel, od
+
+
+def _to_gpu(arrs):
+    import torch
+    cnt, ids, act, rel, od = arrs
+    return (torch.from_numpy(cnt).cuda(), torch.from_numpy(ids).cuda(),
+            torch.from_numpy(act).cuda(), torch.from_numpy(rel).cuda(), torch.from_numpy(od).cuda())
+
+
+def _run(scs, N, F, spans, kinds, dtype=pyekf.EKF_F64, warm=None, holes=False):
+    """Replay the spans [(T0, T1), ...] in order, span i through kinds[i] ('host' / 'device')."""
+    e = pyekf.EKF(n_landmarks=N, n_filters=F, dtype=dtype)
+    if warm is not None:
+        for f in range(F):
+            x, S, tmo, c = warm
+            e.set_state(x, S, tmo=tmo, counter=c, f=f)
+    keep = []
+    for (t0, t1), kind in zip(spans, kinds):
+        cnt, ids, act, rel, od = _inputs(scs, F, t0, t1, holes)
+        if kind == "device":
+            g = _to_gpu((cnt, ids, act, rel, od))
+            keep.append(g)
+            e.replay_device(g[0], g[3], g[4], g[1], g[2])
+        else:
+            e.replay(cnt, rel, od, ids=ids, actions=act)
+    out = [e.state(f) for f in range(F)]
+    st = [e.status(f) for f in range(F)]
+    poses = np.stack([e.pose(f) for f in range(F)])
+    e.close()
+    return out, st, poses
+
+
+def _close(a, b, tol, stol=SIGMA_TOL):
+    for (xa, Sa, ca), (xb, Sb, cb) in zip(a, b):
+        assert ca == cb
+        assert np.abs(xa - xb).max() <= tol
+        assert np.abs(Sa - Sb).max() <= stol
+
+
+@pytest.mark.parametrize("F,env", [(1, {}), (4, {}), (1, {"EKF_DEVSYNC": "0"}),
+                                   (4, {"EKF_SERIAL": "1"}), (3, {"EKF_STAGE": "0", "EKF_ROWS": "0"})],
+                         ids=["1filter", "4filters", "1filter_events", "4filters_serial",
+                              "3filters_nostage_norows"])
+def test_device_replay_equals_host_replay(monkeypatch, F, env):
+    """fp64 N = 96 (the HBM pipeline), 30 messages, every schedule: the device-planned replay ends
+    where the host-planned one does, holes (empty and all-DELETE messages) included."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE", "EKF_ROWS"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pyekf.poison_lds()
+    scs = [synth.synthetic(96, 30, seed=7 + k) for k in range(3)]
+    host, sh, ph = _run(scs, 96, F, [(0, 30)], ["host"], holes=True)
+    dev, sd, pd = _run(scs, 96, F, [(0, 30)], ["device"], holes=True)
+    assert sh == sd == [0] * F
+    _close(host, dev, STATE_TOL)
+    assert np.abs(ph - pd).max() <= STATE_TOL
+
+
+def test_device_replay_chains_with_host_calls():
+    """Host, device, device, host spans of one drive (the planning state goes down to the GPU,
+    stays there between the two device calls, comes back for the host call) against the whole drive
+    on the host, and filter 0 against the CPU oracle."""
+    scs = [synth.synthetic(80, 40, seed=21 + k) for k in range(2)]
+    spans = [(0, 8), (8, 20), (20, 31), (31, 40)]
+    mixed, sm, _ = _run(scs, 80, 2, spans, ["host", "device", "device", "host"])
+    host, sh, _ = _run(scs, 80, 2, [(0, 40)], ["host"])
+    assert sm == sh == [0, 0]
+    _close(host, mixed, STATE_TOL)
+    o = orc.run_scenario(scs[0], False)
+    assert np.abs(mixed[0][0] - o["state"]).max() < 1e-7
+    assert np.abs(mixed[0][1] - o["sigma"]).max() < 1e-7
+
+
+def test_device_replay_fp32_n1024():
+    """The headline shape: fp32 N = 1024 from an fp64 survey, 24 messages of 16 markers through the
+    device planner against the host planner (the staged rebuild operands and the fp32 patch are
+    planned on the GPU too)."""
+    N, warm, T = 1024, 40, 24
+    sc = synth.synthetic(N, warm + T)
+    assert sc.ids.shape[1] <= 16  # EKF_MAX_CHUNK: one chunk per message
+    e64 = pyekf.EKF(n_landmarks=N)
+    odom = pyekf.odometry(sc)
+    e64.replay(sc.count[:warm, None], sc.rel[:warm, None], odom[:warm, None],
+               ids=sc.ids[:warm, None], actions=sc.actions[:warm, None])
+    x0, S0, c0 = e64.state()
+    ws = (x0, S0, e64.map_odom(), c0)
+    e64.close()
+    host, sh, _ = _run([sc], N, 1, [(warm, warm + T)], ["host"], dtype=pyekf.EKF_F32, warm=ws)
+    dev, sd, _ = _run([sc], N, 1, [(warm, warm + T)], ["device"], dtype=pyekf.EKF_F32, warm=ws)
+    assert sh == sd == [0]
+    (xh, Sh, ch), (xd, Sd, cd) = host[0], dev[0]
+    assert ch == cd
+    assert np.abs(xh - xd).max() < 1e-6
+    assert np.abs(Sh - Sd).max() < 1e-6
+    assert np.all(np.isfinite(Sd))
+
+
+def test_device_replay_rejects():
+    """No resident handles, no Joseph form, at most EKF_MAX_CHUNK markers per message (one chunk)."""
+    import torch
+    sc = synth.synthetic(96, 4)
+    g = _to_gpu(_inputs([sc], 1, 0, 4))
+    e = pyekf.EKF(n_landmarks=20)  # fp64, n = 43: the resident path
+    with pytest.raises(pyekf.EkfError):
+        e.replay_device(g[0], g[3], g[4], g[1], g[2])
+    e.close()
+    e = pyekf.EKF(n_landmarks=96)
+    e.set_joseph(True)
+    with pytest.raises(pyekf.EkfError):
+        e.replay_device(g[0], g[3], g[4], g[1], g[2])
+    e.set_joseph(False)
+    wide = torch.zeros((4, 1, 17, 2), dtype=torch.float64, device="cuda")
+    with pytest.raises(pyekf.EkfError):
+        e.replay_device(g[0], wide, g[4], torch.zeros((4, 1, 17), dtype=torch.int32, device="cuda"))
+    with pytest.raises(ValueError):  # host arrays are not device inputs
+        e.replay_device(g[0].cpu(), g[3], g[4], g[1], g[2])
+    e.replay_device(g[0], g[3], g[4], g[1], g[2])
+    e.sync()
+    assert e.status() == 0
+    e.close()
