@@ -442,14 +442,16 @@ def run(args, rank, world, local, backend=None):
                   ((counts, np.int32), (ids, np.int32), (act, np.int32), (rel, np.float64),
                    (odom, np.float64))]
         torch.cuda.synchronize()
+        gpu_rows = [(g.data_ptr(), g[0].numel() * g.element_size()) for g in gpu_in]
 
     def msgs(a, b, e=None, known=False, host=False):
         if sim is not None and e is None:  # the GPU simulates, senses and plans these messages
             sim.run(sw.cmd[a * tpm:b * tpm], sw.sense[a:b])
             return
         if gpu_in is not None and e is None and not host:  # planned on the GPU from HBM
-            gc, gi, ga, gr, go = (g[a:b] for g in gpu_in)
-            ekf.replay_device(gc, gr, go, gi, ga)
+            # message a's rows by address (no tensor slicing on the timed path)
+            pc, pi, pa, pr, po = (base + a * rb for base, rb in gpu_rows)
+            ekf.replay_device_raw(b - a, ids.shape[2], pc, pr, po, pi, pa)
             return
         sl = slice(a, b)
         un = assoc and not known  # the survey sights with known ids; the drive's ids are stripped

@@ -894,6 +894,9 @@ int run_device_plan(ekf_t h, const MsgDesc* dd, const PlanEntry* dplan, int T,
         return launch_resident(a, dplan, T, 0, h->F, h->stream, e0, e1);
       });
     } else {
+      // an owed Σ-pass epoch (the last flush's last pass published none): the chains take every
+      // earlier pass as complete (PassArgs::first_ready), which holds once main has joined bulk
+      if (h->epoch_owed && join_bulk(h)) return EKF_E_HIP;
       // the bulk stream reads these descriptors too (written on the main stream)
       HIPCHK(hipEventRecord(h->ev_chain, h->stream));
       HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
@@ -1245,7 +1248,8 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
       return EKF_E_NOMEM;
   }
   if (int rc = reserve_upload(h, static_cast<size_t>(T) * F)) return rc;
-  if (join_bulk(h)) return EKF_E_HIP;  // the bulk stream may still read the last descriptors
+  // the bulk stream may still read the last descriptors (an idle one reads nothing: no hop)
+  if (hipStreamQuery(h->bulk) != hipSuccess && join_bulk(h)) return EKF_E_HIP;
   if (!h->dev_plan) {  // the host mirror goes down once; later device replays chain on the device
     for (size_t f = 0; f < F; ++f) {
       PlanState& ps = h->hstate[f];
@@ -1279,7 +1283,8 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   a.stage = h->stage != nullptr;
   HIPCHK(launch_plan_replay(a, h->stream));
   h->dstate_cur ^= 1;
-  // the bulk stream reads these descriptors too: one main → bulk hop
+  // the bulk stream reads these descriptors too: one main → bulk hop (recorded before the chain:
+  // behind a persistent chain launch the bulk kernels it waits for could never start)
   HIPCHK(hipEventRecord(h->ev_chain, h->stream));
   HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
   h->main_dirty = false;

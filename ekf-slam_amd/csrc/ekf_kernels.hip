@@ -776,7 +776,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // vmcnt(0), together with every early load below
   const int cA = tid >= 3 && tid < 3 + 2 * d.m ? (tid - 3) >> 1 : 0;
   const int aj = ctl->assoc_j[min(max(d.assoc_slot + cA, 0), kMaxAssoc - 1)];
-  if (A.polls && need && tid == 0 && !built && !(ci == 0 && A.first_ready) &&
+  // first_ready: the host joined the bulk stream before this launch, so every pass before it is
+  // complete (epochs ≤ A.seq), published or not — the launch's second chunk needs the pass just
+  // before the launch, whose epoch the flush that issued it did not publish (waiting for a later
+  // epoch instead held that chunk until this launch's first pass: ≈ 27 µs)
+  if (A.polls && need && tid == 0 && !built && !(A.first_ready && need <= A.seq) &&
       !epoch_wait_acquire(A.sync + kSyncSigma, need))
     atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)

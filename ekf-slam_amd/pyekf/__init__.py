@@ -249,6 +249,12 @@ class EKF:
                                      _dptr(rel_xy, torch.float64), _dptr(odom, torch.float64))
         _check(rc, "ekf_replay_device")
 
+    def replay_device_raw(self, T, M, counts, rel_xy, odom, ids, actions=0):
+        """ekf_replay_device on raw device addresses (ints: the same layouts as replay_device):
+        no tensor work on the caller's path (bench.py's timed region)."""
+        _check(lib().ekf_replay_device(self.h, T, M, counts, ids, actions or None, rel_xy, odom),
+               "ekf_replay_device")
+
     # fine-grained
     def predict(self, f=0):
         return lib().ekf_predict(self.h, f)

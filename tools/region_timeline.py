@@ -19,7 +19,8 @@ for r in csv.DictReader(open(glob.glob(d + "/*kernel_trace.csv")[0])):
         ks.append((a, b, r["Kernel_Name"].split("(")[0].split("::")[-1], r["Queue_Id"]))
 ks.sort()
 api = []
-for r in csv.DictReader(open(glob.glob(d + "/*hip_api_trace.csv")[0])):
+for r in (csv.DictReader(open(glob.glob(d + "/*hip_api_trace.csv")[0]))
+          if glob.glob(d + "/*hip_api_trace.csv") else []):
     a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     if b >= t0 and a <= t1:
         api.append((a, b, r["Function"]))
