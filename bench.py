@@ -510,9 +510,11 @@ def run(args, rank, world, local, backend=None):
     if backend is not None:
         ekf.sync()  # (a CPU stand-in backend: its own sync; on the GPU the device-wide sync below
     be.sync()       # waits for every stream of the library — ekf_replay has enqueued everything)
+    # this rank's own region (its K messages, enqueue to device-wide sync); the closing barrier
+    # aligns the ranks, and reduce_ranks takes the MAX of these over ranks
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     if trace:
         clk.append(("synced", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                     time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
@@ -548,9 +550,9 @@ def run(args, rank, world, local, backend=None):
         t1 = time.perf_counter()
         msgs(hs.start, hs.stop, host=True)
         be.sync()
+        el_h = time.perf_counter() - t1
         if world > 1:
             dist.barrier()
-        el_h = time.perf_counter() - t1
         live_h = np.arange(act.shape[2]) < counts[hs][..., None]
         corr_h = int(np.count_nonzero(live_h & (act[hs] != 2)))
         if world > 1:
