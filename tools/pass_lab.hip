@@ -16,7 +16,7 @@ using namespace ekfslam;
 // 1 Σ buffers chosen by the descriptor's parity (as the product: every load waits for it),
 // 2 no MFMA (one VALU product keeps the operand loads live), 4 constant operands (no operand loads),
 // 8 issue priority 2 once the MFMAs are done, 16 Σ_in loads issued before the operand loads
-enum { kDesc = 1, kNoMfma = 2, kNoOps = 4, kPrio = 8, kSigFirst = 16 };
+enum { kDesc = 1, kNoMfma = 2, kNoOps = 4, kPrio = 8, kSigFirst = 16, kStag1 = 32, kStag2 = 64, kStagW = 128 };
 template <int WPB, int MODE>
 __global__ __launch_bounds__(64 * WPB) void k_lab_region(PassArgs<float> A, int tcols) {
   using Tile = SigmaTile<float>;
@@ -32,6 +32,11 @@ __global__ __launch_bounds__(64 * WPB) void k_lab_region(PassArgs<float> A, int 
   if (tt >= (r1 - r0) * cw) return;
   const int tr = r0 + tt / cw, tc = c0 + tt % cw;
   const int R0 = tr * 32, C0 = tc * 32;
+  // stagger: odd workgroup rounds (or odd wave slots) start ≈ 0.5 / 1 µs late
+  if ((MODE & (kStag1 | kStag2)) && (((MODE & kStagW) ? (threadIdx.x >> 6) : (blockIdx.x >> 3)) & 1)) {
+    if (MODE & kStag1) __builtin_amdgcn_s_sleep(20);
+    else { __builtin_amdgcn_s_sleep(38); }
+  }
   int par = 0;
   if (MODE & kDesc) {
     if (!(d.flags & kActive)) return;
@@ -145,6 +150,142 @@ __global__ __launch_bounds__(256) void k_lab_lds(PassArgs<float> A, int bcols) {
 void launch_lds(const PassArgs<float>& a, hipStream_t s) {
   const int b = (a.n + 63) / 64;
   hipLaunchKernelGGL((k_lab_lds<0>), dim3(8 * region_tiles(b, b)), dim3(256), 0, s, a, b);
+}
+
+// 2 × 2 tile blocks per workgroup (wave w: tile (2·br + (w >> 1), 2·bc + (w & 1))): each K slice
+// is read by two waves of one CU and each M slice by two (L1 reuse) instead of one K slice by four
+// waves and four M slices. BAR: an LDS-only barrier between the operand loads and the Σ_in loads,
+// so the workgroup's operand requests go out ahead of its Σ traffic.
+template <bool BAR>
+__global__ __launch_bounds__(256) void k_lab_2x2(PassArgs<float> A, int bcols) {
+  using Tile = SigmaTile<float>;
+  const MsgDesc& d = A.desc[0];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = A.n;
+  const int brows = (n + 63) / 64;
+  const int x = blockIdx.x & 7, bb = blockIdx.x >> 3;
+  const int hx = x / kRegCols, qx = x % kRegCols;
+  const int r0 = hx * brows / kRegRows, r1 = (hx + 1) * brows / kRegRows;
+  const int c0 = qx * bcols / kRegCols, c1 = (qx + 1) * bcols / kRegCols;
+  const int cw = c1 - c0;
+  if (bb >= (r1 - r0) * cw) return;
+  const int br = r0 + bb / cw, bc = c0 + bb % cw;
+  const int R0 = br * 64 + 32 * (wv >> 1), C0 = bc * 64 + 32 * (wv & 1);
+  const bool live = R0 < n && C0 < n;
+  F32TileRegs g;
+  if (live) Tile::load_ops(g, A.kcat, A.mcat, n, A.ldk, R0, C0, lane);
+  if (BAR) lds_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (!live) return;
+  Tile::load_sig(g, A.sig[0], n, A.ld, R0, C0, lane);
+  const int kw = ((2 + 2 * d.m + 3) / 4) * 4;
+  Tile::finish(g, A.sig[1], n, A.ld, kw, (d.flags & kFirst) != 0, A.q, R0, C0, lane);
+}
+template <bool BAR>
+void launch_2x2(const PassArgs<float>& a, hipStream_t s) {
+  const int b = (a.n + 63) / 64;
+  hipLaunchKernelGGL((k_lab_2x2<BAR>), dim3(8 * region_tiles(b, b)), dim3(256), 0, s, a, b);
+}
+
+// Generic tile placement: a wave computes a 32 × 32·TJ block (TJ accumulators sharing the K
+// operand); a workgroup's WPB waves are placed WR tile-rows × (WPB / WR) block-columns; workgroups
+// dealt over the product's 2 × 4 XCD regions of the workgroup grid.
+template <int TJ, int WPB, int WR>
+__global__ __launch_bounds__(64 * WPB) void k_lab_gen(PassArgs<float> A, int gcols) {
+  using Tile = SigmaTile<float>;
+  constexpr int WC = WPB / WR;
+  const MsgDesc& d = A.desc[0];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const int grows = (n + 32 * WR - 1) / (32 * WR);
+  const int x = blockIdx.x & 7, bb = blockIdx.x >> 3;
+  const int hx = x / kRegCols, qx = x % kRegCols;
+  const int r0 = hx * grows / kRegRows, r1 = (hx + 1) * grows / kRegRows;
+  const int c0 = qx * gcols / kRegCols, c1 = (qx + 1) * gcols / kRegCols;
+  const int cw = c1 - c0;
+  if (bb >= (r1 - r0) * cw) return;
+  const int gr = r0 + bb / cw, gc = c0 + bb % cw;
+  const int R0 = gr * 32 * WR + 32 * (wv / WC), Cb = gc * 32 * TJ * WC + 32 * TJ * (wv % WC);
+  if (R0 >= n || Cb >= n) return;
+  const int kw = ((2 + 2 * d.m + 3) / 4) * 4;
+  const bool first = (d.flags & kFirst) != 0;
+  const int kr = lane >> 5, kcol = lane & 31;
+  const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 4u;
+  const auto rk = buf_rsrc(A.kcat, kbytes), rm = buf_rsrc(A.mcat, kbytes);
+  const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 4u;
+  const unsigned kstep = 2u * ldk * 4u;
+  float a[kSteps], b[TJ][kSteps], sv[TJ][16];
+#pragma unroll
+  for (int s2 = 0; s2 < kSteps; ++s2) a[s2] = ld_f32(rk, ko, s2 * kstep);
+#pragma unroll
+  for (int tj = 0; tj < TJ; ++tj) {
+    const unsigned mo = static_cast<unsigned>(kr * ldk + min(Cb + 32 * tj + kcol, n - 1)) * 4u;
+#pragma unroll
+    for (int s2 = 0; s2 < kSteps; ++s2) b[tj][s2] = ld_f32(rm, mo, s2 * kstep);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const auto rin = Tile::panel(A.sig[0], n, ld, R0), rout = Tile::panel(A.sig[1], n, ld, R0);
+  const unsigned rstride = static_cast<unsigned>(ld) * 4u;
+  unsigned so[TJ];
+#pragma unroll
+  for (int tj = 0; tj < TJ; ++tj) {
+    so[tj] = Tile::soff(n, ld, Cb + 32 * tj, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[tj][r] = ld_f32(rin, so[tj] + ((r & 3) + 8 * (r >> 2)) * rstride, 0);
+  }
+  const float q = static_cast<float>(A.q);
+#pragma unroll
+  for (int tj = 0; tj < TJ; ++tj) {
+    f16v acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int s2 = 0; s2 < kSteps; ++s2) {
+      const bool live = 2 * s2 < kw;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(live ? a[s2] : 0.0f, live ? b[tj][s2] : 0.0f, acc, 0, 0, 0);
+    }
+    const int col = Cb + 32 * tj + kcol;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
+      float v = sv[tj][r] - acc[r];
+      if (first && row == col && row < 3) v += q;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout,
+                                            so[tj] + ((r & 3) + 8 * (r >> 2)) * rstride, 0, 0);
+    }
+  }
+}
+template <int TJ, int WPB, int WR>
+void launch_gen(const PassArgs<float>& a, hipStream_t s) {
+  constexpr int WC = WPB / WR;
+  const int grows = (a.n + 32 * WR - 1) / (32 * WR), gcols = (a.n + 32 * TJ * WC - 1) / (32 * TJ * WC);
+  hipLaunchKernelGGL((k_lab_gen<TJ, WPB, WR>), dim3(8 * region_tiles(grows, gcols)), dim3(64 * WPB), 0, s, a, gcols);
+}
+
+// XCD row bands: XCD x (blocks L ≡ x mod 8) takes tiles [x·T/8, (x+1)·T/8) of the row-major tile
+// grid, WPB consecutive tiles per workgroup: every XCD gets the same tile count (±1), its L2 holds
+// Mcat whole and an eighth of Kcat.
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_lab_band(PassArgs<float> A, int tcols) {
+  using Tile = SigmaTile<float>;
+  const MsgDesc& d = A.desc[0];
+  const int lane = threadIdx.x & 63;
+  const int trows = (A.n + 31) / 32, T = trows * tcols;
+  const int x = blockIdx.x & 7;
+  const int t0 = x * T / 8, t1 = (x + 1) * T / 8;
+  const int t = __builtin_amdgcn_readfirstlane(t0 + (blockIdx.x >> 3) * WPB + (threadIdx.x >> 6));
+  if (t >= t1) return;
+  const int tr = t / tcols, tc = t - tr * tcols;
+  const int kw = ((2 + 2 * d.m + 3) / 4) * 4;
+  F32TileRegs g;
+  Tile::load(g, A.sig[0], A.kcat, A.mcat, A.n, A.ld, A.ldk, tr * 32, tc * 32, lane);
+  Tile::finish(g, A.sig[1], A.n, A.ld, kw, (d.flags & kFirst) != 0, A.q, tr * 32, tc * 32, lane);
+}
+template <int WPB>
+void launch_band(const PassArgs<float>& a, hipStream_t s) {
+  const int tr = (a.n + 31) / 32, T = tr * tr;
+  const int per = (T + 7) / 8;
+  hipLaunchKernelGGL((k_lab_band<WPB>), dim3(8 * ((per + WPB - 1) / WPB)), dim3(64 * WPB), 0, s, a, tr);
 }
 
 // 4 × 4 transpose of v[0..3] across each lane quad: afterwards lane j of a quad holds in v[i] what
@@ -356,14 +497,10 @@ int main(int argc, char** argv) {
   for (int round = 0; round < 2; ++round) {
     time_it("product k_sigma_pass", prod);
     time_it("region wpb4", [&](hipStream_t st) { launch_region<4, 0>(a, st); });
-    time_it("region desc", [&](hipStream_t st) { launch_region<4, kDesc>(a, st); });
-    time_it("region nomfma", [&](hipStream_t st) { launch_region<4, kNoMfma>(a, st); });
-    time_it("region noops", [&](hipStream_t st) { launch_region<4, kNoOps>(a, st); });
-    time_it("region nomfma noops", [&](hipStream_t st) { launch_region<4, kNoOps | kNoMfma>(a, st); });
-    time_it("region prio", [&](hipStream_t st) { launch_region<4, kPrio>(a, st); });
-    time_it("region sigfirst", [&](hipStream_t st) { launch_region<4, kSigFirst>(a, st); });
-    time_it("x4 stores", [&](hipStream_t st) { launch_x4<4, false>(a, st); });
-    time_it("lds operands", [&](hipStream_t st) { launch_lds(a, st); });
+    time_it("stagger wg 0.5us", [&](hipStream_t st) { launch_region<4, kStag1>(a, st); });
+    time_it("stagger wg 1us", [&](hipStream_t st) { launch_region<4, kStag2>(a, st); });
+    time_it("stagger wave 0.5us", [&](hipStream_t st) { launch_region<4, kStag1 | kStagW>(a, st); });
+    time_it("stagger wave 1us", [&](hipStream_t st) { launch_region<4, kStag2 | kStagW>(a, st); });
   }
   return 0;
 }
