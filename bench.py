@@ -338,6 +338,11 @@ class HipBackend:
         self.torch = torch
         self.EKF = pyekf.EKF
         self.F32, self.F64 = pyekf.EKF_F32, pyekf.EKF_F64
+        if os.environ.get("EKF_BENCH_SHARE_GPU") == "1":
+            # dev rehearsal of the N > 1 path on a one-GPU box: every rank on the GPUs there are,
+            # the rank reductions over gloo (RCCL wants one GPU per rank)
+            local = local % torch.cuda.device_count()
+            self.dist_backend, self.device = "gloo", "cpu"
         self.local = local
         torch.cuda.set_device(local)
 
@@ -401,6 +406,7 @@ def run(args, rank, world, local, backend=None):
         traffic, traffic_err = pmc_traffic(args)  # child runs, before this process uses the GPU
     import torch.distributed as dist
     be = backend if backend is not None else HipBackend(local)
+    local = getattr(be, "local", local)  # (EKF_BENCH_SHARE_GPU: the GPU this rank shares)
     if world > 1:
         dist.init_process_group(be.dist_backend)
     dtype = be.F32 if dt == "f32" else be.F64
