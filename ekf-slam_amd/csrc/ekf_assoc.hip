@@ -50,8 +50,8 @@ namespace ekfslam {
 __device__ unsigned long long g_am_stamps[2][kMaxChunk + 1][8];
 #define AM_STAMP(c, i)                                                                    \
   do {                                                                                    \
-    if (blockIdx.y == 0 && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
-      g_am_stamps[blockIdx.x == 0 ? 0 : 1][c][i] = __builtin_amdgcn_s_memrealtime();      \
+    if (blockIdx.y == 0 && threadIdx.x == 0 && (g == 0 || g == G - 1))                    \
+      g_am_stamps[g == 0 ? 0 : 1][c][i] = __builtin_amdgcn_s_memrealtime();               \
   } while (0)
 #else
 #define AM_STAMP(c, i) \
@@ -114,38 +114,85 @@ __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long lon
   return __hip_atomic_load((const gu64*)(p), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ double ld_sc1_f64(const double* p) {
-  return __longlong_as_double(static_cast<long long>(
-      ld_sc1_u64(reinterpret_cast<const unsigned long long*>(p))));
+
+// Coherence of what a filter's G workgroups exchange within a launch (granules, tables):
+//  - agent mode (any placement): stores write through past the XCD's L2 (sc1) and loads miss it
+//    (sc1) — every hand-off is a round trip through the fabric;
+//  - XCD-local mode (all G workgroups on one XCD, established by `same_xcd` at the launch's start):
+//    stores stop in that XCD's L2 (the CU's L1 is write-through) and loads take sc0 (they miss the
+//    CU's L1 and hit the L2 the workgroups share) — one L2 round trip. The kernel boundaries (L2
+//    write-back at the end, invalidate at the start) order launches of either mode.
+// Loads go through a buffer descriptor of the filter's table (wave-uniform) with the entry's byte
+// offset per lane.
+constexpr int kAuxSc0 = 1, kAuxSc1 = 16;
+__device__ __forceinline__ unsigned long long ld_x64(__amdgpu_buffer_rsrc_t r, unsigned off,
+                                                     bool loc) {
+  const auto v = loc ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc0)
+                     : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1);
+  return __builtin_bit_cast(unsigned long long, v);
+}
+__device__ __forceinline__ double ld_xf64(__amdgpu_buffer_rsrc_t r, unsigned off, bool loc) {
+  return __longlong_as_double(static_cast<long long>(ld_x64(r, off, loc)));
+}
+__device__ __forceinline__ void st_x64(unsigned long long* p, unsigned long long v, bool loc) {
+  if (loc)
+    __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-byte table store: write-through past L2 (agent mode) or into the shared L2 (local mode)
+template <bool LOC>
+__device__ __forceinline__ void st_x2(__amdgpu_buffer_rsrc_t r, int off, double a, double b) {
+  if (LOC) {
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4, make_double2(a, b)), r, off, 0, 0);
+  } else {
+    st_wt2(r, off, a, b);
+  }
 }
 
 // This lane's rows of the write-through tables. The buffer descriptor is built from the
 // workgroup's block of 64 rows (wave-uniform, so it stays in SGPRs); the lane's row is the voffset.
 // (A per-lane descriptor made hipcc wrap every store in a 64-iteration waterfall loop: ≈ 30 µs per
 // step.)
-__device__ __forceinline__ void put_cur(AmCur* blk, int lane, const double (&kk)[4],
-                                        const double (&kp)[6], const double (&pk)[6],
-                                        const double (&xk)[2]) {
+template <bool LOC>
+__device__ __forceinline__ void put_cur_m(AmCur* blk, int lane, const double (&kk)[4],
+                                          const double (&kp)[6], const double (&pk)[6],
+                                          const double (&xk)[2]) {
   const auto r = buf_rsrc(blk, kAmSlots * sizeof(AmCur));
   const int o = lane * static_cast<int>(sizeof(AmCur));
-  st_wt2(r, o + 0, kk[0], kk[1]);
-  st_wt2(r, o + 16, kk[2], kk[3]);
-  st_wt2(r, o + 32, kp[0], kp[1]);
-  st_wt2(r, o + 48, kp[2], kp[3]);
-  st_wt2(r, o + 64, kp[4], kp[5]);
-  st_wt2(r, o + 80, pk[0], pk[1]);
-  st_wt2(r, o + 96, pk[2], pk[3]);
-  st_wt2(r, o + 112, pk[4], pk[5]);
-  st_wt2(r, o + 128, xk[0], xk[1]);
+  st_x2<LOC>(r, o + 0, kk[0], kk[1]);
+  st_x2<LOC>(r, o + 16, kk[2], kk[3]);
+  st_x2<LOC>(r, o + 32, kp[0], kp[1]);
+  st_x2<LOC>(r, o + 48, kp[2], kp[3]);
+  st_x2<LOC>(r, o + 64, kp[4], kp[5]);
+  st_x2<LOC>(r, o + 80, pk[0], pk[1]);
+  st_x2<LOC>(r, o + 96, pk[2], pk[3]);
+  st_x2<LOC>(r, o + 112, pk[4], pk[5]);
+  st_x2<LOC>(r, o + 128, xk[0], xk[1]);
 }
-__device__ __forceinline__ void put_hist(AmHist* blk, int lane, double k0, double k1, double k2,
-                                         double k3, double m0, double m1, double m2, double m3) {
+template <bool LOC>
+__device__ __forceinline__ void put_hist_m(AmHist* blk, int lane, double k0, double k1, double k2,
+                                           double k3, double m0, double m1, double m2, double m3) {
   const auto r = buf_rsrc(blk, kAmSlots * sizeof(AmHist));
   const int o = lane * static_cast<int>(sizeof(AmHist));
-  st_wt2(r, o + 0, k0, k1);
-  st_wt2(r, o + 16, k2, k3);
-  st_wt2(r, o + 32, m0, m1);
-  st_wt2(r, o + 48, m2, m3);
+  st_x2<LOC>(r, o + 0, k0, k1);
+  st_x2<LOC>(r, o + 16, k2, k3);
+  st_x2<LOC>(r, o + 32, m0, m1);
+  st_x2<LOC>(r, o + 48, m2, m3);
+}
+
+__device__ __forceinline__ void put_cur(AmCur* blk, int lane, const double (&kk)[4],
+                                        const double (&kp)[6], const double (&pk)[6],
+                                        const double (&xk)[2], bool loc) {
+  if (loc) put_cur_m<true>(blk, lane, kk, kp, pk, xk);
+  else put_cur_m<false>(blk, lane, kk, kp, pk, xk);
+}
+__device__ __forceinline__ void put_hist(AmHist* blk, int lane, double k0, double k1, double k2,
+                                         double k3, double m0, double m1, double m2, double m3,
+                                         bool loc) {
+  if (loc) put_hist_m<true>(blk, lane, k0, k1, k2, k3, m0, m1, m2, m3);
+  else put_hist_m<false>(blk, lane, k0, k1, k2, k3, m0, m1, m2, m3);
 }
 
 // wave argmin of (d, k): the smaller d, ties (and two +inf) to the lower k
@@ -166,32 +213,30 @@ __device__ __forceinline__ void wave_argmin(double& d, int& k) {
 // wave's write-through table stores have drained; lanes < G poll one workgroup's each. Returns the
 // filter-wide argmin (the same in every workgroup), or (inf, INT_MAX) and *timeout on a stuck poll.
 __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g, int c,
-                                         unsigned tag, double& d, int& k, bool* timeout) {
-  drain_stores();  // R1: this wave's sc1 table stores of the step are complete before its granule
+                                         unsigned tag, double& d, int& k, bool* timeout, bool loc) {
+  drain_stores();  // R1: this wave's table stores of the step are complete before its granule
   const int lane = threadIdx.x;
   unsigned long long* mine = gran + (static_cast<size_t>(c) * G + g) * 4;
   const unsigned long long hi = static_cast<unsigned long long>(tag) << 32;
   const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(d));
   if (lane == 0) {
-    __hip_atomic_store((gu64*)(mine + 0), hi | (bits & 0xffffffffull),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu64*)(mine + 1), hi | (bits >> 32), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu64*)(mine + 2), hi | static_cast<unsigned>(k),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_x64(mine + 0, hi | (bits & 0xffffffffull), loc);
+    st_x64(mine + 1, hi | (bits >> 32), loc);
+    st_x64(mine + 2, hi | static_cast<unsigned>(k), loc);
   }
+  const auto gr = buf_rsrc(gran, static_cast<unsigned>((kMaxChunk + 1) * G * 4 * 8));
   double od = INFINITY;
   int ok = INT_MAX;
   for (int base = 0; base < G; base += 64) {
     const int w = base + lane;
-    const unsigned long long* src = gran + (static_cast<size_t>(c) * G + (w < G ? w : 0)) * 4;
+    const unsigned src = static_cast<unsigned>(((c * G + (w < G ? w : 0)) * 4) * 8);
     for (unsigned spins = 0;; ++spins) {
       bool got = true;
       unsigned long long v0 = 0, v1 = 0, v2 = 0;
       if (w < G) {
-        v0 = ld_sc1_u64(src + 0);
-        v1 = ld_sc1_u64(src + 1);
-        v2 = ld_sc1_u64(src + 2);
+        v0 = ld_x64(gr, src + 0, loc);
+        v1 = ld_x64(gr, src + 8, loc);
+        v2 = ld_x64(gr, src + 16, loc);
         got = (v0 >> 32) == tag && (v1 >> 32) == tag && (v2 >> 32) == tag;
       }
       if (__all(got)) {
@@ -213,11 +258,47 @@ __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g,
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  // loads of the published tables come after the poll (sc1 loads: they bypass this CU's L1)
+  // loads of the published tables come after the poll (they bypass this CU's L1)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   wave_argmin(od, ok);
   d = od;
   k = ok;
+}
+
+// Roll call of a launch in XCD-local placement: every workgroup of the filter publishes its XCD
+// (HW_REG_XCC_ID) in word 3 of its step-0 granule, agent-coherent, and reads everyone's. The
+// exchanges run XCD-local only if all G workgroups sit on one XCD — the same answer in every
+// workgroup, so all take the same mode (on a timeout: agent mode, and the flag is raised).
+__device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, bool* timeout) {
+  const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) & 0xffffu;
+  const int lane = threadIdx.x;
+  if (lane == 0)
+    st_x64(gran + static_cast<size_t>(g) * 4 + 3,
+           (static_cast<unsigned long long>(tag) << 32) | xcc, false);
+  bool same = true;
+  for (int base = 0; base < G; base += 64) {
+    const int w = base + lane;
+    const unsigned long long* src = gran + static_cast<size_t>(w < G ? w : 0) * 4 + 3;
+    for (unsigned spins = 0;; ++spins) {
+      bool got = true;
+      unsigned long long v = 0;
+      if (w < G) {
+        v = ld_sc1_u64(src);
+        got = (v >> 32) == tag;
+      }
+      if (__all(got)) {
+        if (w < G) same = same && static_cast<unsigned>(v & 0xffffu) == xcc;
+        break;
+      }
+      if (spins >= kAmSpin) {
+        *timeout = true;
+        same = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return __all(same) != 0;
 }
 
 }  // namespace
@@ -225,7 +306,14 @@ __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g,
 template <typename T>
 __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B) {
   __shared__ AmShared sh;
-  const int g = blockIdx.x, G = B.G, fy = blockIdx.y;
+  const int G = B.G, fy = blockIdx.y;
+  // XCD-local placement (B.xcd): the grid has 8 blocks per workgroup; filter fy's workgroups are
+  // the blocks x ≡ fy (mod 8), which round-robin dispatch puts on one XCD (checked: same_xcd)
+  int g = blockIdx.x;
+  if (B.xcd) {
+    if ((g & 7) != (fy & 7)) return;
+    g >>= 3;
+  }
   const MsgDesc& d = A.desc[fy];
   const int flags = d.flags;
   if (!(flags & kActive)) return;  // (every workgroup of the filter)
@@ -250,6 +338,9 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   const unsigned tagbase = (A.seq & 0x07ffffffu) << 5;
   bool timeout = false;
   unsigned status = 0;
+  const bool loc = B.xcd && G > 1 && same_xcd(gran, G, g, tagbase | 31u, &timeout);
+  const auto cur_r = buf_rsrc(cur, static_cast<unsigned>(B.cur_stride * sizeof(AmCur)));
+  const auto hist_r = buf_rsrc(hist, static_cast<unsigned>(B.hist_stride * sizeof(AmHist)));
 
   // ---- predict (slam.cpp:321-335): the pose, At's two entries, the pose block (every lane) ----
   double pose[3], a1, a2;
@@ -277,7 +368,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   unsigned s = ctl->counter;
 
   // the state at the chunk's start, for the first step's exchange
-  if (valid && G > 1) put_cur(cur + g * kAmSlots, lane, kk, kp, pk, xk);
+  if (valid && G > 1) put_cur(cur + g * kAmSlots, lane, kk, kp, pk, xk, loc);
   bool any_new = false;
 
   AM_STAMP(kMaxChunk, 0);
@@ -311,7 +402,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     wave_argmin(key, kbest);
     AM_STAMP(c, 1);
     if (G > 1 && !full)
-      exchange(gran, G, g, c, tagbase | static_cast<unsigned>(c + 1), key, kbest, &timeout);
+      exchange(gran, G, g, c, tagbase | static_cast<unsigned>(c + 1), key, kbest, &timeout, loc);
     key = __longlong_as_double(static_cast<long long>(__builtin_amdgcn_readfirstlane(
               static_cast<int>(__double_as_longlong(key))) & 0xffffffffull) |
           (static_cast<long long>(__builtin_amdgcn_readfirstlane(
@@ -357,17 +448,16 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       }
       // ---- j's block, state and history (one round of sc1 loads), crosses from Σ_in ----
       double v[3];
-      const AmCur* jc = cur + static_cast<size_t>(c) * Np + j;
+      const unsigned jco = static_cast<unsigned>((c * Np + j) * sizeof(AmCur));
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int e = lane + 64 * i;  // 0..17: the AmCur fields; then 8 per earlier step
         v[i] = 0.0;
         if (G > 1 && e < 18) {
-          v[i] = ld_sc1_f64(&jc->kk[0] + e);
+          v[i] = ld_xf64(cur_r, jco + 8 * e, loc);
         } else if (G > 1 && e < 18 + 8 * c) {
-          const int cc = (e - 18) >> 3, t = (e - 18) & 7;
-          const AmHist* hh = hist + static_cast<size_t>(cc) * Np + j;
-          v[i] = ld_sc1_f64((t < 4 ? hh->k : hh->m) + (t & 3));
+          const int cc = (e - 18) >> 3, t = (e - 18) & 7;  // AmHist: k[4] then m[4]
+          v[i] = ld_xf64(hist_r, static_cast<unsigned>((cc * Np + j) * sizeof(AmHist) + 8 * t), loc);
         }
       }
       // Σ_in crosses of this lane's slot with j (no predict term between landmarks)
@@ -617,7 +707,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       }
       if (G > 1 && c + 1 < m)
         put_hist(hist + static_cast<size_t>(c) * Np + g * kAmSlots, lane, Kk[0][0], Kk[0][1],
-                 Kk[1][0], Kk[1][1], Mk[0][0], Mk[0][1], Mk[1][0], Mk[1][1]);
+                 Kk[1][0], Kk[1][1], Mk[0][0], Mk[0][1], Mk[1][0], Mk[1][1], loc);
     }
     if (g == 0 && lane < 3) {
 #pragma unroll
@@ -629,7 +719,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       }
     }
     if (valid && G > 1 && c + 1 < m)  // the slot's block and state as step c + 1 starts
-      put_cur(cur + static_cast<size_t>(c + 1) * Np + g * kAmSlots, lane, kk, kp, pk, xk);
+      put_cur(cur + static_cast<size_t>(c + 1) * Np + g * kAmSlots, lane, kk, kp, pk, xk, loc);
   }
 
   AM_STAMP(kMaxChunk, 1);
@@ -691,12 +781,12 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       put_hist(hist + static_cast<size_t>(m - 1) * Np + g * kAmSlots, lane, sh.hk[m - 1][0][lane],
                sh.hk[m - 1][1][lane], sh.hk[m - 1][2][lane], sh.hk[m - 1][3][lane],
                sh.hm[m - 1][0][lane], sh.hm[m - 1][1][lane], sh.hm[m - 1][2][lane],
-               sh.hm[m - 1][3][lane]);
-      put_cur(cur + static_cast<size_t>(m) * Np + g * kAmSlots, lane, kk, kp, pk, xk);
+               sh.hm[m - 1][3][lane], loc);
+      put_cur(cur + static_cast<size_t>(m) * Np + g * kAmSlots, lane, kk, kp, pk, xk, loc);
     }
     double dd = 0.0;
     int kd = 0;
-    exchange(gran, G, g, m, tagbase | static_cast<unsigned>(m + 1), dd, kd, &timeout);
+    exchange(gran, G, g, m, tagbase | static_cast<unsigned>(m + 1), dd, kd, &timeout, loc);
     if (timeout && lane == 0) atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
     if (g != 0) return;
   }
@@ -711,12 +801,13 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   if (G > 1) {
     for (int e = lane; e < m * 18; e += 64) {
       const int c = e / 18, t = e - c * 18;
-      sh.pb[c][t] = ld_sc1_f64(&cur[static_cast<size_t>(m) * Np + max(sh.jl[c], 0)].kk[0] + t);
+      sh.pb[c][t] = ld_xf64(
+          cur_r, static_cast<unsigned>((m * Np + max(sh.jl[c], 0)) * sizeof(AmCur) + 8 * t), loc);
     }
     for (int e = lane; e < m * m * 8; e += 64) {
       const int c = e / (8 * m), cc = (e >> 3) % m, t = e & 7;
-      const AmHist& hh = hist[static_cast<size_t>(cc) * Np + max(sh.jl[c], 0)];
-      const double v = ld_sc1_f64((t < 4 ? hh.k : hh.m) + (t & 3));
+      const double v = ld_xf64(
+          hist_r, static_cast<unsigned>((cc * Np + max(sh.jl[c], 0)) * sizeof(AmHist) + 8 * t), loc);
       __builtin_amdgcn_wave_barrier();  // every lane's loads issued before any lane overwrites
       ph[e] = v;
     }
@@ -807,7 +898,7 @@ namespace ekfslam {
 template <typename T>
 hipError_t launch_assoc_msg(const PassArgs<T>& a, const AmArgs& b, int nf, hipStream_t s,
                             hipEvent_t e0, hipEvent_t e1) {
-  const dim3 grid(b.G, nf);
+  const dim3 grid(b.xcd ? 8 * b.G : b.G, nf);
   if (e0 && e1)
     hipExtLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmSlots), 0, s, e0, e1, 0, a, b);
   else

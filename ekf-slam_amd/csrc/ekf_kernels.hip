@@ -287,18 +287,27 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
   // independent chains (f64 ALU vs LDS round trips) interleave in one basic block.
   double lx = 0.0, ly = 0.0, H0[5], H1[5], zhat[2], braw = 0.0;
   bool init = false, bok = true;
+  // the marker's measurement and skip flag, read one step ahead (the descriptor and the skip list
+  // are constant during the chunk): their LDS round trip stays off the step's dependent chain
+  const bool noinit = (d.flags & kNoInit) != 0;
+  double zn0 = 0.0, zn1 = 0.0;
+  int skn = 0;
+  if (m > 0) {
+    zn0 = d.z[0][0];
+    zn1 = d.z[0][1];
+    skn = sh.skip[0];
+  }
   auto geometry = [&](int c) {
     const int pj = 3 + 2 * c;
     const double pose[3] = {readlane_f64(xl, 0), readlane_f64(xl, 1), readlane_f64(xl, 2)};
     lx = readlane_f64(xl, pj);
     ly = readlane_f64(xl, pj + 1);
     init = false;
-    if (!sh.skip[c] && !(d.flags & kNoInit) && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216
+    if (!skn && !noinit && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216 (zn, skn: marker c)
       init = true;
       sh.any_init = 1;
-      const double z0 = d.z[c][0], z1 = d.z[c][1];
-      lx = pose[1] + z0 * cos(z1 + pose[0]);
-      ly = pose[2] + z0 * sin(z1 + pose[0]);
+      lx = pose[1] + zn0 * cos(zn1 + pose[0]);
+      ly = pose[2] + zn0 * sin(zn1 + pose[0]);
     }
     range_bearing(pose, lx, ly, zhat, H0, H1, &braw, &bok);
   };
@@ -307,8 +316,13 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
     const int pj = 3 + 2 * c, nx = pj + 2;
     const bool more = c + 1 < m;
     EKF_STAMP(64 + 8 * c);
-    const double z0 = d.z[c][0], z1 = d.z[c][1];
-    bool sk = sh.skip[c] != 0;
+    const double z0 = zn0, z1 = zn1;
+    bool sk = skn != 0;
+    if (more) {  // marker c + 1's, for geometry(c + 1) and the next step
+      zn0 = d.z[c + 1][0];
+      zn1 = d.z[c + 1][1];
+      skn = sh.skip[c + 1];
+    }
     double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0, Sm_keep[4];
     if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
     EKF_STAMP(65 + 8 * c);

@@ -79,7 +79,9 @@ struct AmArgs {
   unsigned long long* gran;
   size_t hist_stride, cur_stride, gran_stride;  // elements between filters
   int G;                                        // workgroups per filter
+  int xcd;  // XCD-local placement: 8 blocks per workgroup, a filter's G on one XCD (k_assoc_msg)
 };
+constexpr int kAmXcdMaxG = 32;  // largest G that takes the XCD-local placement
 // Scores, decides and corrects every marker of the chunk (slam.cpp:338-488) and writes the chunk's
 // Kcat / Mcat, the new state, t_map_odom and the decisions; the Σ pass then runs as for a known-id
 // chunk. One grid (G, n_filters) of 64-lane workgroups; a filter's G workgroups exchange each
