@@ -500,10 +500,11 @@ int ensure_am(ekf_ctx* h) {
   b.hist_stride = kMaxChunk * Np;
   b.cur_stride = (kMaxChunk + 1) * Np;
   b.gran_stride = static_cast<size_t>(kMaxChunk + 1) * G * 4;
-  {  // EKF_AM_XCD=1: the exchanges XCD-local when a filter's workgroups share an XCD. A filter's G workgroups must all be resident at once on that XCD (≈ 28 bulk-
-     // stream CUs × 2 workgroups of 68 KB LDS): only up to kAmXcdMaxG of them (N ≤ 2048).
-    const char* e = std::getenv("EKF_AM_XCD");  // (opt-in while its coherence is being measured)
-    b.xcd = G > 1 && G <= kAmXcdMaxG && e && std::atoi(e) != 0 ? 1 : 0;
+  {  // the exchanges XCD-local: a filter's workgroups placed on one XCD (EKF_AM_XCD=0: anywhere).
+     // Its G workgroups must all be resident at once there (≈ 28 bulk-stream CUs × 2 workgroups
+     // of 68 KB LDS): only up to kAmXcdMaxG of them (N ≤ 2048).
+    const char* e = std::getenv("EKF_AM_XCD");
+    b.xcd = G > 1 && G <= kAmXcdMaxG && !(e && std::atoi(e) == 0) ? 1 : 0;
   }
   if (hipMalloc(&b.hist, sizeof(AmHist) * b.hist_stride * F) != hipSuccess ||
       hipMalloc(&b.cur, sizeof(AmCur) * b.cur_stride * F) != hipSuccess ||

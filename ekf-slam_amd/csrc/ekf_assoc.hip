@@ -115,32 +115,35 @@ __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long lon
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Coherence of what a filter's G workgroups exchange within a launch (granules, tables):
-//  - agent mode (any placement): stores write through past the XCD's L2 (sc1) and loads miss it
-//    (sc1) — every hand-off is a round trip through the fabric;
+// Coherence of what a filter's G workgroups exchange within a launch (granules, tables). Loads are
+// sc1 in both modes: they miss the CU's L1 and read the XCD's L2 coherently. Stores:
+//  - agent mode (any placement): sc1, written through past the XCD's L2 to memory, where a reader
+//    on another XCD finds them;
 //  - XCD-local mode (all G workgroups on one XCD, established by `same_xcd` at the launch's start):
-//    stores stop in that XCD's L2 (the CU's L1 is write-through) and loads take sc0 (they miss the
-//    CU's L1 and hit the L2 the workgroups share) — one L2 round trip. The kernel boundaries (L2
-//    write-back at the end, invalidate at the start) order launches of either mode.
+//    plain, so they stop in the L2 the workgroups share (the CU's L1 is write-through).
+// Measured (tools/xcd_probe.hip, one-way hand-off between two CUs): same XCD, plain store + sc1
+// load 224 ns, sc1 store + sc1 load 414 ns; across XCDs sc1 + sc1 564 ns (plain stores are never
+// seen there); sc0 loads hit a stale L1 line forever. Every value a local-mode launch reads was
+// written in that launch by a CU of the same XCD, so a stale L2 line from an earlier launch is
+// never read (the granules carry the launch's tag).
 // Loads go through a buffer descriptor of the filter's table (wave-uniform) with the entry's byte
 // offset per lane.
-constexpr int kAuxSc0 = 1, kAuxSc1 = 16;
-__device__ __forceinline__ unsigned long long ld_x64(__amdgpu_buffer_rsrc_t r, unsigned off,
-                                                     bool loc) {
-  const auto v = loc ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc0)
-                     : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1);
-  return __builtin_bit_cast(unsigned long long, v);
+constexpr int kAuxSc1 = 16;
+__device__ __forceinline__ unsigned long long ld_x64(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(unsigned long long,
+                            __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxSc1));
 }
-__device__ __forceinline__ double ld_xf64(__amdgpu_buffer_rsrc_t r, unsigned off, bool loc) {
-  return __longlong_as_double(static_cast<long long>(ld_x64(r, off, loc)));
+__device__ __forceinline__ double ld_xf64(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __longlong_as_double(static_cast<long long>(ld_x64(r, off)));
 }
 __device__ __forceinline__ void st_x64(unsigned long long* p, unsigned long long v, bool loc) {
-  if (loc)
-    __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  typedef unsigned u2 __attribute__((ext_vector_type(2)));
+  if (loc)  // a plain store (no cache-policy bits), as the probe's
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), buf_rsrc(p, 8), 0, 0, 0);
   else
     __hip_atomic_store((gu64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// 16-byte table store: write-through past L2 (agent mode) or into the shared L2 (local mode)
+// 16-byte table store: write-through past L2 (agent mode) or into the shared L2 (XCD-local)
 template <bool LOC>
 __device__ __forceinline__ void st_x2(__amdgpu_buffer_rsrc_t r, int off, double a, double b) {
   if (LOC) {
@@ -234,9 +237,9 @@ __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g,
       bool got = true;
       unsigned long long v0 = 0, v1 = 0, v2 = 0;
       if (w < G) {
-        v0 = ld_x64(gr, src + 0, loc);
-        v1 = ld_x64(gr, src + 8, loc);
-        v2 = ld_x64(gr, src + 16, loc);
+        v0 = ld_x64(gr, src + 0);
+        v1 = ld_x64(gr, src + 8);
+        v2 = ld_x64(gr, src + 16);
         got = (v0 >> 32) == tag && (v1 >> 32) == tag && (v2 >> 32) == tag;
       }
       if (__all(got)) {
@@ -258,7 +261,7 @@ __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g,
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  // loads of the published tables come after the poll (they bypass this CU's L1)
+  // loads of the published tables come after the poll (sc1: they bypass this CU's L1)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   wave_argmin(od, ok);
   d = od;
@@ -454,10 +457,10 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
         const int e = lane + 64 * i;  // 0..17: the AmCur fields; then 8 per earlier step
         v[i] = 0.0;
         if (G > 1 && e < 18) {
-          v[i] = ld_xf64(cur_r, jco + 8 * e, loc);
+          v[i] = ld_xf64(cur_r, jco + 8 * e);
         } else if (G > 1 && e < 18 + 8 * c) {
           const int cc = (e - 18) >> 3, t = (e - 18) & 7;  // AmHist: k[4] then m[4]
-          v[i] = ld_xf64(hist_r, static_cast<unsigned>((cc * Np + j) * sizeof(AmHist) + 8 * t), loc);
+          v[i] = ld_xf64(hist_r, static_cast<unsigned>((cc * Np + j) * sizeof(AmHist) + 8 * t));
         }
       }
       // Σ_in crosses of this lane's slot with j (no predict term between landmarks)
@@ -802,12 +805,12 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     for (int e = lane; e < m * 18; e += 64) {
       const int c = e / 18, t = e - c * 18;
       sh.pb[c][t] = ld_xf64(
-          cur_r, static_cast<unsigned>((m * Np + max(sh.jl[c], 0)) * sizeof(AmCur) + 8 * t), loc);
+          cur_r, static_cast<unsigned>((m * Np + max(sh.jl[c], 0)) * sizeof(AmCur) + 8 * t));
     }
     for (int e = lane; e < m * m * 8; e += 64) {
       const int c = e / (8 * m), cc = (e >> 3) % m, t = e & 7;
       const double v = ld_xf64(
-          hist_r, static_cast<unsigned>((cc * Np + max(sh.jl[c], 0)) * sizeof(AmHist) + 8 * t), loc);
+          hist_r, static_cast<unsigned>((cc * Np + max(sh.jl[c], 0)) * sizeof(AmHist) + 8 * t));
       __builtin_amdgcn_wave_barrier();  // every lane's loads issued before any lane overwrites
       ph[e] = v;
     }

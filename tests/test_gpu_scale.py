@@ -350,12 +350,16 @@ def test_association_at_scale_decisions(known_map):
 def test_association_at_scale_schedules_bit_identical(known_map, monkeypatch):
     """Unknown association on the pipeline under the three schedules — device epochs (k_assoc
     polls the last Σ pass's epoch), HIP events (the main stream joins the bulk stream before each
-    k_assoc) and one stream: the same decisions and bit-identical state."""
+    k_assoc) and one stream — and k_assoc_msg's two exchange transports (agent-coherent, and
+    XCD-local: the filter's 8 workgroups on one XCD, EKF_AM_XCD): the same decisions and
+    bit-identical state."""
     sc, odom, ws = known_map
     w = sc.n_warm
     out = []
-    for env in ({"EKF_DEVSYNC": "1"}, {"EKF_DEVSYNC": "0"}, {"EKF_SERIAL": "1"}):
-        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
+    for env in ({"EKF_DEVSYNC": "1", "EKF_AM_XCD": "0"}, {"EKF_DEVSYNC": "0", "EKF_AM_XCD": "0"},
+                {"EKF_SERIAL": "1", "EKF_AM_XCD": "0"}, {"EKF_DEVSYNC": "1", "EKF_AM_XCD": "1"},
+                {"EKF_SERIAL": "1", "EKF_AM_XCD": "1"}):
+        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_AM_XCD"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
