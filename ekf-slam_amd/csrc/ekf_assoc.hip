@@ -198,37 +198,6 @@ __device__ __forceinline__ void put_hist(AmHist* blk, int lane, double k0, doubl
   else put_hist_m<false>(blk, lane, k0, k1, k2, k3, m0, m1, m2, m3);
 }
 
-// wave argmin of (d, k): the smaller d, ties (and two +inf) to the lower k. A strict total order
-// on the pairs, so any reduction tree gives the same pair: DPP row shifts 1, 2, 4, 8 (lane 15 of
-// each row holds its row's minimum), row_bcast15 / row_bcast31 (lane 63 holds the wave's), then a
-// broadcast — six steps of three 32-bit DPP moves instead of six rounds of three ds_bpermutes. A
-// lane whose DPP source lies outside its row (or whose row the step masks off) combines with
-// itself.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ void argmin_dpp(double& d, int& k) {
-  const long long b = __double_as_longlong(d);
-  const int lo = static_cast<int>(b), hi = static_cast<int>(b >> 32);
-  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWS, 0xf, false);
-  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWS, 0xf, false);
-  const int ok = __builtin_amdgcn_update_dpp(k, k, CTRL, ROWS, 0xf, false);
-  const double od = __longlong_as_double(static_cast<long long>(
-      (static_cast<unsigned long long>(static_cast<unsigned>(ohi)) << 32) | static_cast<unsigned>(olo)));
-  if (od < d || (od == d && ok < k)) {
-    d = od;
-    k = ok;
-  }
-}
-__device__ __forceinline__ void wave_argmin(double& d, int& k) {
-  argmin_dpp<0x111, 0xf>(d, k);  // row_shr:1
-  argmin_dpp<0x112, 0xf>(d, k);  // row_shr:2
-  argmin_dpp<0x114, 0xf>(d, k);  // row_shr:4
-  argmin_dpp<0x118, 0xf>(d, k);  // row_shr:8
-  argmin_dpp<0x142, 0xa>(d, k);  // row_bcast:15 into rows 1, 3
-  argmin_dpp<0x143, 0xc>(d, k);  // row_bcast:31 into rows 2, 3
-  d = readlane_f64(d, 63);
-  k = __builtin_amdgcn_readlane(k, 63);
-}
-
 // The G workgroups of a filter publish their (d, k) for exchange `c` and wait for everyone's:
 // three 8-byte {tag, value} granules per workgroup (d's two halves, k), stored by lane 0 after the
 // wave's write-through table stores have drained; lanes < G poll one workgroup's each. Returns the

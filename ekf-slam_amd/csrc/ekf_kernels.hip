@@ -2336,15 +2336,7 @@ __global__ __launch_bounds__(kAssocThreads) void k_assoc(PassArgs<T> A) {
       bestk = static_cast<int>(k);
     }
   }
-  // wave argmin (64 lanes), ties → lower index
-  for (int off = 32; off > 0; off >>= 1) {
-    const double od = __shfl_xor(bestd, off, 64);
-    const int ok = __shfl_xor(bestk, off, 64);
-    if (od < bestd || (od == bestd && ok < bestk)) {
-      bestd = od;
-      bestk = ok;
-    }
-  }
+  wave_argmin(bestd, bestk);  // 64 lanes, ties → lower index (DPP, ekf_math.hpp)
   const int wv = tid >> 6;
   if ((tid & 63) == 0) {
     s_bd[wv] = bestd;

@@ -171,4 +171,35 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
+// wave argmin of (d, k): the smaller d, ties (and two +inf) to the lower k. A strict total order
+// on the pairs, so any reduction tree gives the same pair: DPP row shifts 1, 2, 4, 8 (lane 15 of
+// each row holds its row's minimum), row_bcast15 / row_bcast31 (lane 63 holds the wave's), then a
+// broadcast — six steps of three 32-bit DPP moves instead of six rounds of three ds_bpermutes. A
+// lane whose DPP source lies outside its row (or whose row the step masks off) combines with
+// itself. Every lane of the wave must be active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void argmin_dpp(double& d, int& k) {
+  const long long b = __double_as_longlong(d);
+  const int lo = static_cast<int>(b), hi = static_cast<int>(b >> 32);
+  const int olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWS, 0xf, false);
+  const int ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWS, 0xf, false);
+  const int ok = __builtin_amdgcn_update_dpp(k, k, CTRL, ROWS, 0xf, false);
+  const double od = __longlong_as_double(static_cast<long long>(
+      (static_cast<unsigned long long>(static_cast<unsigned>(ohi)) << 32) | static_cast<unsigned>(olo)));
+  if (od < d || (od == d && ok < k)) {
+    d = od;
+    k = ok;
+  }
+}
+__device__ __forceinline__ void wave_argmin(double& d, int& k) {
+  argmin_dpp<0x111, 0xf>(d, k);  // row_shr:1
+  argmin_dpp<0x112, 0xf>(d, k);  // row_shr:2
+  argmin_dpp<0x114, 0xf>(d, k);  // row_shr:4
+  argmin_dpp<0x118, 0xf>(d, k);  // row_shr:8
+  argmin_dpp<0x142, 0xa>(d, k);  // row_bcast:15 into rows 1, 3
+  argmin_dpp<0x143, 0xc>(d, k);  // row_bcast:31 into rows 2, 3
+  d = readlane_f64(d, 63);
+  k = __builtin_amdgcn_readlane(k, 63);
+}
+
 }  // namespace ekfslam

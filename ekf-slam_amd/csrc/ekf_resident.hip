@@ -514,18 +514,7 @@ __global__ __launch_bounds__(W * 64) void k_resident(PassArgs<double> A, const P
                 bestk = static_cast<int>(k);
               }
             }
-            // butterfly over the live lanes only: for off ≥ counter every live lane's partner
-            // (ℓ + off ≥ counter) holds no landmark, so those steps are skipped (uniform branch)
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-              if (off >= static_cast<int>(counter)) continue;
-              const double od = __shfl_xor(bestd, off, 64);
-              const int ok = __shfl_xor(bestk, off, 64);
-              if (od < bestd || (od == bestd && ok < bestk)) {
-                bestd = od;
-                bestk = ok;
-              }
-            }
+            wave_argmin(bestd, bestk);  // (DPP, ekf_math.hpp; every lane holds the result)
             if (lane == 0) {
               // the new slot (d = gate, slam.cpp:406-408) wins only over a larger minimum
               const bool nw = !(bestd <= A.gate);
