@@ -376,6 +376,43 @@ def test_association_at_scale_schedules_bit_identical(known_map, monkeypatch):
         np.testing.assert_array_equal(o[1], out[0][1])
 
 
+@pytest.mark.parametrize("nf", [3, 9], ids=["3filters", "9filters"])
+def test_association_at_scale_many_filters_xcd_placement(known_map, nf, monkeypatch):
+    """k_assoc_msg with several filters: filter f's 8 workgroups are placed on XCD f mod 8 (with 9
+    filters two share an XCD). The same messages to every filter from the same state, XCD-local and
+    agent-coherent exchanges: every filter's state bit-identical across both and filters, equal to
+    the oracle's."""
+    sc, odom, ws = known_map
+    w = sc.n_warm
+    sl = slice(w, sc.n_messages)
+    x, S, tmo, cnt = ws
+    out = []
+    for xcd in ("1", "0"):
+        monkeypatch.setenv("EKF_AM_XCD", xcd)
+        e = pyekf.EKF(n_landmarks=512, n_filters=nf)
+        for f in range(nf):
+            e.set_state(x, S, tmo=tmo, counter=cnt, f=f)
+        T = sc.n_messages - w
+        rep = lambda a: np.repeat(a[sl, None], nf, axis=1)  # noqa: E731
+        e.replay(rep(sc.count), rep(sc.rel), rep(odom), ids=None, actions=rep(sc.actions),
+                 assoc=True)
+        assert T > 0 and all(e.status(f) == 0 for f in range(nf))
+        out.append([e.state(f) for f in range(nf)])
+        e.close()
+    ref = _oracle_from(ws, 512)
+    for t in range(w, sc.n_messages):
+        ref.set_odom(odom[t])
+        ref.sensor_cb(sc.rel[t, :int(sc.count[t])])
+    xr, Sr, _, cr = ref.get()
+    for st in out:
+        for xg, Sg, cg in st:
+            np.testing.assert_array_equal(xg, out[0][0][0])
+            np.testing.assert_array_equal(Sg, out[0][0][1])
+            assert cg == cr
+    assert np.abs(out[0][0][0] - xr).max() < POSE_TOL
+    assert np.abs(out[0][0][1] - Sr).max() < SIGMA_TOL
+
+
 def test_association_at_scale_batched_replay(known_map):
     """The same messages through ekf_replay(assoc=1) (decisions on the device, no host round
     trip), from the same state: the final state equals the oracle's."""
