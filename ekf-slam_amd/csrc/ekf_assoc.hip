@@ -64,8 +64,8 @@ namespace {
 constexpr unsigned kAmSpin = 1u << 22;  // bounded granule polls (EKF_FLAG_TIMEOUT)
 
 struct AmShared {
-  double hk[kMaxChunk][4][kAmSlots];  // this wave's K_c[k], by lane
-  double hm[kMaxChunk][4][kAmSlots];  // this wave's M_c[:, k], by lane
+  alignas(16) double hkm[kMaxChunk][kAmSlots][8];  // this wave's K_c[k] (0..3) and M_c[:, k] (4..7), by lane:
+                                       // a lane's step in 64 contiguous bytes (ds_read_b128 × 4)
   double jh[kMaxChunk][8];            // the step's landmark: K (0..3) and M (4..7) of every step
   double jc[18];                      // its block and state (AmCur, x included)
   double pb[kMaxChunk][18];           // fp32 patch: every marker's landmark's final block
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
         }
         for (int e = lane; e < 8 * c; e += 64) {
           const int cc = e >> 3, t = e & 7;
-          sh.jh[cc][t] = t < 4 ? sh.hk[cc][t][lj] : sh.hm[cc][t - 4][lj];
+          sh.jh[cc][t] = sh.hkm[cc][lj][t];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -517,10 +517,10 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
         auto term = [&](int cc, double (&acc)[8]) __attribute__((always_inline)) {
           const double* jk = sh.jh[cc];
           const double* jm = sh.jh[cc] + 4;
-          const double ok0 = sh.hk[cc][0][lane], ok1 = sh.hk[cc][1][lane];
-          const double ok2 = sh.hk[cc][2][lane], ok3 = sh.hk[cc][3][lane];
-          const double om0 = sh.hm[cc][0][lane], om1 = sh.hm[cc][1][lane];
-          const double om2 = sh.hm[cc][2][lane], om3 = sh.hm[cc][3][lane];
+          const double2* hl = reinterpret_cast<const double2*>(sh.hkm[cc][lane]);
+          const double2 q0 = hl[0], q1 = hl[1], q2 = hl[2], q3 = hl[3];  // ds_read_b128 × 4
+          const double ok0 = q0.x, ok1 = q0.y, ok2 = q1.x, ok3 = q1.y;
+          const double om0 = q2.x, om1 = q2.y, om2 = q3.x, om3 = q3.y;
           acc[0] = fma(ok1, jm[2], fma(ok0, jm[0], acc[0]));
           acc[1] = fma(ok1, jm[3], fma(ok0, jm[1], acc[1]));
           acc[2] = fma(ok3, jm[2], fma(ok2, jm[0], acc[2]));
@@ -679,14 +679,13 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     }
     AM_STAMP(c, 4);
     // ---- the step's factors: history (LDS + write-through table), Kcat / Mcat rows ----
-    sh.hk[c][0][lane] = Kk[0][0];
-    sh.hk[c][1][lane] = Kk[0][1];
-    sh.hk[c][2][lane] = Kk[1][0];
-    sh.hk[c][3][lane] = Kk[1][1];
-    sh.hm[c][0][lane] = Mk[0][0];
-    sh.hm[c][1][lane] = Mk[0][1];
-    sh.hm[c][2][lane] = Mk[1][0];
-    sh.hm[c][3][lane] = Mk[1][1];
+    {
+      double2* hl = reinterpret_cast<double2*>(sh.hkm[c][lane]);
+      hl[0] = make_double2(Kk[0][0], Kk[0][1]);
+      hl[1] = make_double2(Kk[1][0], Kk[1][1]);
+      hl[2] = make_double2(Mk[0][0], Mk[0][1]);
+      hl[3] = make_double2(Mk[1][0], Mk[1][1]);
+    }
     if (valid) {
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -768,10 +767,9 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   }
   if (G > 1) {  // the final blocks (cur[m]) and every history row published; then workgroup 0 only
     if (valid) {
-      put_hist(hist + static_cast<size_t>(m - 1) * Np + g * kAmSlots, lane, sh.hk[m - 1][0][lane],
-               sh.hk[m - 1][1][lane], sh.hk[m - 1][2][lane], sh.hk[m - 1][3][lane],
-               sh.hm[m - 1][0][lane], sh.hm[m - 1][1][lane], sh.hm[m - 1][2][lane],
-               sh.hm[m - 1][3][lane], loc);
+      const double* hl = sh.hkm[m - 1][lane];
+      put_hist(hist + static_cast<size_t>(m - 1) * Np + g * kAmSlots, lane, hl[0], hl[1], hl[2],
+               hl[3], hl[4], hl[5], hl[6], hl[7], loc);
       put_cur(cur + static_cast<size_t>(m) * Np + g * kAmSlots, lane, kk, kp, pk, xk, loc);
     }
     double dd = 0.0;
@@ -787,7 +785,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   const int nu = 3 + 2 * m;
-  double* ph = &sh.hk[0][0][0];  // G > 1: [m][m][8] ≤ 2 048 doubles (the hk region holds 4 096)
+  double* ph = &sh.hkm[0][0][0];  // G > 1: [m][m][8] ≤ 2 048 doubles (the region holds 8 192)
   if (G > 1) {
     for (int e = lane; e < m * 18; e += 64) {
       const int c = e / 18, t = e - c * 18;
@@ -832,7 +830,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   auto hv = [&](int c, int cc, int t) -> double {
     if (G > 1) return ph[(c * m + cc) * 8 + t];
     const int j = max(sh.jl[c], 0);
-    return t < 4 ? sh.hk[cc][t][j] : sh.hm[cc][t - 4][j];
+    return sh.hkm[cc][j][t];
   };
   for (int e = lane; e < nu * nu; e += 64) {
     const int a = e / nu, b = e - a * nu;
