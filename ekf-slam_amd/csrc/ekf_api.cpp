@@ -68,6 +68,10 @@ struct ekf_ctx {
   bool epoch_owed = false;       // the last Σ pass published no device epoch (the flush's last
                                  // launch: the next flush joins the bulk stream on the host)
   AmArgs am{};                   // k_assoc_msg scratch (allocated at the first association chunk)
+  int am_route = 0;              // unknown association: EKF_ASSOC_* (fixed at ekf_create)
+  int bulk_cus_per_xcd = 0;      // CUs the bulk stream may use on each XCD
+  unsigned* fatal_h = nullptr;   // host-mapped: a device poll timed out (EKF_E_TIMEOUT)
+  unsigned* fatal_d = nullptr;   // its device address (PassArgs::fatal)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
   hipEvent_t ev_join = nullptr;           // bulk → main: everything issued so far
   bool devsync = false;                   // streams synchronise through device epochs
@@ -147,6 +151,7 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.rows = static_cast<T*>(h->rows);
   a.rows_stride = static_cast<size_t>(h->ldk) * kRowW;
   a.sync = h->sync;
+  a.fatal = h->fatal_d;
   a.desc = desc;
   a.n = h->n;
   a.ld = h->ld;
@@ -315,12 +320,14 @@ constexpr int kCuSplitMaxFilters = 32;
 int create_streams(ekf_ctx* h) {
   int split = h->F <= kCuSplitMaxFilters ? kCuSplit : 0;
   if (const char* e = std::getenv("EKF_CU_SPLIT")) split = std::atoi(e);
-  hipDeviceProp_t prop;
   int cus = 0;
-  if (split > 0 && hipGetDeviceProperties(&prop, h->cfg.device) == hipSuccess)
-    cus = prop.multiProcessorCount;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->cfg.device) !=
+      hipSuccess)
+    cus = 0;
   constexpr int kXcd = 8;
+  h->bulk_cus_per_xcd = cus / kXcd;
   if (split > 0 && cus % kXcd == 0 && split * kXcd < cus) {
+    h->bulk_cus_per_xcd = cus / kXcd - split;
     const int words = (cus + 31) / 32;
     std::vector<uint32_t> mmain(words, 0), mbulk(words, 0);
     for (int b = 0; b < cus; ++b) (b < split * kXcd ? mmain : mbulk)[b / 32] |= 1u << (b % 32);
@@ -490,6 +497,22 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
   }
 }
 
+// Which path unknown association takes (EKF_ASSOC_*). k_assoc_msg's G workgroups per filter spin
+// on each other's granules, so all G must be resident at once on the CUs the bulk stream may use.
+// Workgroups are dispatched in order, block b on XCD b mod 8, and a filter's blocks come before the
+// next filter's on every XCD, so the earliest unfinished filter is always whole: progress needs G
+// workgroups on one XCD (XCD-local placement) or ⌈G / 8⌉ on each (agent placement), whatever the
+// number of filters. Beyond that the markers go one per launch (k_assoc + a launch pair).
+int am_route(ekf_ctx* h) {
+  if (h->resident || !h->assoc_msg) return EKF_ASSOC_MARKER;
+  const int G = (h->cfg.n_landmarks + kAmSlots - 1) / kAmSlots;
+  const int per_xcd = assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32) * h->bulk_cus_per_xcd;
+  const char* e = std::getenv("EKF_AM_XCD");  // EKF_AM_XCD=0: the agent placement only
+  if (G > 1 && G <= per_xcd && !(e && std::atoi(e) == 0)) return EKF_ASSOC_CHUNK_XCD;
+  if ((G + 7) / 8 <= per_xcd) return EKF_ASSOC_CHUNK;
+  return EKF_ASSOC_MARKER;
+}
+
 // k_assoc_msg's tables and granules for every filter (once; zeroed so no stale tag matches)
 int ensure_am(ekf_ctx* h) {
   if (h->am.hist) return EKF_OK;
@@ -500,21 +523,25 @@ int ensure_am(ekf_ctx* h) {
   b.hist_stride = kMaxChunk * Np;
   b.cur_stride = (kMaxChunk + 1) * Np;
   b.gran_stride = static_cast<size_t>(kMaxChunk + 1) * G * 4;
-  {  // the exchanges XCD-local: a filter's workgroups placed on one XCD (EKF_AM_XCD=0: anywhere).
-     // Its G workgroups must all be resident at once there (≈ 28 bulk-stream CUs × 2 workgroups
-     // of 68 KB LDS): only up to kAmXcdMaxG of them (N ≤ 2048).
-    const char* e = std::getenv("EKF_AM_XCD");
-    b.xcd = G > 1 && G <= kAmXcdMaxG && !(e && std::atoi(e) == 0) ? 1 : 0;
-  }
+  b.xcd = h->am_route == EKF_ASSOC_CHUNK_XCD ? 1 : 0;
+  b.spin = 1u << 22;  // ≈ 0.1 s of polls per exchange
+  if (const char* e = std::getenv("EKF_AM_SPIN_LOG2")) b.spin = 1u << std::min(std::atoi(e), 30);
+  if (const char* e = std::getenv("EKF_AM_DROP")) b.drop = std::atoi(e) != 0 ? 1 : 0;
+  auto release = [&]() {
+    if (b.hist) hipFree(b.hist);
+    if (b.cur) hipFree(b.cur);
+    if (b.gran) hipFree(b.gran);
+  };
   if (hipMalloc(&b.hist, sizeof(AmHist) * b.hist_stride * F) != hipSuccess ||
       hipMalloc(&b.cur, sizeof(AmCur) * b.cur_stride * F) != hipSuccess ||
       hipMalloc(&b.gran, sizeof(unsigned long long) * b.gran_stride * F) != hipSuccess) {
-    if (b.hist) hipFree(b.hist);
-    if (b.cur) hipFree(b.cur);
+    release();
     return EKF_E_NOMEM;
   }
-  if (hipMemset(b.gran, 0, sizeof(unsigned long long) * b.gran_stride * F) != hipSuccess)
+  if (hipMemset(b.gran, 0, sizeof(unsigned long long) * b.gran_stride * F) != hipSuccess) {
+    release();
     return EKF_E_HIP;
+  }
   h->am = b;
   return EKF_OK;
 }
@@ -564,10 +591,11 @@ void plan_assoc_msg(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, in
 }
 
 // Route unknown association: whole chunks through k_assoc_msg on the HBM pipeline (simple form);
-// the resident path, the Joseph form and EKF_ASSOC_MSG=0 take one marker per launch.
+// the resident path, the Joseph form, EKF_ASSOC_MSG=0 and maps too large for the bulk stream's
+// CUs to hold a filter's workgroups at once (am_route) take one marker per launch.
 void plan_unknown(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0, int i1,
                   const char* absent = nullptr) {
-  if (!h->resident && !h->joseph && h->assoc_msg)
+  if (!h->joseph && h->am_route != EKF_ASSOC_MARKER)
     plan_assoc_msg(h, f0, nf, predict, posterior, i0, i1, absent);
   else
     plan_assoc(h, f0, nf, predict, posterior, i0, i1, absent);
@@ -623,22 +651,28 @@ int posterior_launch(ekf_ctx* h, const MsgDesc* dp, int f0, int nf) {
   return e == hipSuccess ? EKF_OK : EKF_E_HIP;
 }
 
-// Upload capacity for `need` descriptors: the device buffer and EVERY pinned ring slot grow together
-// (geometrically), so an allocation happens the first time a plan this large is seen, never on a
-// later same-sized call that lands on a ring slot not used before (a hipHostMalloc costs ≈ 120 µs,
-// a device re-allocation a drain: round 3 measured both inside a 20-message bench region).
+// Upload capacity for `need` descriptors. The device buffer grows geometrically (a re-allocation
+// drains both streams). The pinned ring — host-planned uploads only, so ekf_replay_device never
+// grows it — grows EVERY slot together, so an allocation happens the first time a plan this large
+// is seen, never on a later same-sized call that lands on a ring slot not used before (a
+// hipHostMalloc costs ≈ 120 µs, a device re-allocation a drain: round 3 measured both inside a
+// 20-message bench region). Host plans are flushed every kFlushDesc descriptors (plus one
+// message), which bounds the ring.
 constexpr size_t kDescInit = 256;  // descriptors at creation (×F/64 for wide handles)
+int reserve_device(ekf_ctx* h, size_t need) {
+  if (need <= h->ddesc_cap) return EKF_OK;
+  if (drain(h)) return EKF_E_HIP;  // the previous launch may still read the old buffer
+  if (h->ddesc) HIPCHK(hipFree(h->ddesc));
+  h->ddesc = nullptr;
+  const size_t cap = std::max(need, 2 * h->ddesc_cap);
+  if (hipMalloc(&h->ddesc, cap * sizeof(MsgDesc)) != hipSuccess) return EKF_E_NOMEM;
+  h->ddesc_cap = cap;
+  return EKF_OK;
+}
 int reserve_upload(ekf_ctx* h, size_t need) {
-  if (need > h->ddesc_cap) {  // the previous launch may still read the old buffer
-    if (drain(h)) return EKF_E_HIP;
-    if (h->ddesc) HIPCHK(hipFree(h->ddesc));
-    h->ddesc = nullptr;
-    const size_t cap = std::max(need, 2 * h->ddesc_cap);
-    if (hipMalloc(&h->ddesc, cap * sizeof(MsgDesc)) != hipSuccess) return EKF_E_NOMEM;
-    h->ddesc_cap = cap;
-  }
+  if (int rc = reserve_device(h, need)) return rc;
   if (need > h->ring_cap || !h->ring[0].p) {
-    const size_t cap = std::max(need, std::max(h->ring_cap, h->ddesc_cap));
+    const size_t cap = std::max(need, std::min(2 * h->ring_cap, h->ddesc_cap));
     for (StageSlot& sl : h->ring) {
       if (sl.used) HIPCHK(hipEventSynchronize(sl.ev));
       if (sl.p) HIPCHK(hipHostFree(sl.p));
@@ -803,6 +837,15 @@ int settle(ekf_ctx* h) {
   return adopt_device_plan(h);
 }
 
+// After a drain: did a device poll of this handle time out since the last report? Reported once
+// (EKF_E_TIMEOUT); which filters it hit stays in their status (EKF_FLAG_TIMEOUT).
+int take_fatal(ekf_ctx* h) {
+  volatile unsigned* p = h->fatal_h;
+  if (!p || *p == 0) return EKF_OK;
+  *p = 0;
+  return EKF_E_TIMEOUT;
+}
+
 // Association with the decisions read back (synchronous), kMaxAssoc markers per upload.
 int assoc_sync(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int m_max, int* j_out,
                int* new_out) {
@@ -952,6 +995,9 @@ const char* ekf_strerror(int s) {
     case EKF_E_NUMERIC: return "singular or non-finite innovation covariance";
     case EKF_E_HIP: return "HIP runtime error";
     case EKF_E_NOMEM: return "out of memory";
+    case EKF_E_TIMEOUT:
+      return "a device hand-off timed out: the state of the filters flagged EKF_FLAG_TIMEOUT is "
+             "undefined (ekf_reset / ekf_set_state them)";
     default: return "unknown status";
   }
 }
@@ -1002,6 +1048,13 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
       hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_sig[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_sig[1], hipEventDisableTiming) != hipSuccess)
+    return fail(EKF_E_HIP);
+  h->am_route = am_route(h);
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->fatal_h), 64,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return fail(EKF_E_NOMEM);
+  *h->fatal_h = 0;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&h->fatal_d), h->fatal_h, 0) != hipSuccess)
     return fail(EKF_E_HIP);
   const size_t sig_bytes = h->sig_stride * h->F * h->w;
   for (int p = 0; p < 2; ++p) {
@@ -1081,6 +1134,7 @@ int ekf_destroy(ekf_t h) {
   for (PlanState* p : h->dstate)
     if (p) hipFree(p);
   if (h->hstate) hipHostFree(h->hstate);
+  if (h->fatal_h) hipHostFree(h->fatal_h);
   if (h->am.hist) hipFree(h->am.hist);
   if (h->am.cur) hipFree(h->am.cur);
   if (h->am.gran) hipFree(h->am.gran);
@@ -1167,6 +1221,7 @@ int ekf_sensor(ekf_t h, int f, int m, const double* rel_xy, int* assoc_out, int*
   {
     unsigned fl = 0;
     if (drain(h)) return EKF_E_HIP;
+    if (int t = take_fatal(h)) return t;
     HIPCHK(hipMemcpy(&fl, &h->ctl[f].status, sizeof(unsigned), hipMemcpyDeviceToHost));
     if (fl & EKF_FLAG_RANGE) return EKF_E_RANGE;
   }
@@ -1253,7 +1308,7 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
                       hipHostMallocDefault) != hipSuccess)
       return EKF_E_NOMEM;
   }
-  if (int rc = reserve_upload(h, static_cast<size_t>(T) * F)) return rc;
+  if (int rc = reserve_device(h, static_cast<size_t>(T) * F)) return rc;  // (no host staging)
   // the bulk stream may still read the last descriptors (an idle one reads nothing: no hop)
   if (hipStreamQuery(h->bulk) != hipSuccess && join_bulk(h)) return EKF_E_HIP;
   if (!h->dev_plan) {  // the host mirror goes down once; later device replays chain on the device
@@ -1342,6 +1397,7 @@ int ekf_associate_correct(ekf_t h, int f, double rx, double ry, int* j, int* is_
   int jj = -1, nn = 0;
   const int rc = assoc_sync(h, f, 1, false, false, 1, &jj, &nn);
   if (rc) return rc;
+  if (int t = take_fatal(h)) return t;  // (assoc_sync drained)
   if (j) *j = jj;
   if (is_new) *is_new = nn;
   if (jj < 0) return EKF_E_RANGE;
@@ -1363,7 +1419,14 @@ int ekf_posterior(ekf_t h, int f) {
 
 int ekf_sync(ekf_t h) {
   if (!h) return EKF_E_ARG;
-  return settle(h);
+  if (int rc = settle(h)) return rc;
+  return take_fatal(h);
+}
+
+int ekf_get_assoc_route(ekf_t h, int* route) {
+  if (!h || !route) return EKF_E_ARG;
+  *route = h->am_route;
+  return EKF_OK;
 }
 
 int ekf_set_joseph(ekf_t h, int on) {

@@ -61,7 +61,6 @@ __device__ unsigned long long g_am_stamps[2][kMaxChunk + 1][8];
 
 namespace {
 
-constexpr unsigned kAmSpin = 1u << 22;  // bounded granule polls (EKF_FLAG_TIMEOUT)
 
 struct AmShared {
   alignas(16) double hkm[kMaxChunk][kAmSlots][8];  // this wave's K_c[k] (0..3) and M_c[:, k] (4..7), by lane:
@@ -201,15 +200,18 @@ __device__ __forceinline__ void put_hist(AmHist* blk, int lane, double k0, doubl
 // The G workgroups of a filter publish their (d, k) for exchange `c` and wait for everyone's:
 // three 8-byte {tag, value} granules per workgroup (d's two halves, k), stored by lane 0 after the
 // wave's write-through table stores have drained; lanes < G poll one workgroup's each. Returns the
-// filter-wide argmin (the same in every workgroup), or (inf, INT_MAX) and *timeout on a stuck poll.
+// filter-wide argmin (the same in every workgroup), or a partial argmin and *timeout after `spin`
+// polls — the filter's state is then undefined (EKF_FLAG_TIMEOUT, reported by the host as
+// EKF_E_TIMEOUT). `drop`: fault injection, this workgroup does not publish (tests only).
 __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g, int c,
-                                         unsigned tag, double& d, int& k, bool* timeout, bool loc) {
+                                         unsigned tag, double& d, int& k, bool* timeout, bool loc,
+                                         unsigned spin, bool drop = false) {
   drain_stores();  // R1: this wave's table stores of the step are complete before its granule
   const int lane = threadIdx.x;
   unsigned long long* mine = gran + (static_cast<size_t>(c) * G + g) * 4;
   const unsigned long long hi = static_cast<unsigned long long>(tag) << 32;
   const unsigned long long bits = static_cast<unsigned long long>(__double_as_longlong(d));
-  if (lane == 0) {
+  if (lane == 0 && !drop) {
     st_x64(mine + 0, hi | (bits & 0xffffffffull), loc);
     st_x64(mine + 1, hi | (bits >> 32), loc);
     st_x64(mine + 2, hi | static_cast<unsigned>(k), loc);
@@ -241,7 +243,7 @@ __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g,
         }
         break;
       }
-      if (spins >= kAmSpin) {
+      if (spins >= spin) {
         *timeout = true;
         break;
       }
@@ -256,15 +258,30 @@ __device__ __forceinline__ void exchange(unsigned long long* gran, int G, int g,
 }
 
 // Roll call of a launch in XCD-local placement: every workgroup of the filter publishes its XCD
-// (HW_REG_XCC_ID) in word 3 of its step-0 granule, agent-coherent, and reads everyone's. The
-// exchanges run XCD-local only if all G workgroups sit on one XCD — the same answer in every
-// workgroup, so all take the same mode (on a timeout: agent mode, and the flag is raised).
-__device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, bool* timeout) {
+// (HW_REG_XCC_ID) in word 3 of its step-0 granule, agent-coherent; workgroup 0 reads all G and
+// publishes the launch's transport in word 3 of its step-1 granule (unused by the exchanges), and
+// every other workgroup takes that one decision. XCD-local only if all G sit on one XCD; so every
+// workgroup runs the same transport, also when a poll times out (workgroup 0 then publishes the
+// agent transport; a workgroup that never sees the decision takes it too, and the timeout is
+// flagged: EKF_FLAG_TIMEOUT, the filter's state is undefined).
+__device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, bool* timeout,
+                         unsigned spin) {
   const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) & 0xffffu;
   const int lane = threadIdx.x;
-  if (lane == 0)
-    st_x64(gran + static_cast<size_t>(g) * 4 + 3,
-           (static_cast<unsigned long long>(tag) << 32) | xcc, false);
+  const unsigned long long hi = static_cast<unsigned long long>(tag) << 32;
+  unsigned long long* decision = gran + static_cast<size_t>(G) * 4 + 3;  // (c = 1, g = 0) word 3
+  if (lane == 0) st_x64(gran + static_cast<size_t>(g) * 4 + 3, hi | xcc, false);
+  if (g != 0) {
+    for (unsigned spins = 0;; ++spins) {
+      const unsigned long long v = ld_sc1_u64(decision);
+      if ((v >> 32) == tag) return (v & 1ull) != 0;  // (the same address in every lane: uniform)
+      if (spins >= spin) {
+        *timeout = true;
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
   bool same = true;
   for (int base = 0; base < G; base += 64) {
     const int w = base + lane;
@@ -280,7 +297,7 @@ __device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, b
         if (w < G) same = same && static_cast<unsigned>(v & 0xffffu) == xcc;
         break;
       }
-      if (spins >= kAmSpin) {
+      if (spins >= spin) {
         *timeout = true;
         same = false;
         break;
@@ -288,7 +305,9 @@ __device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, b
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  return __all(same) != 0;
+  const bool all = __all(same) != 0;
+  if (lane == 0) st_x64(decision, hi | (all ? 1ull : 0ull), false);
+  return all;
 }
 
 }  // namespace
@@ -328,7 +347,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   const unsigned tagbase = (A.seq & 0x07ffffffu) << 5;
   bool timeout = false;
   unsigned status = 0;
-  const bool loc = B.xcd && G > 1 && same_xcd(gran, G, g, tagbase | 31u, &timeout);
+  const bool loc = B.xcd && G > 1 && same_xcd(gran, G, g, tagbase | 31u, &timeout, B.spin);
   const auto cur_r = buf_rsrc(cur, static_cast<unsigned>(B.cur_stride * sizeof(AmCur)));
   const auto hist_r = buf_rsrc(hist, static_cast<unsigned>(B.hist_stride * sizeof(AmHist)));
 
@@ -392,7 +411,8 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     wave_argmin(key, kbest);
     AM_STAMP(c, 1);
     if (G > 1 && !full)
-      exchange(gran, G, g, c, tagbase | static_cast<unsigned>(c + 1), key, kbest, &timeout, loc);
+      exchange(gran, G, g, c, tagbase | static_cast<unsigned>(c + 1), key, kbest, &timeout, loc,
+               B.spin, B.drop && c == 0 && g == G - 1);
     key = __longlong_as_double(static_cast<long long>(__builtin_amdgcn_readfirstlane(
               static_cast<int>(__double_as_longlong(key))) & 0xffffffffull) |
           (static_cast<long long>(__builtin_amdgcn_readfirstlane(
@@ -754,8 +774,8 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       ctl->tmo[2] = tmo.y;
     }
   }
-  if (lane == 0 && (status || timeout) && (g == 0 || timeout))
-    atomicOr(&ctl->status, (g == 0 ? status : 0u) | (timeout ? EKF_FLAG_TIMEOUT_D : 0u));
+  if (lane == 0 && g == 0 && status) atomicOr(&ctl->status, status);
+  if (lane == 0 && timeout) flag_timeout(&ctl->status, A.fatal);
 
   // ---- fp32 Σ: the final Σ[U, U] in fp64 over the pass's block when a landmark was committed
   // (k_patch_stage; its first sighting cancels 1e7 − (1e7 − δ) in fp32) ----
@@ -774,8 +794,9 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     }
     double dd = 0.0;
     int kd = 0;
-    exchange(gran, G, g, m, tagbase | static_cast<unsigned>(m + 1), dd, kd, &timeout, loc);
-    if (timeout && lane == 0) atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+    bool late = false;
+    exchange(gran, G, g, m, tagbase | static_cast<unsigned>(m + 1), dd, kd, &late, loc, B.spin);
+    if (late && lane == 0) flag_timeout(&ctl->status, A.fatal);
     if (g != 0) return;
   }
   // workgroup 0: U = {θ, x, y, jx, jy per marker} (a skipped marker maps onto θ: never a first
@@ -892,6 +913,14 @@ hipError_t launch_assoc_msg(const PassArgs<T>& a, const AmArgs& b, int nf, hipSt
   else
     hipLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmSlots), 0, s, a, b);
   return hipGetLastError();
+}
+
+int assoc_msg_blocks_per_cu(bool f32) {
+  int nb = 0;
+  const hipError_t e =
+      f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<float>, kAmSlots, 0)
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<double>, kAmSlots, 0);
+  return e == hipSuccess ? nb : 0;
 }
 
 template hipError_t launch_assoc_msg<double>(const PassArgs<double>&, const AmArgs&, int,

@@ -796,7 +796,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // epoch instead held that chunk until this launch's first pass: ≈ 27 µs)
   if (A.polls && need && tid == 0 && !built && !(A.first_ready && need <= A.seq) &&
       !epoch_wait_acquire(A.sync + kSyncSigma, need))
-    atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+    flag_timeout(&ctl->status, A.fatal);
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
   if (tid == 0) sh.status = 0;
   __syncthreads();
@@ -1657,7 +1657,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
   // the chain of this chunk runs on the other stream: wait for its record
   if (tid < 64) sh.pos64[tid] = kMaxU;
   if (A.polls && tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
-    atomicOr(&A.ctl[f].status, EKF_FLAG_TIMEOUT_D);
+    flag_timeout(&A.ctl[f].status, A.fatal);
   drain_stores();
   __syncthreads();
   {  // the record into LDS: every load of a thread issued before its first LDS store
@@ -2272,7 +2272,7 @@ __global__ __launch_bounds__(kAssocThreads) void k_assoc(PassArgs<T> A) {
   // device epochs: Σ_in and x are the last Σ pass's (bulk stream), its epoch A.need_sigma
   if (A.polls && A.need_sigma) {
     if (tid == 0 && !epoch_wait_acquire(A.sync + kSyncSigma, A.need_sigma))
-      atomicOr(&ctl->status, EKF_FLAG_TIMEOUT_D);
+      flag_timeout(&ctl->status, A.fatal);
     __syncthreads();
   }
   const unsigned s = ctl->counter;

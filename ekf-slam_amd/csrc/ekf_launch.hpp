@@ -28,6 +28,7 @@ struct PassArgs {
   size_t rec_stride;
   StageRec<T>* stage;   // [2][rec_stride]: rebuild operands staged for a kLook chain (kStageIn)
   unsigned* sync;       // device epochs (ekf_device.hpp kSync*)
+  unsigned* fatal;      // host-mapped word: set when any poll of the handle timed out (flag_timeout)
   unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
   unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
   unsigned pub_sigma;   // factors: publish this Σ-pass epoch first (the previous chunk's pass, 0 = none)
@@ -80,8 +81,15 @@ struct AmArgs {
   size_t hist_stride, cur_stride, gran_stride;  // elements between filters
   int G;                                        // workgroups per filter
   int xcd;  // XCD-local placement: 8 blocks per workgroup, a filter's G on one XCD (k_assoc_msg)
+  unsigned spin;  // bounded polls per exchange (EKF_FLAG_TIMEOUT beyond; EKF_AM_SPIN_LOG2)
+  int drop;       // fault injection (EKF_AM_DROP=1, tests only): the last workgroup never
+                  // publishes its first exchange, so every workgroup's poll times out
 };
-constexpr int kAmXcdMaxG = 32;  // largest G that takes the XCD-local placement
+// Workgroups of k_assoc_msg one CU holds at once (its LDS bounds it), for the co-residency check:
+// a filter's G workgroups spin on each other, so all of them must fit the bulk stream's CUs
+// (per XCD in the XCD-local placement) at once, or the host routes the markers through the
+// one-marker-per-launch path instead (ekf_api.cpp am_route).
+int assoc_msg_blocks_per_cu(bool f32);
 // Scores, decides and corrects every marker of the chunk (slam.cpp:338-488) and writes the chunk's
 // Kcat / Mcat, the new state, t_map_odom and the decisions; the Σ pass then runs as for a known-id
 // chunk. One grid (G, n_filters) of 64-lane workgroups; a filter's G workgroups exchange each

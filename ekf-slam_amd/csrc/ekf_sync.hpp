@@ -30,6 +30,14 @@ __device__ __noinline__ bool epoch_wait_acquire(const unsigned* p, unsigned v) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return ok;
 }
+// A poll that timed out leaves the filter's state undefined (a hand-off was not seen): its status
+// gets EKF_FLAG_TIMEOUT and the handle's host-mapped fatal word is set, which the host reports as
+// EKF_E_TIMEOUT at its next synchronising call (a vector store of a constant to system scope: no RMW
+// across PCIe).
+__device__ __forceinline__ void flag_timeout(unsigned* status, unsigned* fatal) {
+  atomicOr(status, EKF_FLAG_TIMEOUT_D);
+  if (fatal) __hip_atomic_store(fatal, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // write-through stores of hand-off payload
 __device__ __forceinline__ void st_wt(double* p, double v) {

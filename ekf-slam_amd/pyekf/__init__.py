@@ -16,7 +16,9 @@ LIB_PATH = os.path.join(PKG_DIR, os.environ.get("EKF_LIB", "libekfslam.so"))
 
 EKF_OK, EKF_E_ARG, EKF_E_RANGE, EKF_E_EMPTY, EKF_E_NUMERIC, EKF_E_HIP, EKF_E_NOMEM = \
     0, -1, -2, -3, -4, -5, -6
-EKF_FLAG_RANGE, EKF_FLAG_NUMERIC = 1, 2
+EKF_E_TIMEOUT = -7
+EKF_FLAG_RANGE, EKF_FLAG_NUMERIC, EKF_FLAG_TIMEOUT = 1, 2, 4
+EKF_ASSOC_MARKER, EKF_ASSOC_CHUNK, EKF_ASSOC_CHUNK_XCD = 0, 1, 2
 EKF_F64, EKF_F32 = 0, 1
 EKF_PATH_PIPELINE, EKF_PATH_RESIDENT = 0, 1
 ADD, DELETE = 0, 2
@@ -25,6 +27,7 @@ SOURCE_SIM, SOURCE_ASSOC = 0, 1
 # every symbol include/ekf.h and include/slam_core.h declare
 EXPORTS = [
     "ekf_config_default", "ekf_strerror", "ekf_create", "ekf_destroy", "ekf_dims", "ekf_get_path",
+    "ekf_get_assoc_route",
     "ekf_set_odom",
     "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_replay_device",
     "ekf_predict",
@@ -83,6 +86,7 @@ def lib():
             "ekf_destroy": (_i, [_vp]),
             "ekf_dims": (_i, [_vp, _ip, _ip, _ip]),
             "ekf_get_path": (_i, [_vp, _ip]),
+            "ekf_get_assoc_route": (_i, [_vp, _ip]),
             "ekf_set_odom": (_i, [_vp, _i, _d, _d, _d]),
             "ekf_fake_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
             "ekf_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
@@ -192,6 +196,8 @@ class EKF:
         p = C.c_int()
         _check(lib().ekf_get_path(self.h, C.byref(p)), "ekf_get_path")
         self.path = p.value  # EKF_PATH_PIPELINE | EKF_PATH_RESIDENT
+        _check(lib().ekf_get_assoc_route(self.h, C.byref(p)), "ekf_get_assoc_route")
+        self.assoc_route = p.value  # EKF_ASSOC_*
 
     def close(self):
         if getattr(self, "h", None):

@@ -27,10 +27,18 @@ extern "C" {
 #define EKF_E_NUMERIC (-4) /* singular or non-finite innovation covariance S (slam.cpp:252) */
 #define EKF_E_HIP (-5)     /* HIP runtime error */
 #define EKF_E_NOMEM (-6)
+#define EKF_E_TIMEOUT (-7) /* a device hand-off (cross-stream epoch or k_assoc_msg's exchange
+                              between a filter's workgroups) was not seen within its bounded poll:
+                              the flagged filters' state after that message is undefined. Reported
+                              once by the next ekf_sync / ekf_sensor / ekf_associate_correct;
+                              ekf_get_status names the filters (EKF_FLAG_TIMEOUT). No reference
+                              counterpart (the reference has no device). */
 
 /* status flag bits (ekf_get_status), accumulated on the device */
-#define EKF_FLAG_RANGE 1u
-#define EKF_FLAG_NUMERIC 2u
+#define EKF_FLAG_RANGE 1u   /* a marker was skipped: id >= N / map full (slam.cpp:213, :351) */
+#define EKF_FLAG_NUMERIC 2u /* a marker was skipped: S singular or non-finite (slam.cpp:252) */
+#define EKF_FLAG_TIMEOUT 4u /* a device poll timed out: this filter's state is undefined
+                               (EKF_E_TIMEOUT) */
 
 #define EKF_F64 0
 #define EKF_F32 1 /* Σ stored and contracted in fp32; state and all O(n) math stay fp64 */
@@ -74,6 +82,19 @@ int ekf_dims(ekf_t h, int* n, int* ld, int* n_filters);
 #define EKF_PATH_RESIDENT 1
 #define EKF_RESIDENT_MAX_N 128
 int ekf_get_path(ekf_t h, int* path);
+
+/* How unknown association (ekf_sensor, ekf_associate_correct, assoc replays) runs on the pipeline
+ * (fixed at ekf_create; same decisions either way, slam.cpp:344-440):
+ *   EKF_ASSOC_CHUNK_XCD  a chunk of <= EKF_MAX_CHUNK markers per launch, one workgroup per 64
+ *                        landmark slots, a filter's workgroups on one XCD exchanging through its L2;
+ *   EKF_ASSOC_CHUNK      the same kernel with the workgroups anywhere (agent-coherent exchange;
+ *                        EKF_AM_XCD=0 forces it);
+ *   EKF_ASSOC_MARKER     one marker per launch (resident path, Joseph form, EKF_ASSOC_MSG=0, or a
+ *                        map whose ceil(N/64) workgroups the CUs cannot hold at once). */
+#define EKF_ASSOC_MARKER 0
+#define EKF_ASSOC_CHUNK 1
+#define EKF_ASSOC_CHUNK_XCD 2
+int ekf_get_assoc_route(ekf_t h, int* route);
 
 /* ---- the callbacks (fast path) ---- */
 
@@ -150,6 +171,8 @@ int ekf_defer(ekf_t h, int on);
 int ekf_reset(ekf_t h, int filter);
 
 /* ---- state access (synchronising) ---- */
+/* Waits for everything submitted; EKF_E_TIMEOUT if a device hand-off timed out since the last
+ * report (see EKF_E_TIMEOUT). */
 int ekf_sync(ekf_t h);
 int ekf_get_pose(ekf_t h, int filter, double* theta_x_y);
 int ekf_get_map_odom(ekf_t h, int filter, double* theta_x_y); /* t_map_odom */

@@ -36,7 +36,7 @@ def test_config_defaults_match_reference():
 
 def test_strerror_table():
     L = pyekf.lib()
-    for rc in (0, -1, -2, -3, -4, -5, -6):
+    for rc in (0, -1, -2, -3, -4, -5, -6, -7):
         assert L.ekf_strerror(rc)
 
 

@@ -115,8 +115,8 @@ def test_device_replay_chains_with_host_calls():
 
 def test_device_replay_fp32_n1024():
     """The headline shape: fp32 N = 1024 from an fp64 survey, 24 messages of 16 markers through the
-    device planner against the host planner (the staged rebuild operands and the fp32 patch are
-    planned on the GPU too)."""
+    device planner (bench.py's timed entry point) against the host planner (the staged rebuild
+    operands and the fp32 patch are planned on the GPU too) and against the fp64 oracle."""
     N, warm, T = 1024, 40, 24
     sc = synth.synthetic(N, warm + T)
     assert sc.ids.shape[1] <= 16  # EKF_MAX_CHUNK: one chunk per message
@@ -135,6 +135,20 @@ def test_device_replay_fp32_n1024():
     assert np.abs(xh - xd).max() < 1e-6
     assert np.abs(Sh - Sd).max() < 1e-6
     assert np.all(np.isfinite(Sd))
+    # the timed entry point itself against the fp64 oracle (fake_sensor_cb, slam.cpp:180-316) from
+    # the same warm state, at the fp32 tolerances of tests/test_gpu_scale.py: pose 1e-6, state
+    # 1e-5, Σ 5e-5 absolute
+    ref = orc.OracleEKF(n_landmarks=N)
+    ref.set(x0, S0, ws[2], x0[:3], c0)
+    for t in range(warm, warm + T):
+        ref.set_odom(odom[t])
+        c = int(sc.count[t])
+        ref.fake_sensor_cb(sc.ids[t, :c], sc.actions[t, :c], sc.rel[t, :c])
+    xr, Sr, _, cr = ref.get()
+    assert cd == cr
+    assert np.abs(xd[:3] - xr[:3]).max() < 1e-6
+    assert np.abs(xd - xr).max() < 1e-5
+    assert np.abs(Sd - Sr).max() < 5e-5
 
 
 def test_device_replay_rejects():

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The 20-step timed region under rocprofv3 --kernel-trace --hip-trace with the host clocks
-# (EKF_BENCH_TRACE=1); then tools/region_timeline.py on it. Usage: bash tools/p3_trace.sh <tag> [bench args]
+# (EKF_BENCH_TRACE=1); then tools/region_timeline.py on it. Usage: bash tools/api_trace.sh <tag> [bench args]
 set -o pipefail
 tag=${1:?tag}; shift
 export TMPDIR=/tmp

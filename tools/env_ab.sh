@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of one environment switch on bench workloads, alternating (repo root on the box).
-# Usage: bash tools/p3_envab.sh <tag> <VAR> "<values>" "<workloads>" [bench args...]
+# Usage: bash tools/env_ab.sh <tag> <VAR> "<values>" "<workloads>" [bench args...]
 set -o pipefail
 tag=${1:?tag}; var=${2:?var}; vals=${3:?values}; wls=${4:?workloads}; shift 4
 mkdir -p gpurun_out

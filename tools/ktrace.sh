@@ -1,7 +1,7 @@
 #!/bin/bash
 # The timed region under rocprofv3 --kernel-trace only (no API tracing, so the host side runs at
 # its own speed), with the host clocks (EKF_BENCH_TRACE=1), for --steps 20 and 200.
-# Usage: bash tools/p3_ktrace.sh <tag> [bench args]
+# Usage: bash tools/ktrace.sh <tag> [bench args]
 set -o pipefail
 tag=${1:?tag}; shift
 export TMPDIR=/tmp
