@@ -58,7 +58,8 @@ struct ekf_ctx {
   hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
-  bool nb = false;               // EKF_NB=1: the chain's helper waves rebuild the next block
+  bool build = false;            // EKF_BUILD=1: chain launches of > 1 chunk take a builder
+                                 // workgroup per filter (k_chain, PassArgs::build)
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
   bool defer = false;            // ekf_defer: plan now, upload and launch later
   bool joseph = false;           // ekf_set_joseph (resident: its own kernel; pipeline: kJoseph chunks)
@@ -70,6 +71,9 @@ struct ekf_ctx {
   AmArgs am{};                   // k_assoc_msg scratch (allocated at the first association chunk)
   int am_route = 0;              // unknown association: EKF_ASSOC_* (fixed at ekf_create)
   int bulk_cus_per_xcd = 0;      // CUs the bulk stream may use on each XCD
+  int main_cus_per_xcd = 0;      // CUs the main stream may use on each XCD (0: every CU, no mask)
+  BuildRec* bout = nullptr;      // [2][F] the builders' blocks
+  BuildChan* chan = nullptr;     // [F] the chains' predict parameters for the builders
   unsigned* fatal_h = nullptr;   // host-mapped: a device poll timed out (EKF_E_TIMEOUT)
   unsigned* fatal_d = nullptr;   // its device address (PassArgs::fatal)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
@@ -152,6 +156,8 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.rows_stride = static_cast<size_t>(h->ldk) * kRowW;
   a.sync = h->sync;
   a.fatal = h->fatal_d;
+  a.bout = h->bout;
+  a.chan = h->chan;
   a.desc = desc;
   a.n = h->n;
   a.ld = h->ld;
@@ -247,7 +253,9 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
   hipStream_t ms = h->stream, bs = two ? h->bulk : h->stream;
   a.polls = two && h->devsync ? 1 : 0;
   a.first_ready = h->epoch_owed ? 1 : 0;  // (the host joined the bulk stream since that pass)
-  a.nb = a.polls && h->nb ? 1 : 0;
+  // a builder workgroup per filter beside each chain (k_chain): multi-chunk device-epoch launches
+  a.build = a.polls && h->build && nchunks > 1 ? 1 : 0;
+  a.nf_launch = nf;
   if (pipelined && !nolook) {
     // events: a rebuilding (kLook) chain needs the Σ pass two launches back
     if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s0 & 1], 0));
@@ -328,6 +336,7 @@ int create_streams(ekf_ctx* h) {
   h->bulk_cus_per_xcd = cus / kXcd;
   if (split > 0 && cus % kXcd == 0 && split * kXcd < cus) {
     h->bulk_cus_per_xcd = cus / kXcd - split;
+    h->main_cus_per_xcd = split;
     const int words = (cus + 31) / 32;
     std::vector<uint32_t> mmain(words, 0), mbulk(words, 0);
     for (int b = 0; b < cus; ++b) (b < split * kXcd ? mmain : mbulk)[b / 32] |= 1u << (b % 32);
@@ -1037,7 +1046,6 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   };
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
   if (const char* e = std::getenv("EKF_SERIAL")) h->serial = std::atoi(e) != 0;
-  if (const char* e = std::getenv("EKF_NB")) h->nb = std::atoi(e) != 0;
   if (const char* e = std::getenv("EKF_ASSOC_MSG")) h->assoc_msg = std::atoi(e) != 0;
   {  // EKF_RESIDENT=0: the HBM pipeline at every size (tests compare the two)
     const char* e = std::getenv("EKF_RESIDENT");
@@ -1080,9 +1088,18 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     if (hipMalloc(&h->stage, stage_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
     if (hipMemset(h->stage, 0, stage_bytes) != hipSuccess) return fail(EKF_E_HIP);
   }
-  const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + h->F);
+  const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + kSyncKinds * h->F);
   if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
+  {  // the block builders: device epochs, staged operands, and room on the main stream's CUs of
+     // every XCD for the chain and the builder of its filters (one workgroup per CU: LDS)
+    const char* e = std::getenv("EKF_BUILD");  // opt-in (EKF_BUILD=1): measured slower, DESIGN.md
+    h->build = h->devsync && !h->serial && h->stage && !h->resident &&
+               h->main_cus_per_xcd >= 2 * ((h->F + 7) / 8) && e && std::atoi(e) != 0;
+    if (h->build && (hipMalloc(&h->bout, 2 * sizeof(BuildRec) * h->F) != hipSuccess ||
+                     hipMalloc(&h->chan, sizeof(BuildChan) * h->F) != hipSuccess))
+      return fail(EKF_E_NOMEM);
+  }
   h->ddesc_cap = std::max(kDescInit, static_cast<size_t>(h->F) * 4);
   if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->ddesc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
   for (int i = 0; i < kRing; ++i)
@@ -1150,6 +1167,8 @@ int ekf_destroy(ekf_t h) {
   if (h->ev_chain) hipEventDestroy(h->ev_chain);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->sync) hipFree(h->sync);
+  if (h->bout) hipFree(h->bout);
+  if (h->chan) hipFree(h->chan);
   for (hipEvent_t e : h->ev_sig)
     if (e) hipEventDestroy(e);
   if (h->bulk) hipStreamDestroy(h->bulk);
@@ -1423,6 +1442,13 @@ int ekf_sync(ekf_t h) {
   return take_fatal(h);
 }
 
+int ekf_get_schedule(ekf_t h, int* flags) {
+  if (!h || !flags) return EKF_E_ARG;
+  *flags = (h->devsync ? EKF_SCHED_DEVSYNC : 0) | (h->build ? EKF_SCHED_BUILDER : 0) |
+           (h->serial ? EKF_SCHED_SERIAL : 0);
+  return EKF_OK;
+}
+
 int ekf_get_assoc_route(ekf_t h, int* route) {
   if (!h || !route) return EKF_E_ARG;
   *route = h->am_route;
@@ -1595,9 +1621,6 @@ int ekf_debug_poison_lds(int device) {
 int ekfslam_diag_read_stamps(unsigned long long* out, int n);  // ekf_kernels.hip
 // dev only (libekfslam_diag.so): the chain kernel's s_memtime stamps of filter 0's last chunk
 int ekf_diag_stamps(unsigned long long* out, int n) { return ekfslam_diag_read_stamps(out, n); }
-extern "C" int ekfslam_diag_read_nb(double* out, unsigned* info);  // ekf_kernels.hip
-// dev only: the helper-rebuilt block vs the prologue's (tools/chain_stamps.py NBCHK=1)
-int ekf_diag_nb(double* out, unsigned* info) { return ekfslam_diag_read_nb(out, info); }
 int ekfslam_res_read_stamps(unsigned long long* out, int n);  // ekf_resident.hip
 // dev only: the resident kernel's stamps (filter flo, thread 0): 6 per correction
 int ekf_diag_res_stamps(unsigned long long* out, int n) { return ekfslam_res_read_stamps(out, n); }

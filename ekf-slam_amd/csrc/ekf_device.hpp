@@ -21,6 +21,11 @@ constexpr int kZC = 2 * kMaxChunk;               // correction columns of Z / ro
 // Device epochs (unsigned words of the handle's sync buffer, each polled word on its own line):
 constexpr int kSyncSigma = 0;    // epoch (seq + 1) of the last complete Σ pass (k_sigma_epoch)
 constexpr int kSyncChain = 64;   // [F]: epoch of each filter's last complete chain
+// Further [F] arrays behind kSyncChain (word kSyncChain + kind·F + f), the block builder's
+// hand-offs (k_chain, PassArgs::build): the chain's Z / Y progress ((seq << 5) | steps done), its
+// predict parameters (seq + 1) and the builder's finished block (seq + 1 of the block's chunk).
+constexpr int kSyncKindZ = 1, kSyncKindY = 2, kSyncKindPro = 3, kSyncKindBuilt = 4;
+constexpr int kSyncKinds = 5;
 
 // MsgDesc.flags
 constexpr int kFirst = 1;    // chunk carries the predict (slam.cpp:184-198) for this message
@@ -106,6 +111,20 @@ template <typename T>
 struct alignas(16) StageRec {
   double r0u[kStW], c0u[kStW], r0p[kStW], c0p[kStW], xg[kStW];
   T v[3][kStW * kStW];
+};
+
+// The next chunk's rebuilt block, from the builder workgroup to the chain (PassArgs::build):
+// P = Σ_in[U, U] before the chunk's own predict (the prologue's P after its K'·M' tiles), R =
+// Σ_pred'[U, U'] (x_in[U] = x' + R·Zx' for rows the previous chunk did not touch), xg = x_in'[U].
+// [2][F] by the built chunk's Σ parity. chan: the chain's predict parameters (a1, a2) for the
+// builder of its next chunk.
+struct alignas(16) BuildRec {
+  double P[kMaxU][kMaxU + 1];
+  double R[kMaxU][kMaxU + 1];
+  double xg[kMaxU + 1];
+};
+struct alignas(16) BuildChan {
+  double a1, a2;
 };
 
 // ---- unknown association of a whole chunk in one launch (k_assoc_msg, ekf_assoc.hip) ----

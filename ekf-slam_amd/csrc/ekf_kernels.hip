@@ -52,7 +52,16 @@ __device__ unsigned long long g_stamps[4 * 512];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                   \
       g_stamps[512 * (seq & 3) + (i)] = (v);                                      \
   } while (0)
+// the builder workgroup (block 8 of the build grid: filter 0's), thread t, ring slot of chunk seqv
+#define EKF_BSTAMP(seqv, i, t)                                                    \
+  do {                                                                            \
+    if (A.build && blockIdx.x == 8 && threadIdx.x == (t))                         \
+      g_stamps[512 * ((seqv) & 3) + (i)] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
 #else
+#define EKF_BSTAMP(seqv, i, t) \
+  do {                         \
+  } while (0)
 #define EKF_STAMPT(i, t) \
   do {                   \
   } while (0)
@@ -177,13 +186,13 @@ struct ChainShared {
   int pub;    // steps whose K, M, H, S⁻¹ wave 0 has published
   int pdone;  // steps wave 3 has applied outside the cross
   int any_init;  // a correction of this chunk initialised its landmark (slam.cpp:213-216)
-  // the next chunk's block, rebuilt by waves 1–2 during this chunk's corrections
-  unsigned built;  // seq + 1 of the chunk whose block the chunk before rebuilt
-  int kdone;       // k-blocks whose K' columns wave 1 has stored
-  int nb_ok1, nb_ok2;  // wave 1 / 2 completed its part (set at their ends)
-  int w1fin;       // wave 1 has decided (wave 2 waits for it before finishing)
-  int un[kMaxU];   // the next chunk's U
-  double c0U2[kMaxU];  // Σ_in[u⁺_a][0] (wave 2's copy)
+  // the builder workgroup (PassArgs::build): the block of its target chunk, rebuilt as the chain of
+  // the chunk before publishes its factors
+  int kdone;       // k-blocks whose K' columns are final (builder wave 0)
+  int mdone;       // k-blocks whose M' rows are final (builder wave 1)
+  int cdone;       // builder wave 1 has stored C̃ and D̃
+  int un[kMaxU];   // the target chunk's U
+  double c0U2[kMaxU];  // Σ_in[u⁺_a][0] (builder wave 1's copy)
 };
 
 
@@ -214,29 +223,6 @@ __device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
 // Wave 0's corrections (see k_chain, A2): a function of its own, so that its register allocation
 // is not the one of the kernel's four wave programs together (the shared allocation spilled
 // SGPRs, and their reloads sat in this loop). LDS through address-space-3 references.
-#ifdef EKF_DIAG_STAMPS
-// Diagnostic build only: a chunk whose block waves 1–2 rebuilt runs the prologue's rebuild as well;
-// both versions of R̃, C̃, K', M', P̃ and the vectors (filter 0), kept from the first mismatch on.
-__device__ double g_nb[2][6][kMaxU + 1][kMaxU + 1];
-__device__ unsigned g_nbinfo[8];  // mismatching chunks, seq of the first, checked chunks, frozen
-__device__ void nb_snapshot(ChainShared& sh, const double (&P)[kMaxU][kMaxU + 1], int w) {
-  for (int e = threadIdx.x; e < (kMaxU + 1) * (kMaxU + 1); e += blockDim.x) {
-    const int a = e / (kMaxU + 1), b = e % (kMaxU + 1);
-    g_nb[w][0][a][b] = a < kMaxU ? sh.pv.R[a][b] : 0.0;
-    g_nb[w][1][a][b] = sh.pv.C[a][b];
-    g_nb[w][2][a][b] = a < kMaxU && b < kZC ? sh.pv.K[a][b] : 0.0;
-    g_nb[w][3][a][b] = a < kZC ? sh.pv.M[a][b] : 0.0;
-    g_nb[w][4][a][b] = a < kMaxU ? P[a][b] : 0.0;
-    double v = 0.0;
-    if (b < kMaxU) v = a == 0 ? sh.pv.xU[b] : a == 1 ? sh.pv.Zx[b] : a == 2 ? sh.pv.xg[b] : 0.0;
-    if (a == 3 && b < 3) v = sh.tmo[b];
-    if (b < kMaxU && a >= 4 && a <= 8)
-      v = a == 4 ? sh.pv.r0U[b] : a == 5 ? sh.pv.c0U[b] : a == 6 ? sh.pv.r0P[b] : a == 7 ? sh.pv.c0P[b] : sh.c0U2[b];
-    g_nb[w][5][a][b] = v;
-  }
-}
-#endif
-
 typedef __attribute__((address_space(3))) ChainShared LdsChain;
 typedef __attribute__((address_space(3))) const MsgDesc LdsDesc;
 typedef __attribute__((address_space(3))) double ldsd;
@@ -503,11 +489,12 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
 }
 
 
-// ---- the next chunk's block, rebuilt by k_chain's waves 1–2 during this chunk's corrections ----
-// (device-epoch groups, when the staged operands land in time.) The prologue's rebuild, spread
+// ---- the next chunk's block, rebuilt by the builder workgroup during this chunk's corrections ----
+// (device-epoch launches of more than one chunk, PassArgs::build.) The prologue's rebuild, spread
 // over the corrections: the same formulas and the same MFMA sequence (K' and M' tiles over U',
 // then P̃ −= K'·M' per k-block of 4 factor columns = 2 corrections, in order), so the block is
-// bit-identical to the one the prologue builds. LDS through address-space-3 pointers.
+// bit-identical to the one the prologue builds. "This chunk" below is the chunk before the target
+// (its U, its predict, its Z and Y); LDS through address-space-3 pointers.
 constexpr int kStE = (kStW * kStW + 63) / 64;  // 21 block entries per lane of one wave
 
 // the next chunk's U (k_chain A0's mapping: bad id → slot 0's columns, padding → 0)
@@ -516,11 +503,6 @@ __device__ __forceinline__ int nb_ucol(LdsDesc* nd, int nun, int a, int N) {
   if (a >= nun) return 0;
   const int id = nd->ids[(a - 3) >> 1];
   return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
-}
-
-// the next chunk's staged operands have landed: the Σ-pass epoch it waits for (k_chain's `need`)
-__device__ __forceinline__ bool nb_landed(const unsigned* sync, unsigned seq) {
-  return static_cast<int>(__builtin_amdgcn_readfirstlane(epoch_load(sync + kSyncSigma)) - seq) >= 0;
 }
 
 // Wave 1: R̃ = pred(Σ_in[U⁺, U]) into pv.R (the prologue's R), x_in[U⁺] into pv.xg. U⁺ = the next
@@ -723,7 +705,295 @@ __device__ __noinline__ void nb_pblock(LdsChain* sh, int pn, int pb, int nun) {
   }
 }
 
+
+// The previous chunk's predict on the gathered rebuild operands: v + α_i·Σ[0][j] +
+// (Σ[i][0] + α_i·Σ00)·α_j + Q̄, for D = Σ_in'[U, U] → P, R = Σ_in'[U, U'] → pv.R and
+// C = Σ_in'[U', U] → pv.C (R / C columns k ≥ |U'| up to 36 zeroed: MFMA k padding). Thread tid's
+// entries e = tid + i·256 of the 36 × 36 block. k_chain's prologue and the builder both run it, so
+// their blocks agree bit for bit. Reads sh.u (U), sh.pv.u (U'), the staged row 0 / column 0
+// (pv.r0U, c0U, r0P, c0P) and the previous predict (pv.first, a1, a2).
 constexpr int kChainThreads = 256;
+constexpr int kRebW = kMaxU + 1;                                      // 36: entry e = a·36 + b
+constexpr int kRebPer = (kRebW * kRebW + kChainThreads - 1) / kChainThreads;  // 6
+template <typename T>
+__device__ __forceinline__ void rebuild_rcd(ChainShared& sh, double (&P)[kMaxU][kMaxU + 1],
+                                            const T (&vd)[kRebPer], const T (&vr)[kRebPer],
+                                            const T (&vc)[kRebPer], int tid, int nu, int np,
+                                            double q) {
+  constexpr int kW = kRebW, kPer = kRebPer;
+  const bool pf = sh.pv.first != 0;
+  const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
+  // every LDS read of the six entries first (clamped indices, no branch around a read): one
+  // LDS round instead of a wait per predicated read
+  double r0Ub[kPer], r0Ua[kPer], c0Ua[kPer], r0Pb[kPer], c0Pb[kPer];
+  int ua[kPer], ub[kPer], pu[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = tid + i * kChainThreads;
+    const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
+    ua[i] = sh.u[a];
+    ub[i] = sh.u[b];
+    pu[i] = sh.pv.u[b];
+    r0Ub[i] = sh.pv.r0U[b];
+    r0Ua[i] = sh.pv.r0U[a];
+    c0Ua[i] = sh.pv.c0U[a];
+    r0Pb[i] = sh.pv.r0P[b];
+    c0Pb[i] = sh.pv.c0P[b];
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = tid + i * kChainThreads;
+    const int a = e / kW, b = e % kW;
+    double v = static_cast<double>(vd[i]), vR = 0.0, wC = 0.0;
+    if (b < np) {
+      vR = static_cast<double>(vr[i]);
+      wC = static_cast<double>(vc[i]);
+    }
+    if (pf) {
+      const double ai = alpha_of(ua[i], qa1, qa2), aj = alpha_of(ub[i], qa1, qa2);
+      const double ak = alpha_of(pu[i], qa1, qa2);
+      v = v + ai * r0Ub[i];
+      v = v + (c0Ua[i] + ai * s00) * aj;
+      v = (ua[i] == ub[i] && ua[i] < 3) ? v + q : v;
+      double v2 = vR + ai * r0Pb[i];
+      v2 = v2 + (c0Ua[i] + ai * s00) * ak;
+      double w2 = wC + ak * r0Ua[i];
+      w2 = w2 + (c0Pb[i] + ak * s00) * ai;
+      const bool qd = ua[i] == pu[i] && ua[i] < 3;
+      vR = b < np ? (qd ? v2 + q : v2) : 0.0;
+      wC = b < np ? (qd ? w2 + q : w2) : 0.0;
+    }
+    if (a < nu && b < nu) P[a][b] = v;
+    if (a < nu) {  // b = k over U' (36: the MFMA k padding, zero)
+      sh.pv.R[a][b] = vR;
+      sh.pv.C[b][a] = wC;
+    }
+  }
+}
+
+// P̃ −= K'·M' over k-blocks [pb0, pb1) in order (the prologue's P-tile MFMA sequence, a k-block at
+// a time): the 9 tiles' accumulators read once, one MFMA per tile and k-block, stored once (the
+// LDS round trip of an f64 accumulator is exact, so any split of the k-blocks gives the same bits).
+__device__ __noinline__ void nb_pblocks(LdsChain* sh, int pn, int pb0, int pb1, int nun) {
+  __builtin_amdgcn_wave_barrier();
+  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
+  d4 acc[9];
+#pragma unroll
+  for (int tt = 0; tt < 9; ++tt) {
+    const int ti = tt / 3, tj = tt - 3 * ti, cc = min(16 * tj + i16, kMaxU - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[tt][r] = sh->P[pn][min(16 * ti + k4 + 4 * r, kMaxU - 1)][cc];
+  }
+  for (int pb = pb0; pb < pb1; ++pb) {
+    const int k = 4 * pb + k4;
+    double av[3], bv[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      av[t] = -sh->pv.K[min(16 * t + i16, kMaxU - 1)][k];
+      bv[t] = sh->pv.M[k][min(16 * t + i16, kMaxU - 1)];
+    }
+#pragma unroll
+    for (int tt = 0; tt < 9; ++tt) acc[tt] = mfma_f64(av[tt / 3], bv[tt % 3], acc[tt]);
+  }
+#pragma unroll
+  for (int tt = 0; tt < 9; ++tt) {
+    const int ti = tt / 3, tj = tt - 3 * ti, col = 16 * tj + i16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row2 = 16 * ti + k4 + 4 * r;
+      if (row2 < nun && col < nun) sh->P[pn][row2][col] = acc[tt][r];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+
+// Word `kind` of filter f in the handle's sync buffer (ekf_device.hpp kSyncKind*).
+template <typename T>
+__device__ __forceinline__ unsigned* sync_word(const PassArgs<T>& A, int kind, int f) {
+  return A.sync + kSyncChain + static_cast<size_t>(kind) * A.rec_stride + f;
+}
+
+// A chunk t whose block the builder rebuilds from the chunk p before it: both active, t rebuilds
+// from staged operands (kLook | kStageIn), p is no Joseph chunk (its rank-4 factor stays with the
+// prologue) and has known ids only (A0 maps an association id through FilterCtl). The chain and
+// the builder evaluate it on the same two descriptors.
+__device__ __forceinline__ bool build_pred(const MsgDesc& dp, const MsgDesc& dt) {
+  constexpr int kNeed = kActive | kLook | kStageIn;
+  if (!(dp.flags & kActive) || (dp.flags & kJoseph) || (dt.flags & kNeed) != kNeed) return false;
+  bool ok = true;
+  for (int c = 0; c < dp.m; ++c) ok = ok && dp.ids[c] >= 0;
+  return ok;
+}
+
+// One lane polls a progress word of the chain until it reaches v (wrap-safe), then the wave
+// acquires; false on timeout.
+__device__ __forceinline__ bool wave_wait_acquire(const unsigned* p, unsigned v) {
+  bool ok = true;
+  if ((threadIdx.x & 63) == 0) ok = epoch_wait_acquire(p, v);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
+}
+
+// The builder workgroup of filter f (PassArgs::build). For every chunk t ≥ 1 of the launch whose
+// block its chain would rebuild from staged operands (build_pred), the prologue's rebuild — the
+// same expressions and MFMA sequence, so the same bits — while the chain still runs chunk t − 1
+// on another CU of the same XCD:
+//   intake (all waves, once the stage has landed: the Σ-pass epoch the chain of t would wait
+//     for): R̃, C̃, D̃ = the previous predict on the staged Σ_in' entries (rebuild_rcd);
+//   wave 0  K' = R̃·Z' column tiles, wave 1  M' = Y'·C̃ row tiles, for the k-blocks (two
+//     corrections each) whose Z' / Y' the chain's waves 1–2 have published (write-through record
+//     + progress words): every k-block complete at a poll in one round of loads and tiles;
+//   wave 2  P̃ −= K'·M' over the k-blocks both have finished (nb_pblocks).
+// P̃, R̃ and x_in' at U then go to BuildRec and the epoch kSyncKindBuilt: the chain of t reads them
+// instead of running its prologue's gather, previous predict and MFMA tiles.
+template <typename T>
+__device__ void chain_builder(const PassArgs<T>& A, int nchunks, int fy, ChainShared& sh,
+                              MsgDesc (&sdesc)[2]) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int f = A.f0 + fy;
+  LdsChain* shl = (LdsChain*)(&sh);
+  constexpr int kDV = static_cast<int>(sizeof(MsgDesc) / 16);
+  for (int ci = 1; ci < nchunks; ++ci) {
+    __syncthreads();
+    if (tid < 2 * kDV) {  // the chunk before (p) and the target (t)
+      const int w = tid / kDV, k = tid - w * kDV;
+      reinterpret_cast<uint4*>(&sdesc[w])[k] = reinterpret_cast<const uint4*>(
+          &A.desc[static_cast<size_t>(ci - 1 + w) * A.desc_stride + fy])[k];
+    }
+    __syncthreads();
+    const MsgDesc& dp = sdesc[0];
+    const MsgDesc& dt = sdesc[1];
+    if (!build_pred(dp, dt)) continue;
+    const unsigned seqp = A.seq + static_cast<unsigned>(ci - 1), seqt = seqp + 1u;
+    const int m = dp.m, np = 3 + 2 * m, nu = 3 + 2 * dt.m;
+    const int nk = (m + 1) >> 1;
+    EKF_BSTAMP(seqt, 400, 0);
+    if (tid < kMaxU) {  // U (target) and U' (the chunk before): A0's mapping of known ids
+      const int c = (tid - 3) >> 1, e = (tid - 3) & 1;
+      int u = tid < 3 ? tid : 0, up = u;
+      if (tid >= 3 && tid < nu) u = (dt.ids[c] >= A.N ? 3 : 3 + 2 * dt.ids[c]) + e;
+      if (tid >= 3 && tid < np) up = (dp.ids[c] >= A.N ? 3 : 3 + 2 * dp.ids[c]) + e;
+      sh.u[tid] = u;
+      sh.pv.u[tid] = up;
+    }
+    // Z' and Y' start zero (their columns / rows land k-block by k-block)
+    for (int e = tid; e < kMaxU * (kZC + 1); e += kChainThreads) (&sh.Z[0][0])[e] = 0.0;
+    for (int e = tid; e < kZC * (kMaxU + 1); e += kChainThreads) (&sh.Y[0][0])[e] = 0.0;
+    if (tid == 0) {
+      sh.kdone = 0;
+      sh.mdone = 0;
+      // the stage has landed (the chain of t waits for the same epoch) and the chain of p has
+      // published its predict parameters
+      const unsigned need = seqt - 1u;
+      bool ok = true;
+      if (need && !(A.first_ready && need <= A.seq))
+        ok = epoch_wait_acquire(A.sync + kSyncSigma, need);
+      ok = epoch_wait_acquire(sync_word(A, kSyncKindPro, f), seqp + 1u) && ok;
+      if (!ok) flag_timeout(&A.ctl[f].status, A.fatal);
+      sh.pv.a1 = A.chan[f].a1;
+      sh.pv.a2 = A.chan[f].a2;
+      sh.pv.first = (dp.flags & kFirst) ? 1 : 0;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    EKF_BSTAMP(seqt, 401, 0);
+    {  // intake: the staged entries (as the prologue loads them), then the previous predict
+      const StageRec<T>* sg = A.stage + static_cast<size_t>(dt.parity) * A.rec_stride + f;
+      T vd[kRebPer], vr[kRebPer], vc[kRebPer];
+#pragma unroll
+      for (int i = 0; i < kRebPer; ++i) {
+        const int es = min(tid + i * kChainThreads, kRebW * kRebW - 1);
+        vd[i] = sg->v[0][es];
+        vr[i] = sg->v[1][es];
+        vc[i] = sg->v[2][es];
+      }
+      const int tc = tid < kMaxU ? tid : 0;
+      const double r0u = sg->r0u[tc], c0u = sg->c0u[tc], r0p = sg->r0p[tc], c0p = sg->c0p[tc];
+      const double xg = sg->xg[tc];
+      if (tid < kMaxU) {
+        sh.pv.r0U[tid] = r0u;
+        sh.pv.c0U[tid] = c0u;
+        sh.pv.r0P[tid] = r0p;
+        sh.pv.c0P[tid] = c0p;
+        sh.pv.xg[tid] = xg;
+      }
+      __syncthreads();
+      rebuild_rcd<T>(sh, sh.P[0], vd, vr, vc, tid, nu, np, A.q);
+    }
+    __syncthreads();
+    EKF_BSTAMP(seqt, 402, 0);
+    const ChunkRec* rp = A.rec + static_cast<size_t>(dp.parity) * A.rec_stride + f;
+    bool ok = true;
+    if (wave == 0 || wave == 1) {  // K' (wave 0) / M' (wave 1) as the chain publishes Z' / Y'
+      const bool kz = wave == 0;
+      const unsigned* prog = sync_word(A, kz ? kSyncKindZ : kSyncKindY, f);
+      for (int kb = 0; kb < nk;) {
+        // every k-block complete at this poll (correction c done ⇒ progress (seqp << 5) | c + 1)
+        const unsigned want = (seqp << 5) | static_cast<unsigned>(min(2 * kb + 2, m));
+        unsigned got = want;
+        if (lane == 0) {
+          bool w = epoch_wait_acquire(prog, want);
+          ok = ok && w;
+          got = epoch_load(prog);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        got = __builtin_amdgcn_readfirstlane(got);
+        ok = __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;  // (lane 0 polled)
+        const int steps = static_cast<int>(got - (seqp << 5)) >= m || !ok
+                              ? m : static_cast<int>(got - (seqp << 5));
+        const int kb1 = steps >= m ? nk : max(steps >> 1, kb + 1);
+        const int nc = 4 * (kb1 - kb);  // factor columns (Z') / rows (Y') of these k-blocks
+        if (kz) {
+          for (int e = lane; e < kMaxU * nc; e += 64) {
+            const int row = e / nc, col = 4 * kb + (e - row * nc);
+            if (col < 2 * m) sh.Z[row][col] = rp->Z[row][col];
+          }
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: LDS keeps its order)
+          kb = nb_ktiles(shl, kb, kb1, m, np);
+          EKF_BSTAMP(seqt, 409 + kb, 0);
+        } else {
+          for (int e = lane; e < nc * kMaxU; e += 64) {
+            const int r = 4 * kb + e / kMaxU, col = e % kMaxU;
+            if (r < 2 * m) sh.Y[r][col] = rp->Y[r][col];
+          }
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          kb = nb_mtiles(shl, kb, kb1, m, np);
+          lds_publish(&sh.mdone, kb);
+          EKF_BSTAMP(seqt, 419 + kb, 64);
+        }
+      }
+    } else if (wave == 2) {  // P̃ −= K'·M' as both land
+      for (int pb = 0; pb < nk;) {
+        lds_wait_ge(&sh.kdone, pb + 1);
+        lds_wait_ge(&sh.mdone, pb + 1);
+        const int pb1 = min(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                &sh.kdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)),
+                            __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                &sh.mdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)));
+        nb_pblocks(shl, 0, pb, pb1, nu);
+        pb = pb1;
+        EKF_BSTAMP(seqt, 429 + pb, 128);
+      }
+    }
+    if (!ok && lane == 0) flag_timeout(&A.ctl[f].status, A.fatal);
+    __syncthreads();
+    // P̃ (rows / columns < |U|), R̃ (rows < |U|) and x_in' at U to the chain of t
+    BuildRec* bo = A.bout + static_cast<size_t>(dt.parity) * A.rec_stride + f;
+    for (int e = tid; e < kMaxU * kMaxU; e += kChainThreads) {
+      const int a = e / kMaxU, b = e - a * kMaxU;
+      if (a < nu) {
+        if (b < nu) st_wt(&bo->P[a][b], sh.P[0][a][b]);
+        st_wt(&bo->R[a][b], sh.pv.R[a][b]);
+      }
+    }
+    if (tid < nu) st_wt(&bo->xg[tid], sh.pv.xg[tid]);
+    drain_stores();
+    __syncthreads();
+    if (tid == 0) epoch_store(sync_word(A, kSyncKindBuilt, f), seqt + 1u);
+    EKF_BSTAMP(seqt, 440, 0);
+  }
+}
 
 // One workgroup per filter, persistent over the `nchunks` chunks of a launch (descriptors
 // A.desc[i·desc_stride + filter]): per chunk the m sequential corrections on the |U|×|U| block.
@@ -739,7 +1009,18 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // the next one's (and computes its predicted pose from it).
   __shared__ MsgDesc sdesc[2];
   static_assert(sizeof(MsgDesc) % 16 == 0, "MsgDesc copied as uint4");
-  const int f = A.f0 + blockIdx.y;
+  // build: a 1-D grid, 16 blocks per 8 filters — filter fy's chain is block 16·⌊fy/8⌋ + fy mod 8
+  // and its builder the block 8 after it, so both run on XCD fy mod 8 (dispatch deals blocks
+  // round robin over the XCDs) and hand off through that XCD's L2
+  int fy = blockIdx.y;
+  bool builder = false;
+  if (A.build) {
+    const int L = blockIdx.x;
+    fy = 8 * (L >> 4) + (L & 7);
+    builder = ((L >> 3) & 1) != 0;
+    if (fy >= A.nf_launch) return;
+  }
+  const int f = A.f0 + fy;
   const int tid = threadIdx.x;
   const int ld = A.ld;
   FilterCtl* ctl = A.ctl + f;
@@ -747,12 +1028,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // so padding rows / columns that feed MFMA or dot products as zeros really are zeros
   for (int e = tid; e < static_cast<int>(sizeof(ChainShared) / 8); e += blockDim.x)
     reinterpret_cast<double*>(&sh)[e] = 0.0;
+  if (builder) {
+    chain_builder<T>(A, nchunks, fy, sh, sdesc);
+    return;
+  }
   bool pre = false;        // sdesc[ci & 1] was prefetched by the previous chunk's epilogue
   unsigned pending = 0;    // chain epoch of the previous chunk, not yet published (its record
                            // stores are still in flight; see the epilogue)
   for (int ci = 0; ci < nchunks; ++ci) {
   if (!pre) {
-    const MsgDesc& gd = A.desc[static_cast<size_t>(ci) * A.desc_stride + blockIdx.y];
+    const MsgDesc& gd = A.desc[static_cast<size_t>(ci) * A.desc_stride + fy];
     __syncthreads();
     if (threadIdx.x < sizeof(MsgDesc) / 16)
       reinterpret_cast<uint4*>(&sdesc[ci & 1])[threadIdx.x] =
@@ -778,13 +1063,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // stream), and this record parity is free again once that pass is done (its factor kernel read
   // it); a chunk that gathers its own Σ_in needs the pass one back.
   const unsigned need = look ? (seq >= 2 ? seq - 1 : 0u) : seq;
-  // the chunk before rebuilt this chunk's block (it saw the epoch `need` already)
-  bool built = look && ci > 0 && sh.built == seq;
-#ifdef EKF_DIAG_STAMPS
-  const bool nbchk = built && blockIdx.y == 0 && !g_nbinfo[3];
-  if (nbchk) nb_snapshot(sh, sh.P[ci & 1], 0);
-  built = false;
-#endif
+  // the builder workgroup rebuilt this chunk's block (it waited for the epoch `need` already)
+  const bool built = A.build && ci > 0 && build_pred(sdesc[(ci + 1) & 1], d);
   // A0's associated ids (k_assoc, earlier on this stream), loaded unconditionally (clamped) and
   // here, so that the barrier below completes them: under A0's branch the load was waited for,
   // vmcnt(0), together with every early load below
@@ -797,11 +1077,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   if (A.polls && need && tid == 0 && !built && !(A.first_ready && need <= A.seq) &&
       !epoch_wait_acquire(A.sync + kSyncSigma, need))
     flag_timeout(&ctl->status, A.fatal);
+  if (built && tid == 0 && !epoch_wait_acquire(sync_word(A, kSyncKindBuilt, f), seq + 1u))
+    flag_timeout(&ctl->status, A.fatal);
+  EKF_STAMP(305);
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
   if (tid == 0) sh.status = 0;
   __syncthreads();
   EKF_STAMP(0);
-  EKF_STAMPV(304, built ? 1ull : 0ull);
+  EKF_STAMPV(306, __builtin_amdgcn_s_memrealtime());  // (the builder's clock: 100 MHz, chip-wide)
+  EKF_STAMPV(304, built ? 1ull : 0ull);  // (EKF_STAMP(305): the builder's epoch acquired)
   const T* S = A.sig[d.parity] + f * A.sig_stride;
   const double* xin = A.x[d.parity] + f * A.x_stride;
   const int m = d.m;
@@ -875,11 +1159,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     sh.u[tid] = u;
   }
   if (tid == 0) sh.nu_cnt = 3 + 2 * m;
-  // the next descriptor: here when waves 1–2 rebuild the next block (they need it during the
-  // corrections), else in the epilogue (off this barrier's path)
-  if (A.nb && ci + 1 < nchunks && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
+  // the next descriptor: here with a builder (waves 1–2 publish their progress for it when it
+  // builds the next chunk's block), else in the epilogue (off this barrier's path)
+  if (A.build && ci + 1 < nchunks && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
     reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
-        &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
+        &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + fy])[tid - 128];
   if (look && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0)
     const int pm = d.prev_m;
     int u = 0;
@@ -898,11 +1182,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   lds_barrier();
   EKF_STAMP(1);
   const int nu = sh.nu_cnt;
-  // The next chunk's block is rebuilt by waves 1–2 during this chunk's corrections (device epochs,
-  // staged operands, not after a Joseph chunk: its rank-4 factor stays with the prologue).
+  // The builder rebuilds the next chunk's block during this chunk's corrections (device-epoch
+  // launches, staged operands, not after a Joseph chunk: its rank-4 factor stays with the prologue)
   const MsgDesc& nd = sdesc[(ci + 1) & 1];
-  constexpr int kNbFlags = kActive | kLook | kStageIn;
-  const bool nbw = A.nb && ci + 1 < nchunks && !joseph && (nd.flags & kNbFlags) == kNbFlags;
+  const bool bnext = A.build && ci + 1 < nchunks && build_pred(d, nd);
 
   // ---- A1: every global load of the prologue in one round ---------------------------------------
   // Each thread issues all of its loads before its first LDS store: indices are clamped rather
@@ -916,7 +1199,28 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const T* Sp = A.sig[d.parity ^ 1] + f * A.sig_stride;
     const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
     const int np = sh.pv.nu;
-    if (!built) {  // (built: R̃, K', M', P̃ and the record's scalars are in LDS already)
+    if (built) {  // the builder's P̃ (before this chunk's predict), R̃ and x_in' at U (its epoch was
+                  // acquired above); x[U'], Zx' of the chunk before and t_map_odom are in LDS already
+      const BuildRec* bo = A.bout + static_cast<size_t>(d.parity) * A.rec_stride + f;
+      constexpr int kBP = (kMaxU * kMaxU + kChainThreads - 1) / kChainThreads;  // 5
+      double bp[kBP], br[kBP];
+#pragma unroll
+      for (int i = 0; i < kBP; ++i) {
+        const int e = min(tid + i * kChainThreads, kMaxU * kMaxU - 1);
+        bp[i] = bo->P[e / kMaxU][e % kMaxU];
+        br[i] = bo->R[e / kMaxU][e % kMaxU];
+      }
+      const double bx = bo->xg[tid < kMaxU ? tid : 0];
+#pragma unroll
+      for (int i = 0; i < kBP; ++i) {
+        const int e = tid + i * kChainThreads, a = e / kMaxU, b = e % kMaxU;
+        if (a < nu && b < nu) P[a][b] = bp[i];
+        if (a < nu) sh.pv.R[a][b] = br[i];
+      }
+      if (tid < kMaxU) sh.pv.xg[tid] = bx;
+      __syncthreads();
+    }
+    if (!built) {  // (built: R̃ and P̃ came from the builder)
     const int tc = tid < kMaxU ? tid : 0;
     if (!early) {  // (early: the staged operands and the record's values are in registers)
 #pragma unroll
@@ -973,56 +1277,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     if (tid < 3) sh.tmo[tid] = tq;
     __syncthreads();
     EKF_STAMP(21);
-    // the previous predict on the gathered values: v + α_i·Σ[0][j] + (Σ[i][0] + α_i·Σ00)·α_j + Q̄;
-    // R / C columns k ≥ |U'| up to 36 are zeroed (MFMA k padding)
-    const bool pf = sh.pv.first != 0;
-    const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
-    // every LDS read of the six entries first (clamped indices, no branch around a read): one
-    // LDS round instead of a wait per predicated read
-    double r0Ub[kPer], r0Ua[kPer], c0Ua[kPer], r0Pb[kPer], c0Pb[kPer];
-    int ua[kPer], ub[kPer], pu[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = tid + i * kChainThreads;
-      const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
-      ua[i] = sh.u[a];
-      ub[i] = sh.u[b];
-      pu[i] = sh.pv.u[b];
-      r0Ub[i] = sh.pv.r0U[b];
-      r0Ua[i] = sh.pv.r0U[a];
-      c0Ua[i] = sh.pv.c0U[a];
-      r0Pb[i] = sh.pv.r0P[b];
-      c0Pb[i] = sh.pv.c0P[b];
-    }
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = tid + i * kChainThreads;
-      const int a = e / kW, b = e % kW;
-      double v = static_cast<double>(vd[i]), vR = 0.0, wC = 0.0;
-      if (b < np) {
-        vR = static_cast<double>(vr[i]);
-        wC = static_cast<double>(vc[i]);
-      }
-      if (pf) {
-        const double ai = alpha_of(ua[i], qa1, qa2), aj = alpha_of(ub[i], qa1, qa2);
-        const double ak = alpha_of(pu[i], qa1, qa2);
-        v = v + ai * r0Ub[i];
-        v = v + (c0Ua[i] + ai * s00) * aj;
-        v = (ua[i] == ub[i] && ua[i] < 3) ? v + A.q : v;
-        double v2 = vR + ai * r0Pb[i];
-        v2 = v2 + (c0Ua[i] + ai * s00) * ak;
-        double w2 = wC + ak * r0Ua[i];
-        w2 = w2 + (c0Pb[i] + ak * s00) * ai;
-        const bool qd = ua[i] == pu[i] && ua[i] < 3;
-        vR = b < np ? (qd ? v2 + A.q : v2) : 0.0;
-        wC = b < np ? (qd ? w2 + A.q : w2) : 0.0;
-      }
-      if (a < nu && b < nu) P[a][b] = v;
-      if (a < nu) {  // b = k over U' (36: the MFMA k padding, zero)
-        sh.pv.R[a][b] = vR;
-        sh.pv.C[b][a] = wC;
-      }
-    }
+    rebuild_rcd<T>(sh, P, vd, vr, vc, tid, nu, np, A.q);
     __syncthreads();
     EKF_STAMP(3);
     EKF_STAMP(4);
@@ -1131,30 +1386,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
       if (ln < 3) sh.xpose[ln] = sh.pv.xU[ln];  // pose ∈ U' always
     }
-#ifdef EKF_DIAG_STAMPS
-    if (nbchk) {
-      __syncthreads();
-      nb_snapshot(sh, P, 1);
-      __threadfence();
-      __syncthreads();
-      if (tid == 0) {
-        bool bad = false;
-        for (int a = 0; a < nu && !bad; ++a)
-          for (int b = 0; b < nu; ++b)
-            if (__double_as_longlong(g_nb[0][4][a][b]) != __double_as_longlong(g_nb[1][4][a][b])) bad = true;
-        g_nbinfo[2] += 1;
-        if (bad) {
-          g_nbinfo[0] += 1;
-          g_nbinfo[1] = seq;
-          g_nbinfo[3] = 1;
-          g_nbinfo[4] = nu;
-          g_nbinfo[5] = np;
-          g_nbinfo[6] = sh.pv.m;
-        }
-      }
-      __syncthreads();
-    }
-#endif
   } else {
     double vd[kPer];
 #pragma unroll
@@ -1245,10 +1476,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     sh.pub = 0;
     sh.pdone = 0;
     sh.any_init = 0;
-    sh.kdone = 0;
-    sh.w1fin = 0;
-    sh.nb_ok1 = 0;
-    sh.nb_ok2 = 0;
   }
   if (pending) drain_stores();
   __syncthreads();
@@ -1308,10 +1535,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
     const int li = lane < kMaxU ? lane : kMaxU - 1;
-    const StageRec<T>* sgn = A.stage + static_cast<size_t>(nd.parity) * A.rec_stride + f;
-    const int nun = 3 + 2 * nd.m;
-    bool land = false;
-    int kb = 0;
+    unsigned* zprog = sync_word(A, kSyncKindZ, f);
+    if (bnext) {  // the builder of the next chunk: this chunk's predict parameters
+      if (lane == 0) {
+        st_wt(&A.chan[f].a1, sh.a1);
+        st_wt(&A.chan[f].a2, sh.a2);
+      }
+      drain_stores();
+      if (lane == 0) epoch_store(sync_word(A, kSyncKindPro, f), seq + 1u);
+    }
     double zxa = 0.0;  // Σ_c Z_c ν_c of row `lane`, accumulated as the Z_c come (the record's Zx)
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
@@ -1386,30 +1618,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           }
         }
       }
-      if (nbw) {  // the next chunk's K' columns of the complete k-blocks
-        if (!land && nb_landed(A.sync, seq)) {
-          EKF_STAMPT(300, 64);
-          nb_intake_r<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, nu, nun, first, A.q, A.N);
-          EKF_STAMPT(306, 64);
-          land = true;
-        }
-        if (land) kb = nb_ktiles((LdsChain*)(&sh), kb, (c + 1) >> 1, m, nu);
+      if (bnext) {  // Z_c complete in the record: the builder may take it
+        drain_stores();
+        if (lane == 0) epoch_store(zprog, (seq << 5) | static_cast<unsigned>(c + 1));
       }
       EKF_STAMPT(320 + c, 64);
     }
     if (lane < kMaxU) sh.Zx[lane] = zxa;
-    if (nbw) {  // (m odd: the last k-block's second pair of columns is zero)
-      if (!land && nb_landed(A.sync, seq)) {
-        EKF_STAMPT(300, 64);
-        nb_intake_r<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, nu, nun, first, A.q, A.N);
-        land = true;
-      }
-      EKF_STAMPT(305, 64);
-      if (land) kb = nb_ktiles((LdsChain*)(&sh), kb, (m + 1) >> 1, m, nu);
-      EKF_STAMPT(301, 64);
-      if (lane == 0) sh.nb_ok1 = land ? 1 : 0;
-      lds_publish(&sh.w1fin, 1);
-    }
   } else {  // wave 2: Y_c: M_c[:, j] = Y_c·c_0(j) for every column j; Y_c to the record at once
     // Σ_c[pA_c, j] = (E_cᵀ − Σ_{k<c} K_k[pA_c]·Y_k)·c_0(j), so Y_c = H·E_cᵀ − Σ_{k<c} D_k·Y_k with
     // D_k = H·K_k[pA_c] (2×2): lane k forms D_k, lane j its column of Y_c.
@@ -1417,10 +1632,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     for (int e = lane; e < (kZC - 2 * m) * kMaxU; e += 64)  // rows ≥ 2m of the record's Y are zero
       st_wt(&(&rec->Y[2 * m][0])[e], 0.0);
     const int lj = lane < kMaxU ? lane : kMaxU - 1;
-    const StageRec<T>* sgn = A.stage + static_cast<size_t>(nd.parity) * A.rec_stride + f;
-    const int nun = 3 + 2 * nd.m, pn = (ci + 1) & 1;
-    bool land = false;
-    int mb = 0, pb = 0;
+    unsigned* yprog = sync_word(A, kSyncKindY, f);
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1476,48 +1688,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           st_wt(&rec->Y[2 * c + 1][lane], in ? y1 : 0.0);
         }
       }
-      if (nbw) {  // the next chunk's M' rows, then P̃ −= K'·M' over the k-blocks wave 1 has done
-        if (!land && nb_landed(A.sync, seq)) {
-          EKF_STAMPT(302, 128);
-          nb_intake_cd<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, pn, nu, nun, first, A.q, A.N);
-          EKF_STAMPT(307, 128);
-          land = true;
-        }
-        if (land) {
-          mb = nb_mtiles((LdsChain*)(&sh), mb, (c + 1) >> 1, m, nu);
-          EKF_STAMPT(340 + c, 128);
-          const int kd = min(mb, __builtin_amdgcn_readfirstlane(
-                                     __hip_atomic_load(&sh.kdone, __ATOMIC_ACQUIRE,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP)));
-          for (; pb < kd; ++pb) nb_pblock((LdsChain*)(&sh), pn, pb, nun);
-        }
+      if (bnext) {  // Y_c complete in the record: the builder may take it
+        drain_stores();
+        if (lane == 0) epoch_store(yprog, (seq << 5) | static_cast<unsigned>(c + 1));
       }
       EKF_STAMPT(360 + c, 128);
-    }
-    if (nbw) {
-      if (!land && nb_landed(A.sync, seq)) {
-        EKF_STAMPT(302, 128);
-        nb_intake_cd<T>((LdsChain*)(&sh), (LdsDesc*)(&nd), sgn, pn, nu, nun, first, A.q, A.N);
-        land = true;
-      }
-      const int nk = (m + 1) >> 1;
-      if (land) {
-        mb = nb_mtiles((LdsChain*)(&sh), mb, nk, m, nu);
-        while (pb < nk) {  // wave 1 ends with kdone = nk, or without (no stage yet): w1fin either way
-          int kd;
-          for (;;) {
-            const int fin = __hip_atomic_load(&sh.w1fin, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            kd = __hip_atomic_load(&sh.kdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            kd = __builtin_amdgcn_readfirstlane(kd);
-            if (kd > pb || __builtin_amdgcn_readfirstlane(fin)) break;
-            __builtin_amdgcn_s_sleep(1);
-          }
-          if (kd <= pb) break;
-          for (; pb < kd; ++pb) nb_pblock((LdsChain*)(&sh), pn, pb, nun);
-        }
-      }
-      if (lane == 0) sh.nb_ok2 = land && pb == nk ? 1 : 0;
-      EKF_STAMPT(303, 128);
     }
   }
   __syncthreads();
@@ -1555,8 +1730,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // the prologue's poll.
   const double* xfin = sh.xU[0];
   const bool pre_next = ci + 1 < nchunks;
-  const bool nb_ok = nbw && sh.nb_ok1 && sh.nb_ok2;  // waves 1–2 rebuilt the next chunk's block
-  if (nb_ok && tid == 0) sh.built = seq + 1u;
   if (wave == 3) {
     if (lane == 0) {
       if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
@@ -1571,16 +1744,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
   } else {
-    if (!A.nb && pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
+    if (!A.build && pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
       reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
-          &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + blockIdx.y])[tid - 128];
+          &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + fy])[tid - 128];
     if (tid == 0 && sh.status) atomicOr(&ctl->status, sh.status);
     // hand the chunk to the factor kernel (and the next chain): write-through record
     ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
     if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
       const double zx = sh.Zx[tid];  // (wave 1's sum over the corrections)
       const bool in = tid < nu;
-      if (nb_ok) {  // what the next chunk's prologue reads from the record
+      if (bnext) {  // what the next chunk's prologue reads from the record
         sh.pv.Zx[tid] = zx;
         sh.pv.xU[tid] = in ? xfin[tid] : 0.0;
       }
@@ -1605,6 +1778,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   pre = pre_next;
   __syncthreads();
   EKF_STAMP(40);
+  EKF_STAMPV(307, __builtin_amdgcn_s_memrealtime());
   }  // chunk loop
   if (pending) {
     drain_stores();
@@ -2402,7 +2576,10 @@ void launch(K kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t e0, hipEv
 template <typename T>
 hipError_t launch_chain(const PassArgs<T>& a, int nf, int nchunks, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1) {
-  launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a, nchunks);
+  if (a.build)  // chain + builder per filter, 16 blocks per 8 filters (k_chain)
+    launch(k_chain<T>, dim3(16 * ((nf + 7) / 8)), dim3(kChainThreads), s, e0, e1, a, nchunks);
+  else
+    launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a, nchunks);
   return hipGetLastError();
 }
 
@@ -2501,10 +2678,3 @@ EKF_INSTANTIATE(float)
 
 }  // namespace ekfslam
 
-#ifdef EKF_DIAG_STAMPS
-extern "C" int ekfslam_diag_read_nb(double* out, unsigned* info) {
-  using namespace ekfslam;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nb), sizeof(g_nb)) != hipSuccess) return -5;
-  return hipMemcpyFromSymbol(info, HIP_SYMBOL(g_nbinfo), sizeof(g_nbinfo)) == hipSuccess ? 0 : -5;
-}
-#endif

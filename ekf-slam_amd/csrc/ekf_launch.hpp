@@ -36,9 +36,14 @@ struct PassArgs {
                         // the bulk stream before it, and the last pass published no epoch)
   int polls;            // 1: the streams hand off through device epochs (kernels poll them);
                         // 0: stream order / events order everything, no poll and no epoch kernel
-  int nb;               // chain (polls only): waves 1–2 rebuild the next chunk's block during the
-                        // corrections (EKF_NB=1; off by default: the staged operands land too late
-                        // in the chunk at N = 1024)
+  int build;            // chain launches of > 1 chunk with device epochs, EKF_BUILD=1: a builder
+                        // workgroup per filter rebuilds each next chunk's block during the
+                        // corrections (k_chain: 1-D grid, chain of filter f = block 16·⌊f/8⌋ +
+                        // f mod 8, builder 8 later, both on XCD f mod 8); 0 (default): every
+                        // chunk's prologue rebuilds its own
+  int nf_launch;        // filters of the launch (build: the 1-D grid's bound)
+  BuildRec* bout;       // [2][rec_stride] the builder's blocks
+  BuildChan* chan;      // [rec_stride] the chain's predict parameters for the builder
   const MsgDesc* desc;
   int desc_stride;      // descriptors between consecutive chunks of a chain launch
   int n, ld, N, f0;

@@ -19,6 +19,7 @@ EKF_OK, EKF_E_ARG, EKF_E_RANGE, EKF_E_EMPTY, EKF_E_NUMERIC, EKF_E_HIP, EKF_E_NOM
 EKF_E_TIMEOUT = -7
 EKF_FLAG_RANGE, EKF_FLAG_NUMERIC, EKF_FLAG_TIMEOUT = 1, 2, 4
 EKF_ASSOC_MARKER, EKF_ASSOC_CHUNK, EKF_ASSOC_CHUNK_XCD = 0, 1, 2
+EKF_SCHED_DEVSYNC, EKF_SCHED_BUILDER, EKF_SCHED_SERIAL = 1, 2, 4
 EKF_F64, EKF_F32 = 0, 1
 EKF_PATH_PIPELINE, EKF_PATH_RESIDENT = 0, 1
 ADD, DELETE = 0, 2
@@ -27,7 +28,7 @@ SOURCE_SIM, SOURCE_ASSOC = 0, 1
 # every symbol include/ekf.h and include/slam_core.h declare
 EXPORTS = [
     "ekf_config_default", "ekf_strerror", "ekf_create", "ekf_destroy", "ekf_dims", "ekf_get_path",
-    "ekf_get_assoc_route",
+    "ekf_get_assoc_route", "ekf_get_schedule",
     "ekf_set_odom",
     "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_replay_device",
     "ekf_predict",
@@ -87,6 +88,7 @@ def lib():
             "ekf_dims": (_i, [_vp, _ip, _ip, _ip]),
             "ekf_get_path": (_i, [_vp, _ip]),
             "ekf_get_assoc_route": (_i, [_vp, _ip]),
+            "ekf_get_schedule": (_i, [_vp, _ip]),
             "ekf_set_odom": (_i, [_vp, _i, _d, _d, _d]),
             "ekf_fake_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
             "ekf_sensor": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
@@ -198,6 +200,8 @@ class EKF:
         self.path = p.value  # EKF_PATH_PIPELINE | EKF_PATH_RESIDENT
         _check(lib().ekf_get_assoc_route(self.h, C.byref(p)), "ekf_get_assoc_route")
         self.assoc_route = p.value  # EKF_ASSOC_*
+        _check(lib().ekf_get_schedule(self.h, C.byref(p)), "ekf_get_schedule")
+        self.schedule = p.value  # EKF_SCHED_* bits
 
     def close(self):
         if getattr(self, "h", None):

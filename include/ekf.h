@@ -96,6 +96,19 @@ int ekf_get_path(ekf_t h, int* path);
 #define EKF_ASSOC_CHUNK_XCD 2
 int ekf_get_assoc_route(ekf_t h, int* route);
 
+/* The handle's schedule (fixed at ekf_create), bit flags:
+ *   EKF_SCHED_DEVSYNC  the chain and bulk streams hand off through device epochs (<= 32 filters,
+ *                      disjoint CU masks; EKF_DEVSYNC=0 or more filters: HIP events);
+ *   EKF_SCHED_BUILDER  multi-chunk chain launches run a builder workgroup per filter that
+ *                      rebuilds each next chunk's block during the corrections (opt-in,
+ *                      EKF_BUILD=1, <= 16 filters; slower than the chain's own rebuild so far);
+ *   EKF_SCHED_SERIAL   every kernel on one stream (EKF_SERIAL=1).
+ * Every schedule gives bit-identical results. */
+#define EKF_SCHED_DEVSYNC 1
+#define EKF_SCHED_BUILDER 2
+#define EKF_SCHED_SERIAL 4
+int ekf_get_schedule(ekf_t h, int* flags);
+
 /* ---- the callbacks (fast path) ---- */
 
 /* t_odom_robot ← DiffDrive::FKin output (slam.cpp:633, jointStateCallback :599-634). */

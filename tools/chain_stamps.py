@@ -3,8 +3,8 @@ pipelined replay (libekfslam_diag.so; build: make -C ekf-slam_amd diag).
 
   python tools/chain_stamps.py [N] [f32|f64]   (default 1024 f32: configs[2]'s headline shape —
   the fp64 survey lap, then fp32 circle messages from its state, as bench.py runs it)
-  EKF_NB=1 NBCHK=1: with the helper-wave rebuild on, every chunk it built also runs the
-  prologue's rebuild; prints how many of the two blocks differ (and where, for the first one)"""
+  With the block builder (the default of a one-filter device-epoch handle) also its phases
+  during the chunk before."""
 import ctypes as C
 import os
 import sys
@@ -62,12 +62,20 @@ print(f"N={N} {DT}, chunk {-1 - int(os.environ.get('WHICH', '1'))} of {T} messag
       f"the chunk's stamp 0); chunk starts of the ring, relative: {sorted(ring[:, 0] - ring[:, 0].min())}")
 for k in (1, 21, 3, 7, 5, 6, 2, 12, 16, 40):
     print(f"{names[k]:24s} {s[k] - t0:8d}")
-print(f"built by the chunk before: {s[304]}; next-chunk rebuild (waves 1-2): w1 landed {s[300] - t0}, "
-      f"w1 loop end {s[305] - t0}, w1 done {s[301] - t0}, w2 landed {s[302] - t0}, w2 done {s[303] - t0}")
-print(f"  w1 intake done {s[306] - t0}, w2 intake done {s[307] - t0}")
-print("  w1 step ends:", [int(s[320 + c] - t0) for c in range(16)])
-print("  w2 mtiles ends:", [int(s[340 + c] - t0) for c in range(16)])
-print("  w2 step ends:", [int(s[360 + c] - t0) for c in range(16)])
+print(f"built by the builder: {s[304]}; its epoch acquired at {s[305] - t0}")
+# the builder rebuilt this chunk's block during the chunk before: its phases in µs (s_memrealtime,
+# 100 MHz, chip-wide) from the chunk before's start, in this chunk's ring slot
+prev = ring[order[int(os.environ.get("WHICH", "1")) + 1]]
+if s[304] and prev[306]:
+    p0 = prev[306]
+    rel = lambda k: round((int(s[k]) - int(p0)) / 100.0, 2) if s[k] else None  # noqa: E731
+    print("builder, µs from the chunk before's start:", {"start": rel(400),
+          "stage+predict in": rel(401), "intake done": rel(402), "done": rel(440)})
+    print("  K' done through k-block:", {k: rel(409 + k) for k in range(1, 9) if s[409 + k]})
+    print("  M' done through k-block:", {k: rel(419 + k) for k in range(1, 9) if s[419 + k]})
+    print("  P done through k-block:", {k: rel(429 + k) for k in range(1, 9) if s[429 + k]})
+    print("  chunk before's end:", rel_end := round((int(prev[307]) - int(p0)) / 100.0, 2),
+          " this chunk's start:", round((int(s[306]) - int(p0)) / 100.0, 2))
 m = int(sc.count[w + T - 1 - int(os.environ.get("WHICH", "1"))])
 steps = [int(s[64 + 8 * c] - t0) for c in range(m)]
 print("step starts:", steps)
@@ -79,25 +87,3 @@ for c in (0, 1, m // 2, m - 2):
           f"  geometry(c+1)+cross update {s[b + 6] - s[b + 4]}  -> next {s[b + 8] - s[b + 6]}")
     print(f"   wave3: pub seen at {s[192 + 2 * c] - s[b]}, pdone at {s[193 + 2 * c] - s[b]} "
           f"(wave0 publish at {s[b + 4] - s[b]}, next-step pdone wait at {s[b + 8 + 2] - s[b]})")
-if os.environ.get("NBCHK"):
-    # the diag build's g_nb / g_nbinfo (device symbols) through the lib's diag accessor
-    L.ekf_diag_nb.argtypes = [C.c_void_p, C.c_void_p]
-    buf = np.zeros((2, 6, 36, 36))
-    info = np.zeros(8, dtype=np.uint32)
-    assert L.ekf_diag_nb(buf.ctypes.data, info.ctypes.data) == 0
-    print("nb check: mismatching chunks", info[0], "first seq", info[1], "checked", info[2],
-          "nu", info[4], "np", info[5], "pm", info[6])
-    if info[0]:
-        nu, np_ = int(info[4]), int(info[5])
-        for k, nm in enumerate(["R", "C", "K", "M", "P", "vec"]):
-            d = buf[0][k] != buf[1][k]
-            if nm == "R": d = d[:nu, :36]
-            if nm == "P": d = d[:nu, :nu]
-            idx = np.argwhere(d)
-            print(nm, "mismatches", len(idx), idx[:8].tolist())
-            if nm == "vec":
-                for r in range(9):
-                    print("   vec row", r, buf[0][5][r, :6], buf[1][5][r, :6])
-            for a, b in idx[:4]:
-                print("   ", a, b, buf[0][k][a, b], buf[1][k][a, b])
-e.close()
