@@ -76,8 +76,7 @@ struct AmShared {
 // Σ_p[a][k] = Σ[a][k] + α_a·Σ[0][k] (k_assoc's expressions; At has α only in rows 1, 2).
 template <typename T>
 __device__ __forceinline__ void slot_block(const T* S, int ld, int ix, double a1, double a2,
-                                           double (&kk)[4], double (&kp)[6], double (&pk)[6],
-                                           double (&c0)[2], double (&r0)[2]) {
+                                           double (&kk)[4], double (&kp)[6], double (&pk)[6]) {
   const T* q0 = S + static_cast<size_t>(ix) * ld;
   const T* q1 = q0 + ld;
   double rk[2][3], rp[3][2];
@@ -103,10 +102,6 @@ __device__ __forceinline__ void slot_block(const T* S, int ld, int ix, double a1
   for (int a = 0; a < 3; ++a)
 #pragma unroll
     for (int e = 0; e < 2; ++e) pk[2 * a + e] = rp[a][e] + alpha_of(a, a1, a2) * rp[0][e];
-  c0[0] = rk[0][0];
-  c0[1] = rk[1][0];
-  r0[0] = rp[0][0];
-  r0[1] = rp[0][1];
 }
 
 __device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long* p) {
@@ -355,7 +350,9 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   double pose[3], a1, a2;
   predicted_pose(ctl->tmo, d, xin, pose, &a1, &a2);
   const bool first = (flags & kFirst) != 0;
-  double Pp[3][3], raw[3][3];
+  double Pp[3][3];
+  {
+  double raw[3][3];
 #pragma unroll
   for (int a = 0; a < 3; ++a)
 #pragma unroll
@@ -370,9 +367,10 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       if (first && a == b) v += A.q;
       Pp[a][b] = v;
     }
+  }  // (raw: re-read for the factor rows at the end, not kept live through the steps)
   // the lane's slot: its predicted block and state
-  double kk[4], kp[6], pk[6], c0[2], r0[2];
-  slot_block(S, ld, ix, a1, a2, kk, kp, pk, c0, r0);
+  double kk[4], kp[6], pk[6];
+  slot_block(S, ld, ix, a1, a2, kk, kp, pk);
   double xk[2] = {xin[ix], xin[ix + 1]};
   unsigned s = ctl->counter;
 
@@ -450,11 +448,14 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     if (j >= 0) {
       const int jx = 3 + 2 * j;
       // the new landmark's state (slam.cpp:351-354, the pose before this marker's correction)
-      const double nx = pose[1] + z0 * cos(z1 + pose[0]);
-      const double ny = pose[2] + z0 * sin(z1 + pose[0]);
-      if (isnew && k == j) {
-        xk[0] = nx;
-        xk[1] = ny;
+      double nx = 0.0, ny = 0.0;
+      if (isnew) {  // (uniform)
+        nx = pose[1] + z0 * cos(z1 + pose[0]);
+        ny = pose[2] + z0 * sin(z1 + pose[0]);
+        if (k == j) {
+          xk[0] = nx;
+          xk[1] = ny;
+        }
       }
       // ---- j's block, state and history (one round of sc1 loads), crosses from Σ_in ----
       double v[3];
@@ -736,6 +737,10 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   // k_factors writes them), zero rows up to the pass's rank kw ----
   const int kw = ((2 + 2 * m + 3) / 4) * 4;
   if (valid) {
+    // Σ_in[ix + e][0] and Σ_in[0][ix + e] (raw, as slot_block read them)
+    const double c0[2] = {static_cast<double>(S[static_cast<size_t>(ix) * ld]),
+                          static_cast<double>(S[static_cast<size_t>(ix + 1) * ld])};
+    const double r0[2] = {static_cast<double>(S[ix]), static_cast<double>(S[ix + 1])};
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       kc[0 * ldk + ix + e] = static_cast<T>(0.0);                  // −α_i = 0 for landmark rows
@@ -752,10 +757,10 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   }
   if (g == 0 && lane < 3) {
     const double al = alpha_of(lane, a1, a2);
-    const double rc0 = lane == 0 ? raw[0][0] : (lane == 1 ? raw[1][0] : raw[2][0]);
-    const double r0c = lane == 0 ? raw[0][0] : (lane == 1 ? raw[0][1] : raw[0][2]);
+    const double rc0 = static_cast<double>(S[lane * ld]), r0c = static_cast<double>(S[lane]);
+    const double s00 = static_cast<double>(S[0]);
     kc[0 * ldk + lane] = static_cast<T>(first ? -al : 0.0);
-    kc[1 * ldk + lane] = static_cast<T>(first ? -(rc0 + al * raw[0][0]) : 0.0);
+    kc[1 * ldk + lane] = static_cast<T>(first ? -(rc0 + al * s00) : 0.0);
     mc[0 * ldk + lane] = static_cast<T>(first ? r0c : 0.0);
     mc[1 * ldk + lane] = static_cast<T>(first ? al : 0.0);
     for (int rr = 2 + 2 * m; rr < kw; ++rr) {

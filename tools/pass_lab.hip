@@ -403,6 +403,121 @@ void launch_x4(const PassArgs<float>& a, hipStream_t s) {
                      dim3(64 * WPB), 0, s, a, tcols);
 }
 
+// Operands through LDS-DMA: the wave's K rows (34 × 128 B at R0) and M rows (34 × 128 B at C0)
+// land in its LDS image by 4 buffer_load_dwordx4 … lds + 1 buffer_load_dword … lds each (10 VMEM
+// instructions instead of 34 dword loads), read back as the MFMA operands by ds_read_b32. SIG:
+// Σ_in as the product (16 dword loads into registers, issued after the DMA so the operand
+// reads wait for vmcnt(16), not vmcnt(0)); else Σ_in also by LDS-DMA (4 dwordx4) into a
+// lane-linear 32 × 32 image, read back in the MFMA layout.
+typedef __attribute__((address_space(3))) void lds_void;
+template <int WPB, bool SIG_REGS>
+__global__ __launch_bounds__(64 * WPB) void k_lab_glds(PassArgs<float> A, int tcols) {
+  using Tile = SigmaTile<float>;
+  constexpr int kImg = 34 * 32;  // floats per operand image
+  __shared__ float lds[WPB][2 * kImg + (SIG_REGS ? 0 : 32 * 32)];
+  const MsgDesc& d = A.desc[0];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const int trows = (n + 31) / 32;
+  const int x = blockIdx.x & 7, w = (blockIdx.x >> 3) * WPB + wv;
+  const int hx = x / kRegCols, qx = x % kRegCols;
+  const int r0 = hx * trows / kRegRows, r1 = (hx + 1) * trows / kRegRows;
+  const int c0 = qx * tcols / kRegCols, c1 = (qx + 1) * tcols / kRegCols;
+  const int cw = c1 - c0;
+  const int tt = __builtin_amdgcn_readfirstlane(w);
+  if (tt >= (r1 - r0) * cw) return;
+  const int tr = r0 + tt / cw, tc = c0 + tt % cw;
+  const int R0 = tr * 32, C0 = tc * 32;
+  // descriptor read before the DMA: a use of a vector load issued later would wait for vmcnt(0)
+  const int kw = __builtin_amdgcn_readfirstlane(((2 + 2 * d.m + 3) / 4) * 4);
+  const bool first = (__builtin_amdgcn_readfirstlane(d.flags) & kFirst) != 0;
+  float* Ki = lds[wv];
+  float* Mi = Ki + kImg;
+  float* Si = Mi + kImg;
+  const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 4u;
+  const auto rk = buf_rsrc(A.kcat, kbytes), rm = buf_rsrc(A.mcat, kbytes);
+  {
+    const unsigned o16 = static_cast<unsigned>((lane >> 3) * ldk + 4 * (lane & 7)) * 4u;
+    const unsigned o4 = static_cast<unsigned>((32 + (lane >> 5)) * ldk + (lane & 31)) * 4u;
+    const unsigned kr0 = static_cast<unsigned>(R0) * 4u, mc0 = static_cast<unsigned>(C0) * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void*)(Ki + 256 * i), 16, o16 + kr0, i * 8 * ldk * 4, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_void*)(Mi + 256 * i), 16, o16 + mc0, i * 8 * ldk * 4, 0, 0);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (lds_void*)(Ki + 1024), 4, o4 + kr0, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_void*)(Mi + 1024), 4, o4 + mc0, 0, 0, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const auto rin = Tile::panel(A.sig[0], n, ld, R0);
+  const unsigned rstride = static_cast<unsigned>(ld) * 4u;
+  const unsigned so = Tile::soff(n, ld, C0, lane);
+  float sv[16];
+  if (SIG_REGS) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[r] = ld_f32(rin, so + ((r & 3) + 8 * (r >> 2)) * rstride, 0);
+  } else {
+    // lane l: row 8i + (l >> 3), columns 4(l & 7)..+3 (columns ≥ ld lie in the next row: unused)
+    const unsigned s16 = static_cast<unsigned>((lane >> 3) * ld + C0 + 4 * (lane & 7)) * 4u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void*)(Si + 256 * i), 16, s16, i * 8 * rstride, 0, 0);
+  }
+  // the compiler does not order LDS reads after an LDS-DMA: counted waits by hand
+  __builtin_amdgcn_sched_barrier(0);
+  if (SIG_REGS) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  const int kr = lane >> 5, kcol = lane & 31;
+  f16v acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  // operand reads in inline asm: the compiler's own wait for them would be vmcnt(0) (it cannot
+  // tell the operand images from the Σ DMA still in flight)
+  float av[kSteps], bv[kSteps];
+  {
+    typedef __attribute__((address_space(3))) float lds_f;
+    const unsigned ka = static_cast<unsigned>(reinterpret_cast<size_t>((lds_f*)(Ki + kr * 32 + kcol)));
+    const unsigned ma = static_cast<unsigned>(reinterpret_cast<size_t>((lds_f*)(Mi + kr * 32 + kcol)));
+#pragma unroll
+    for (int s2 = 0; s2 < kSteps; ++s2) {
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(av[s2]) : "v"(ka), "i"(256 * s2));
+      asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(bv[s2]) : "v"(ma), "i"(256 * s2));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s2 = 0; s2 < kSteps; ++s2) {
+    const bool live = 2 * s2 < kw;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(live ? av[s2] : 0.0f, live ? bv[s2] : 0.0f, acc, 0, 0, 0);
+  }
+  if (!SIG_REGS) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[r] = Si[((r & 3) + 8 * (r >> 2) + 4 * kr) * 32 + kcol];
+  }
+  const auto rout = Tile::panel(A.sig[1], n, ld, R0);
+  const float q = static_cast<float>(A.q);
+  const int col = C0 + kcol;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
+    float v = sv[r] - acc[r];
+    if (first && row == col && row < 3) v += q;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout,
+                                          so + ((r & 3) + 8 * (r >> 2)) * rstride, 0, 0);
+  }
+}
+template <int WPB, bool SIG_REGS>
+void launch_glds(const PassArgs<float>& a, hipStream_t s) {
+  const int trows = (a.n + 31) / 32, tcols = trows;
+  hipLaunchKernelGGL((k_lab_glds<WPB, SIG_REGS>), dim3(8 * ((region_tiles(trows, tcols) + WPB - 1) / WPB)),
+                     dim3(64 * WPB), 0, s, a, tcols);
+}
+
 template <int WPB, int PRIO>
 void launch_region(const PassArgs<float>& a, hipStream_t s) {
   const int trows = (a.n + 31) / 32, tcols = (a.n + 31) / 32;
@@ -497,10 +612,10 @@ int main(int argc, char** argv) {
   for (int round = 0; round < 2; ++round) {
     time_it("product k_sigma_pass", prod);
     time_it("region wpb4", [&](hipStream_t st) { launch_region<4, 0>(a, st); });
-    time_it("stagger wg 0.5us", [&](hipStream_t st) { launch_region<4, kStag1>(a, st); });
-    time_it("stagger wg 1us", [&](hipStream_t st) { launch_region<4, kStag2>(a, st); });
-    time_it("stagger wave 0.5us", [&](hipStream_t st) { launch_region<4, kStag1 | kStagW>(a, st); });
-    time_it("stagger wave 1us", [&](hipStream_t st) { launch_region<4, kStag2 | kStagW>(a, st); });
+    time_it("glds ops, sig regs", [&](hipStream_t st) { launch_glds<4, true>(a, st); });
+    time_it("glds ops + sig", [&](hipStream_t st) { launch_glds<4, false>(a, st); });
+    time_it("glds ops, sig regs w2", [&](hipStream_t st) { launch_glds<2, true>(a, st); });
+    time_it("glds ops + sig w2", [&](hipStream_t st) { launch_glds<2, false>(a, st); });
   }
   return 0;
 }
