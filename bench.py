@@ -513,9 +513,8 @@ def run(args, rank, world, local, backend=None):
     if trace:
         clk.append(("enqueued", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                     time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
-    if backend is not None:
-        ekf.sync()  # (a CPU stand-in backend: its own sync; on the GPU the device-wide sync below
-    be.sync()       # waits for every stream of the library — ekf_replay has enqueued everything)
+    ekf.sync()  # the library's streams
+    be.sync()   # device-wide (torch.cuda.synchronize on the GPU): nothing may be left running
     # this rank's own region (its K messages, enqueue to device-wide sync); the closing barrier
     # aligns the ranks, and reduce_ranks takes the MAX of these over ranks
     elapsed = time.perf_counter() - t0

@@ -20,6 +20,7 @@ constexpr int kZC = 2 * kMaxChunk;               // correction columns of Z / ro
 
 // Device epochs (unsigned words of the handle's sync buffer, each polled word on its own line):
 constexpr int kSyncSigma = 0;    // epoch (seq + 1) of the last complete Σ pass (k_sigma_epoch)
+constexpr int kSyncPlan = 1;     // (t, f) descriptors device replays have planned so far (a count)
 constexpr int kSyncChain = 64;   // [F]: epoch of each filter's last complete chain
 // Further [F] arrays behind kSyncChain (word kSyncChain + kind·F + f), the block builder's
 // hand-offs (k_chain, PassArgs::build): the chain's Z / Y progress ((seq << 5) | steps done), its

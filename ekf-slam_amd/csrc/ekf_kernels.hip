@@ -1038,6 +1038,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   for (int ci = 0; ci < nchunks; ++ci) {
   if (!pre) {
     const MsgDesc& gd = A.desc[static_cast<size_t>(ci) * A.desc_stride + fy];
+    // planned on the bulk stream beside this launch: the planner's count covers every descriptor
+    if (ci == 0 && A.need_plan && tid == 0 && !epoch_wait_acquire(A.sync + kSyncPlan, A.need_plan))
+      flag_timeout(&ctl->status, A.fatal);
     __syncthreads();
     if (threadIdx.x < sizeof(MsgDesc) / 16)
       reinterpret_cast<uint4*>(&sdesc[ci & 1])[threadIdx.x] =

@@ -31,6 +31,8 @@ struct PassArgs {
   unsigned* fatal;      // host-mapped word: set when any poll of the handle timed out (flag_timeout)
   unsigned seq;         // this launch pair's sequence number; its epochs are seq + 1
   unsigned need_sigma;  // chain: wait until the Σ-pass epoch reaches this (0 = no wait)
+  unsigned need_plan;   // chain: the launch's descriptors are planned once the kSyncPlan count
+                        // reaches this (ekf_replay_device's planner on the bulk stream; 0 = no wait)
   unsigned pub_sigma;   // factors: publish this Σ-pass epoch first (the previous chunk's pass, 0 = none)
   int first_ready;      // chain: the launch's first chunk skips its Σ-epoch poll (the host joined
                         // the bulk stream before it, and the last pass published no epoch)
@@ -142,6 +144,8 @@ struct ReplayArgs {
   int T, F, M, N;
   int rows;               // fp64 pipeline: kRowsOut / kRowsIn hand-offs
   int stage;              // staged rebuild operands (kStageOut / kStageIn)
+  unsigned* plan_count;   // non-null: every wave adds 1 here once its descriptor is stored (the
+                          // chain polls it instead of waiting for the planner's kernel boundary)
 };
 hipError_t launch_plan_replay(const ReplayArgs& a, hipStream_t s);
 

@@ -173,6 +173,13 @@ __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
   __syncthreads();
   uint4* gd = reinterpret_cast<uint4*>(A.desc + tf);
   for (int e = lane; e < static_cast<int>(sizeof(MsgDesc) / 16); e += 64) gd[e] = dz[e];
+  if (A.plan_count) {  // the wave's stores (every lane's) complete, released, then counted; the
+                       // explicit waits around the fence: the compiler may drop the fence's own
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(A.plan_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 hipError_t launch_plan_replay(const ReplayArgs& a, hipStream_t s) {
