@@ -58,7 +58,6 @@ struct ekf_ctx {
   hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
-  bool stream_pass = false;      // fp64 swarms: the persistent streaming Σ pass (EKF_SIG_STREAM)
   bool build = false;            // EKF_BUILD=1: chain launches of > 1 chunk take a builder
                                  // workgroup per filter (k_chain, PassArgs::build)
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
@@ -171,7 +170,6 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.r = h->cfg.r_noise;
   a.gate = h->cfg.mah_gate;
   a.joseph = h->joseph ? 1 : 0;
-  a.stream_blocks = h->stream_pass ? 8 * h->bulk_cus_per_xcd : 0;
   return a;
 }
 
@@ -1098,10 +1096,6 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + kSyncKinds * h->F);
   if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
-  {  // fp64 swarms' Σ pass: the persistent streaming kernel with EKF_SIG_STREAM=1
-    const char* e = std::getenv("EKF_SIG_STREAM");
-    h->stream_pass = cfg.dtype == EKF_F64 && e && std::atoi(e) != 0;
-  }
   {  // the block builders: device epochs, staged operands, and room on the main stream's CUs of
      // every XCD for the chain and the builder of its filters (one workgroup per CU: LDS)
     const char* e = std::getenv("EKF_BUILD");  // opt-in (EKF_BUILD=1): measured slower, DESIGN.md

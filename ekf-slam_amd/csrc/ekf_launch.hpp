@@ -44,9 +44,6 @@ struct PassArgs {
                         // f mod 8, builder 8 later, both on XCD f mod 8); 0 (default): every
                         // chunk's prologue rebuilds its own
   int nf_launch;        // filters of the launch (build: the 1-D grid's bound)
-  int stream_blocks;    // fp64 Σ pass of ≥ 16 filters: the persistent streaming pass
-                        // (k_sigma_stream) on this many workgroups, one per CU of the stream
-                        // (a multiple of 8); 0: the tile grid (k_sigma_pass)
   BuildRec* bout;       // [2][rec_stride] the builder's blocks
   BuildChan* chan;      // [rec_stride] the chain's predict parameters for the builder
   const MsgDesc* desc;

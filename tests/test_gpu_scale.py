@@ -304,27 +304,6 @@ def test_swarm_n256_512_filters_against_oracle():
                                 "messages": T}
 
 
-@pytest.mark.parametrize("F", [24, 40], ids=["devsync", "events"])
-def test_swarm_streaming_pass_bit_identical(F, monkeypatch):
-    """fp64 swarms (≥ 16 filters) take the persistent streaming Σ pass (k_sigma_stream: Σ_in
-    double-buffered through LDS-DMA, the next tile's loads under the current tile's MFMAs) unless
-    EKF_SIG_STREAM=0 (the tile grid, k_sigma_pass): the same 32 × 64 tile and MFMA order, so every
-    filter's x and Σ are bit-identical — the fp64 row hand-off (kRowsOut) included. 24 filters run
-    on split CU masks with device epochs, 40 on shared CUs with events."""
-    sw = synth.swarm(64, F, 6)
-    odom = np.repeat(pyekf.odometry(sw.scenario(0))[:, None], F, 1)
-    outs = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("EKF_SIG_STREAM", v)
-        e = pyekf.EKF(n_landmarks=64, n_filters=F)
-        e.replay(sw.count, sw.rel, odom, ids=sw.ids, actions=sw.actions)
-        assert [e.status(f) for f in range(F)] == [0] * F
-        outs.append([e.state(f) for f in range(F)])
-        e.close()
-    for f, ((x0, S0, c0), (x1, S1, c1)) in enumerate(zip(*outs)):
-        assert np.array_equal(x0, x1) and np.array_equal(S0, S1) and c0 == c1, f
-
-
 @pytest.fixture(scope="module")
 def known_map():
     """512 slots, 256 landmarks surveyed with known ids (fp64 pipeline): the state the unknown-

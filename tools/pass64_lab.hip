@@ -114,6 +114,207 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 }
 
 
+// ---- measured, not kept (profiles/r4/stream_pass_notkept): 529 µs against the tile grid's 475 ----
+// ---- swarm Σ pass (fp64, ≥ 16 filters): persistent, Σ_in double-buffered through LDS-DMA ---------
+// The tile grid's waves (2 per SIMD, registers) each load, multiply, then store: with 2.2 GB of Σ
+// streaming through HBM per message the MFMA phases leave the memory system idle (0.56 of the
+// float4 copy's rate standalone). Here each wave keeps its NEXT tile's Σ_in (LDS-DMA) and operands
+// (registers freed k-step by k-step behind the MFMAs) in flight while it multiplies and stores the
+// current one. One workgroup of 4 waves per CU (128 KiB of LDS: two 16 KiB 32 × 64 images per
+// wave); XCD x (blocks L ≡ x mod 8) walks the tiles of filters x, x+8, … in order, wave by wave
+// (the filter's Kcat / Mcat stay in that XCD's L2). Same tile (32 × 64, SigmaTile64<4>), same MFMA
+// order: bit-identical to k_sigma_pass. Per tile t (next tn):
+//   1. wait for t's operands (a use of the newest one: the compiler's count, exact — the DMA below is
+//      issued after it; t's Σ_in DMA is older, so complete too)
+//   2. Σ_in(tn) → the other LDS image: 16 buffer_load_dwordx4 … lds in inline asm (invisible to the
+//      compiler's wait counting: a visible LDS-DMA makes it wait vmcnt(0) at every later load use)
+//   3. the 72 MFMAs of t, tn's operand loads issued step by step behind them (registers freed)
+//   4. Σ_in(t) from LDS in the MFMA layout, Σ_out = Σ_in − K·M (+ Q̄), stores (+ kRowsOut rows)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+struct StreamTile {
+  int fb, R0, C0, par, kw, flags;
+  bool live;
+};
+__device__ __forceinline__ StreamTile stream_tile(const PassArgs<double>& A, int x, int t, int T,
+                                                  int tpf, int tcols) {
+  StreamTile s;
+  s.live = t < T;
+  const int tt = s.live ? t : 0, k = tt / tpf, r = tt - k * tpf;
+  s.fb = x + 8 * k;
+  // (through the constant address space: scalar loads, no vmcnt)
+  const __attribute__((address_space(4))) MsgDesc& d = ((const __attribute__((address_space(4))) MsgDesc*)A.desc)[s.fb];
+  s.flags = s.live ? d.flags : 0;
+  s.live = s.live && (s.flags & kActive);
+  s.par = d.parity;
+  s.kw = ((2 + ((s.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
+  s.R0 = (r / tcols) * 32;
+  s.C0 = (r % tcols) * 64;
+  return s;
+}
+__device__ __forceinline__ void stream_dma(const PassArgs<double>& A, const StreamTile& s,
+                                           unsigned lds_base, int lane) {
+  const int n = A.n, ld = A.ld;
+  const size_t fo = static_cast<size_t>(A.f0 + s.fb) * A.sig_stride;
+  const double* S = A.sig[s.par] + fo + static_cast<size_t>(s.R0) * ld;
+  const unsigned bytes = s.live ? static_cast<unsigned>(min(n - s.R0, 32)) * ld * 8u : 0u;
+  const auto r = buf_rsrc(S, bytes);
+  const int c = s.C0 + 2 * (lane & 31);
+  const unsigned vo = c < n ? static_cast<unsigned>((lane >> 5) * ld + c) * 8u : kOOB;
+  const unsigned rs = 2u * ld * 8u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen nt lds"
+                 : : "s"(__builtin_amdgcn_readfirstlane(lds_base + 1024u * i)), "v"(vo), "s"(r),
+                     "s"(__builtin_amdgcn_readfirstlane(rs * i)) : "memory");
+}
+__device__ __forceinline__ void stream_ops_step(const PassArgs<double>& A, const StreamTile& s, int st,
+                                                double (&a)[2][9], double (&b)[4][9], int lane) {
+  const int n = A.n, ldk = A.ldk;
+  const size_t fo = static_cast<size_t>(A.f0 + s.fb) * A.km_stride;
+  const unsigned kbytes = s.live ? static_cast<unsigned>(kMaxKW) * ldk * 8u : 0u;
+  const auto rk = buf_rsrc(A.kcat + fo, kbytes), rm = buf_rsrc(A.mcat + fo, kbytes);
+  const int kr = lane >> 4, kcol = lane & 15;
+  const unsigned ko = static_cast<unsigned>(kr * ldk + s.R0 + kcol) * 8u;
+  const unsigned kstep = 4u * ldk * 8u;
+  a[0][st] = ld_f64(rk, ko, st * kstep);
+  a[1][st] = ld_f64(rk, ko + 16 * 8, st * kstep);
+#pragma unroll
+  for (int tj = 0; tj < 4; ++tj) {
+    const unsigned mo = static_cast<unsigned>(kr * ldk + min(s.C0 + 16 * tj + kcol, n - 1)) * 8u;
+    b[tj][st] = ld_f64(rm, mo, st * kstep);
+  }
+}
+__global__ __launch_bounds__(256) void k_sigma_stream(PassArgs<double> A, int tcols, int tpf, int nf) {
+  __shared__ double img[4][2][32 * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int x = blockIdx.x & 7;
+  const int nfx = (nf - x + 7) / 8;  // filters x, x+8, … < nf
+  const int T = nfx * tpf;
+  const int W = static_cast<int>(gridDim.x >> 3) * 4;
+  int t = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x >> 3) * 4 + wv);
+  if (t >= T) return;
+  typedef __attribute__((address_space(3))) double lds_d;
+  const unsigned base0 = static_cast<unsigned>(reinterpret_cast<size_t>((lds_d*)&img[wv][0][0]));
+  const unsigned base1 = static_cast<unsigned>(reinterpret_cast<size_t>((lds_d*)&img[wv][1][0]));
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const int kr = lane >> 4, kcol = lane & 15;
+  const double q = A.q;
+  StreamTile cur = stream_tile(A, x, t, T, tpf, tcols);
+  double a[2][9], b[4][9];
+  stream_dma(A, cur, base0, lane);
+#pragma unroll
+  for (int st = 0; st < 9; ++st) stream_ops_step(A, cur, st, a, b, lane);
+  {  // 48 out-of-range stores: the loop's entry looks like its back edge to the compiler's wait
+     // counting (48 stores behind the operands), so the first wait is vmcnt(48) there as well
+    const auto none = buf_rsrc(A.rows, 0u);
+#pragma unroll
+    for (int i = 0; i < 48; ++i) __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, none, kOOB + 8u * i, 0, 0);
+  }
+  const __attribute__((address_space(4))) MsgDesc* cdesc = (const __attribute__((address_space(4))) MsgDesc*)A.desc;
+  int buf = 0;
+  for (;;) {
+    const int tn = t + W;
+    const StreamTile nxt = stream_tile(A, x, tn, T, tpf, tcols);
+    // 1. t's operands (and, older, its Σ_in DMA) have landed
+    asm volatile("" : : "v"(a[0][0]), "v"(a[0][1]), "v"(a[0][2]), "v"(a[0][3]), "v"(a[0][4]), "v"(a[0][5]),
+                 "v"(a[0][6]), "v"(a[0][7]), "v"(a[0][8]), "v"(a[1][0]), "v"(a[1][1]), "v"(a[1][2]),
+                 "v"(a[1][3]), "v"(a[1][4]), "v"(a[1][5]), "v"(a[1][6]), "v"(a[1][7]), "v"(a[1][8]));
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj)
+      asm volatile("" : : "v"(b[tj][0]), "v"(b[tj][1]), "v"(b[tj][2]), "v"(b[tj][3]), "v"(b[tj][4]),
+                   "v"(b[tj][5]), "v"(b[tj][6]), "v"(b[tj][7]), "v"(b[tj][8]));
+    __builtin_amdgcn_sched_barrier(0);
+    // 2. tn's Σ_in into the other image (a dummy, out of range, past the last tile)
+    stream_dma(A, nxt, buf ? base0 : base1, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    // 3. the MFMAs of t, tn's operands behind each k-step
+    d4 acc[2][4];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = d4{0, 0, 0, 0};
+#pragma unroll
+    for (int st = 0; st < 9; ++st) {
+      const bool live = 4 * st < cur.kw;
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj)
+          acc[ti][tj] = mfma_f64(live ? a[ti][st] : 0.0, live ? b[tj][st] : 0.0, acc[ti][tj]);
+      stream_ops_step(A, nxt, st, a, b, lane);
+      asm volatile("" ::: "memory");      // (tn's loads stay among t's MFMAs: not sunk below,
+      __builtin_amdgcn_sched_barrier(0);  //  not scheduled past)
+    }
+    // 4. Σ_in(t) from LDS (MFMA layout), Σ_out = Σ_in − K·M (+ Q̄) back into the image (columns
+    //    ≥ n as 0: the padding stays zero), the kRowsOut rows from registers; 5. the image row by
+    //    row, 16 × dwordx4 (2 rows × 512 B each). Every store is issued whatever the tile (dummy
+    //    tiles and columns outside U_next go out of range): a fixed 48 VMEM stores per tile, so the
+    //    compiler's wait for the next operands is an exact vmcnt(48)
+    {
+      const size_t fo = static_cast<size_t>(A.f0 + cur.fb) * A.sig_stride;
+      double* So = A.sig[cur.par ^ 1] + fo + static_cast<size_t>(cur.R0) * ld;
+      const auto rout = buf_rsrc(So, cur.live ? static_cast<unsigned>(min(n - cur.R0, 32)) * ld * 8u : 0u);
+      const bool first = (cur.flags & kFirst) != 0;
+      lds_d* im = (lds_d*)&img[wv][buf][0];
+      int bpos[4] = {-1, -1, -1, -1};
+      const bool rows_out = cur.live && (cur.flags & kRowsOut) != 0;
+      if (rows_out) {  // first position in U_next of each column (scalar scan, lowest b first)
+        const int nu = cdesc[cur.fb].nxt_nu;
+        for (int bb = 0; bb < nu; ++bb) {
+          const int dc = cdesc[cur.fb].nxt_u[bb] - cur.C0;
+          if (dc >= 0 && dc < 64) {
+#pragma unroll
+            for (int tj = 0; tj < 4; ++tj)
+              if (bpos[tj] < 0 && 16 * tj + kcol == dc) bpos[tj] = bb;
+          }
+        }
+      }
+      const auto rrows = buf_rsrc(A.rows + static_cast<size_t>(A.f0 + cur.fb) * A.rows_stride,
+                                  rows_out ? static_cast<unsigned>(kRowW) * ldk * 8u : 0u);
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+        double sv[4][4];  // a half tile's LDS reads first (one wait)
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sv[tj][r] = im[(16 * ti + kr + 4 * r) * 64 + 16 * tj + kcol];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rl = 16 * ti + kr + 4 * r, col = cur.C0 + 16 * tj + kcol, row = cur.R0 + rl;
+            double v = sv[tj][r] - acc[ti][tj][r];
+            if (first && row == col && row < 3) v += q;
+            v = col < n ? v : 0.0;
+            im[rl * 64 + 16 * tj + kcol] = v;
+            const unsigned ro = bpos[tj] >= 0 && row < n
+                                    ? static_cast<unsigned>(bpos[tj] * ldk + row) * 8u : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rrows, ro, 0, 0);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const int c = cur.C0 + 2 * (lane & 31);
+      const unsigned vo = c < n ? static_cast<unsigned>((lane >> 5) * ld + c) * 8u : kOOB;
+      const unsigned rs = 2u * ld * 8u;
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      typedef int i4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const d2 w = *(const __attribute__((address_space(3))) d2*)&im[(2 * i + (lane >> 5)) * 64 + 2 * (lane & 31)];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4, w), rout, vo, rs * i, 2);
+      }
+    }
+    if (tn >= T) break;
+    cur = nxt;
+    t = tn;
+    buf ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the last dummy DMA out of the LDS's way)
+}
+#pragma clang diagnostic pop
+
 template <typename V>
 __global__ void k_copy(const V* __restrict__ in, V* __restrict__ out, size_t nv) {
   for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) out[i] = in[i];
