@@ -934,6 +934,7 @@ int handle_info(ekf_t h, HandleInfo* out) {
   out->rows = h->rows != nullptr && !h->resident;
   out->joseph = h->joseph;
   out->stream = h->stream;
+  out->bulk = h->bulk ? h->bulk : h->stream;
   return EKF_OK;
 }
 
@@ -1062,6 +1063,14 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
       hipEventCreateWithFlags(&h->ev_sig[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_sig[1], hipEventDisableTiming) != hipSuccess)
     return fail(EKF_E_HIP);
+  // Many filters (no CU split, so event hand-offs): the Σ pass's waves hold every CU a chain or a
+  // factor kernel needs, so nothing overlaps it anyway; one stream turns the two
+  // cross-stream hops per message into kernel boundaries: swarm 1.12 → 1.15e7 corrections/s, with
+  // the staging off (below) 1.17e7 (profiles/r4/r4s_*). EKF_SERIAL=0 keeps the two streams.
+  {
+    const char* e = std::getenv("EKF_SERIAL");
+    if (!e && !h->devsync && h->F > kCuSplitMaxFilters) h->serial = true;
+  }
   h->am_route = am_route(h);
   if (hipHostMalloc(reinterpret_cast<void**>(&h->fatal_h), 64,
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
@@ -1086,10 +1095,15 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
       hipMalloc(&h->rows, sizeof(double) * kRowW * h->ldk * h->F) != hipSuccess)
     return fail(EKF_E_NOMEM);
   // staged rebuild operands (EKF_STAGE=0: every kLook chain gathers its own, tests compare the two)
+  // The same many-filter handles skip it by default (EKF_STAGE=1 keeps it): there every message's
+  // k_patch_stage runs on the serial critical path (≈ 18 µs for 512 filters), more than the chains'
+  // own gathers cost (two rounds of ≈ 2 µs).
   const char* stage_env = std::getenv("EKF_STAGE");
   const size_t stage_bytes = 2 * h->F *
       (cfg.dtype == EKF_F32 ? sizeof(StageRec<float>) : sizeof(StageRec<double>));
-  if (!(stage_env && std::atoi(stage_env) == 0)) {
+  const bool stage_on = stage_env ? std::atoi(stage_env) != 0
+                                  : (h->devsync || h->F <= kCuSplitMaxFilters);
+  if (stage_on) {
     if (hipMalloc(&h->stage, stage_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
     if (hipMemset(h->stage, 0, stage_bytes) != hipSuccess) return fail(EKF_E_HIP);
   }
@@ -1390,8 +1404,12 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   if (h->devsync && !h->serial) {
     rc = group(h, h->ddesc, nullptr, 0, h->F, T, true, true, false, stg);
   } else {
+    // Events: a chunk t ≥ 1 needs the Σ pass two back (kLook), or — no message of its filter
+    // earlier in this replay — the passes before the replay, which the first chunk's join covers:
+    // the wait on the pass two back suffices, and the chain of t runs beside the factor kernel and
+    // Σ pass of t − 1 where the CUs allow (not a join of the whole bulk stream per message)
     for (int t = 0; t < T && !rc; ++t)
-      rc = group(h, h->ddesc + static_cast<size_t>(t) * F, nullptr, 0, h->F, 1, true, true, true,
+      rc = group(h, h->ddesc + static_cast<size_t>(t) * F, nullptr, 0, h->F, 1, true, t == 0, true,
                  stg);
   }
   h->main_dirty = true;

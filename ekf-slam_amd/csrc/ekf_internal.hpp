@@ -15,6 +15,7 @@ struct HandleInfo {
   bool rows;      // fp64 pipeline: Σ-pass → factor-kernel row hand-off planned
   bool joseph;    // ekf_set_joseph is on (the HBM pipeline then needs one marker per chunk)
   hipStream_t stream;
+  hipStream_t bulk;  // the factors / Σ-pass stream (the main stream when serial)
 };
 
 // Runs everything the host has planned so far (flush) and describes the handle.

@@ -3,9 +3,13 @@
 // The simulator runs on a stream of its own with double-buffered run buffers, so run r's
 // simulation overlaps run r−1's filter work; the host waits only for the simulation (it needs
 // each filter's final parity for the handle's host mirror).
+// A run without SURVEY messages on the HBM pipeline takes the parallel form instead: the wheels per
+// filter, then every (message, filter) sensed at once into marker arrays, which ekf_replay_device
+// plans on the GPU — no host round trip at all (EKF_SIM_PARALLEL=0 keeps the sequential kernel).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -39,14 +43,19 @@ struct ekf_sim {
   size_t cap_ticks = 0, cap_msgs = 0;
   MsgDesc* desc[2] = {nullptr, nullptr};
   PlanEntry* plan = nullptr;
-  // record
-  int* ids = nullptr;
-  int* act = nullptr;
-  double* rel = nullptr;
-  int* cnt = nullptr;
-  double* truth = nullptr;
-  double* odom = nullptr;
-  int last_T = 0;
+  // markers and poses of a run by run buffer: the record (cfg.record) and the parallel form's
+  // hand-over to ekf_replay_device
+  struct Markers {
+    int* ids = nullptr;       // [T][F][M]
+    int* act = nullptr;       // [T][F][M]
+    double* rel = nullptr;    // [T][F][M][2]
+    int* cnt = nullptr;       // [T][F]
+    double* truth = nullptr;  // [T][F][3]
+    double* odom = nullptr;   // [T][3] (filter 0's)
+    double* odomF = nullptr;  // [T][F][3] (the planner's input)
+  } mk[2];
+  bool mk_alloc = false;
+  int last_T = 0, last_b = 0;
   std::vector<int> host_par;
   std::vector<double> host_odom;    // [F][3] t_odom_robot after the last run
 };
@@ -57,20 +66,32 @@ void free_run(ekf_sim* s) {
   for (void* p : {static_cast<void*>(s->cmd[0]), static_cast<void*>(s->sense[0]),
                   static_cast<void*>(s->desc[0]), static_cast<void*>(s->cmd[1]),
                   static_cast<void*>(s->sense[1]), static_cast<void*>(s->desc[1]),
-                  static_cast<void*>(s->plan), static_cast<void*>(s->ids),
-                  static_cast<void*>(s->act), static_cast<void*>(s->rel),
-                  static_cast<void*>(s->cnt), static_cast<void*>(s->truth),
-                  static_cast<void*>(s->odom)})
+                  static_cast<void*>(s->plan)})
     if (p) hipFree(p);
+  for (auto& k : s->mk) {
+    for (void* p : {static_cast<void*>(k.ids), static_cast<void*>(k.act), static_cast<void*>(k.rel),
+                    static_cast<void*>(k.cnt), static_cast<void*>(k.truth),
+                    static_cast<void*>(k.odom), static_cast<void*>(k.odomF)})
+      if (p) hipFree(p);
+    k = ekf_sim::Markers{};
+  }
   for (int b = 0; b < 2; ++b) {
     s->cmd[b] = nullptr;
     s->sense[b] = nullptr;
     s->desc[b] = nullptr;
   }
   s->plan = nullptr;
-  s->ids = s->act = s->cnt = nullptr;
-  s->rel = s->truth = s->odom = nullptr;
+  s->mk_alloc = false;
   s->cap_ticks = s->cap_msgs = 0;
+}
+
+// The parallel form (no SURVEY message, HBM pipeline, M ≤ kMaxChunk; EKF_SIM_PARALLEL=0: never).
+bool parallel_ok(const ekf_sim* s, int T, const int* sense) {
+  const char* e = std::getenv("EKF_SIM_PARALLEL");
+  if ((e && std::atoi(e) == 0) || s->info.resident || s->cfg.marker_stride > kMaxChunk) return false;
+  for (int t = 0; sense && t < T; ++t)
+    if (sense[t] == EKF_SENSE_SURVEY) return false;
+  return true;
 }
 
 // run buffers for T messages (grown, never shrunk)
@@ -89,13 +110,20 @@ int reserve(ekf_sim* s, int T) {
     ok = hipMalloc(&s->cmd[b], tk * 2 * sizeof(double)) == hipSuccess &&
          hipMalloc(&s->sense[b], Tn * sizeof(int)) == hipSuccess &&
          hipMalloc(&s->desc[b], Tn * F * sizeof(MsgDesc)) == hipSuccess;
-  if (ok && s->cfg.record)
-    ok = hipMalloc(&s->ids, Tn * F * M * sizeof(int)) == hipSuccess &&
-         hipMalloc(&s->act, Tn * F * M * sizeof(int)) == hipSuccess &&
-         hipMalloc(&s->rel, Tn * F * M * 2 * sizeof(double)) == hipSuccess &&
-         hipMalloc(&s->cnt, Tn * F * sizeof(int)) == hipSuccess &&
-         hipMalloc(&s->truth, Tn * F * 3 * sizeof(double)) == hipSuccess &&
-         hipMalloc(&s->odom, Tn * 3 * sizeof(double)) == hipSuccess;
+  // markers: both buffers for the parallel form (one run's planner reads them while the next run's
+  // simulation writes the other), buffer 0 only for a record of the sequential form
+  const bool par = !s->info.resident && s->cfg.marker_stride <= kMaxChunk;
+  for (int b = 0; b < (par ? 2 : 1) && ok && (par || s->cfg.record); ++b) {
+    auto& k = s->mk[b];
+    ok = hipMalloc(&k.ids, Tn * F * M * sizeof(int)) == hipSuccess &&
+         hipMalloc(&k.act, Tn * F * M * sizeof(int)) == hipSuccess &&
+         hipMalloc(&k.rel, Tn * F * M * 2 * sizeof(double)) == hipSuccess &&
+         hipMalloc(&k.cnt, Tn * F * sizeof(int)) == hipSuccess &&
+         hipMalloc(&k.truth, Tn * F * 3 * sizeof(double)) == hipSuccess &&
+         hipMalloc(&k.odom, Tn * 3 * sizeof(double)) == hipSuccess &&
+         hipMalloc(&k.odomF, Tn * F * 3 * sizeof(double)) == hipSuccess;
+    s->mk_alloc = ok;
+  }
   if (!ok) {
     free_run(s);
     return EKF_E_NOMEM;
@@ -110,6 +138,65 @@ int reserve(ekf_sim* s, int T) {
   s->cap_msgs = Tn;
   s->cap_ticks = tk;
   return EKF_OK;
+}
+
+// The parallel form of ekf_sim_run (parallel_ok): simulation on the simulator's stream, then
+// ekf_replay_device over its marker arrays behind it on the handle's streams. The planning state
+// stays on the device (the handle adopts it at its next host access), so the host never waits.
+int run_parallel(ekf_sim* s, int T, const double* wheel_cmd, const int* sense) {
+  const int b = s->buf;
+  s->buf ^= 1;
+  const hipStream_t st = s->sst;
+  const size_t ticks = static_cast<size_t>(T) * s->cfg.ticks_per_msg;
+  auto& k = s->mk[b];
+  // buffer b (commands, senses, markers) was last read by the run before the previous one
+  if (hipStreamWaitEvent(st, s->ev_done[b], 0) != hipSuccess ||
+      hipMemcpyAsync(s->cmd[b], wheel_cmd, ticks * 2 * sizeof(double), hipMemcpyHostToDevice, st) !=
+          hipSuccess ||
+      (sense && hipMemcpyAsync(s->sense[b], sense, T * sizeof(int), hipMemcpyHostToDevice, st) !=
+                    hipSuccess))
+    return EKF_E_HIP;
+  SimArgs a{};
+  a.cmd = s->cmd[b];
+  a.sense = sense ? s->sense[b] : nullptr;
+  a.lm = s->lm;
+  a.st = s->st;
+  a.out_ids = k.ids;
+  a.out_act = k.act;
+  a.out_rel = k.rel;
+  a.out_cnt = k.cnt;
+  a.out_truth = k.truth;
+  a.out_odom = s->cfg.record ? k.odom : nullptr;
+  a.seed = s->cfg.seed;
+  a.tick0 = s->tick;
+  a.msg0 = s->msg;
+  a.f0 = s->cfg.f0;
+  a.F = s->info.F;
+  a.L = s->L;
+  a.T = T;
+  a.tpm = s->cfg.ticks_per_msg;
+  a.m = s->m;
+  a.M = s->cfg.marker_stride;
+  a.N = s->info.N;
+  a.slip = s->cfg.slip;
+  a.sigma = s->cfg.sensor_sigma;
+  a.range = s->cfg.max_range;
+  a.radius = s->cfg.wheel_radius;
+  a.track = s->cfg.track_width;
+  if (launch_sim_parallel(a, k.truth, k.odomF, st) != hipSuccess ||
+      hipEventRecord(s->ev_sim, st) != hipSuccess ||
+      hipStreamWaitEvent(s->info.stream, s->ev_sim, 0) != hipSuccess ||
+      hipStreamWaitEvent(s->info.bulk, s->ev_sim, 0) != hipSuccess)
+    return EKF_E_HIP;
+  s->tick += static_cast<long long>(ticks);
+  s->msg += T;
+  s->last_T = T;
+  s->last_b = b;
+  const int rc = ekf_replay_device(s->h, T, s->cfg.marker_stride, k.cnt, k.ids, k.act, k.rel,
+                                   k.odomF);
+  if (rc) return rc;
+  // the chain launch on the main stream polls the planner (or follows it): done there ⇒ read
+  return hipEventRecord(s->ev_done[b], s->info.stream) == hipSuccess ? EKF_OK : EKF_E_HIP;
 }
 
 }  // namespace
@@ -219,6 +306,7 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
   if (s->info.joseph && !s->info.resident) return EKF_E_ARG;
   hipSetDevice(s->info.device);
   if (int rc = reserve(s, T)) return rc;
+  if (parallel_ok(s, T, sense)) return run_parallel(s, T, wheel_cmd, sense);
   const int b = s->buf;
   s->buf ^= 1;
   const hipStream_t st = s->sst;
@@ -247,12 +335,13 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
   a.par = s->par;
   a.desc = s->desc[b];
   if (s->cfg.record) {
-    a.out_ids = s->ids;
-    a.out_act = s->act;
-    a.out_rel = s->rel;
-    a.out_cnt = s->cnt;
-    a.out_truth = s->truth;
-    a.out_odom = s->odom;
+    const auto& k = s->mk[0];
+    a.out_ids = k.ids;
+    a.out_act = k.act;
+    a.out_rel = k.rel;
+    a.out_cnt = k.cnt;
+    a.out_truth = k.truth;
+    a.out_odom = k.odom;
   }
   a.seed = s->cfg.seed;
   a.tick0 = s->tick;
@@ -285,6 +374,7 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
   s->tick += static_cast<long long>(ticks);
   s->msg += T;
   s->last_T = T;
+  s->last_b = 0;
   // the filter's kernels behind the simulation (their descriptors), then release buffer b
   if (hipStreamWaitEvent(s->info.stream, s->ev_sim, 0) != hipSuccess) return EKF_E_HIP;
   const int rc = run_device_plan(s->h, s->desc[b], s->plan, T, s->host_par.data(),
@@ -297,11 +387,14 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
 int ekf_sim_markers(ekf_sim_t s, int* counts, int* ids, int* actions, double* rel_xy) {
   if (!s || !s->cfg.record) return EKF_E_ARG;
   const size_t n = static_cast<size_t>(s->last_T) * s->info.F, M = s->cfg.marker_stride;
-  if (hipStreamSynchronize(s->info.stream) != hipSuccess) return EKF_E_HIP;
-  if ((counts && hipMemcpy(counts, s->cnt, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
-      (ids && hipMemcpy(ids, s->ids, n * M * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
-      (actions && hipMemcpy(actions, s->act, n * M * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
-      (rel_xy && hipMemcpy(rel_xy, s->rel, n * M * 2 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
+  const auto& k = s->mk[s->last_b];
+  if (hipStreamSynchronize(s->info.stream) != hipSuccess ||
+      hipStreamSynchronize(s->sst) != hipSuccess)
+    return EKF_E_HIP;
+  if ((counts && hipMemcpy(counts, k.cnt, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (ids && hipMemcpy(ids, k.ids, n * M * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (actions && hipMemcpy(actions, k.act, n * M * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (rel_xy && hipMemcpy(rel_xy, k.rel, n * M * 2 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
     return EKF_E_HIP;
   return EKF_OK;
 }
@@ -309,9 +402,12 @@ int ekf_sim_markers(ekf_sim_t s, int* counts, int* ids, int* actions, double* re
 int ekf_sim_poses(ekf_sim_t s, double* odom, double* truth) {
   if (!s || !s->cfg.record) return EKF_E_ARG;
   const size_t T = static_cast<size_t>(s->last_T);
-  if (hipStreamSynchronize(s->info.stream) != hipSuccess) return EKF_E_HIP;
-  if ((odom && hipMemcpy(odom, s->odom, T * 3 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
-      (truth && hipMemcpy(truth, s->truth, T * s->info.F * 3 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
+  const auto& k = s->mk[s->last_b];
+  if (hipStreamSynchronize(s->info.stream) != hipSuccess ||
+      hipStreamSynchronize(s->sst) != hipSuccess)
+    return EKF_E_HIP;
+  if ((odom && hipMemcpy(odom, k.odom, T * 3 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (truth && hipMemcpy(truth, k.truth, T * s->info.F * 3 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
     return EKF_E_HIP;
   return EKF_OK;
 }

@@ -81,12 +81,138 @@ struct SimShared {
   int ids[kMaxChunk], prev_ids[kMaxChunk];
 };
 
+// One message's wheels (nusim.cpp:222-230, slam.cpp:599-634): lane j < tpm is tick j, the wave
+// composes the ticks' arcs by a scan, then the true pose and the odometry advance by the product.
+__device__ __forceinline__ void wheels(const SimArgs& A, unsigned long long seed, int t, int lane,
+                                       Pose2& truth, Pose2& odo) {
+  Pose2 dt{0.0, 0.0, 0.0}, dot{0.0, 0.0, 0.0};  // identity past the message's ticks
+  if (lane < A.tpm) {
+    const size_t k = static_cast<size_t>(t) * A.tpm + lane;
+    const double cl = A.cmd[2 * k], cr = A.cmd[2 * k + 1];
+    const unsigned long long g = static_cast<unsigned long long>(A.tick0) + k;
+    const double sl = cl * (1.0 + A.slip * (2.0 * uniform(seed, kSlipStream, 2 * g) - 1.0));
+    const double sr = cr * (1.0 + A.slip * (2.0 * uniform(seed, kSlipStream, 2 * g + 1) - 1.0));
+    dt = arc(sl, sr, A.radius, A.track);
+    dot = arc(cl, cr, A.radius, A.track);
+  }
+  dt = scan_compose(dt, lane);
+  dot = scan_compose(dot, lane);
+  const int last = A.tpm - 1;
+  truth = compose(truth, Pose2{bcast(dt.theta, last), bcast(dt.x, last), bcast(dt.y, last)});
+  odo = compose(odo, Pose2{bcast(dot.theta, last), bcast(dot.x, last), bcast(dot.y, last)});
+}
+
+// The fake sensor of one message at the true pose (th, px, py) (nusim.cpp:317-346): every
+// landmark of the map `lm` in the true body frame R(θ)ᵀ(p − x) into sh.bx / sh.by, the selected
+// landmarks into sh.sel (nearest first, or id order for ALL). Returns their count k.
+__device__ __forceinline__ int sense(const SimArgs& A, const double* lm, int mode, double th,
+                                     double px, double py, SimShared& sh, int lane) {
+  const int L = A.L;
+  const double c = cos(th), s = sin(th);
+  const double rng = mode == kSenseSurvey ? kSurveyRange * A.range : A.range;
+  double key[kPerLane];
+  double dmin = INFINITY;
+  bool any = false;
+#pragma unroll
+  for (int j = 0; j < kPerLane; ++j) {
+    const int l = lane + 64 * j;
+    key[j] = INFINITY;
+    if (l < L) {
+      const double dx = lm[2 * l] - px, dy = lm[2 * l + 1] - py;
+      const double bx = c * dx + s * dy, by = -s * dx + c * dy;
+      const double d = hypot(bx, by);
+      sh.bx[l] = bx;
+      sh.by[l] = by;
+      dmin = fmin(dmin, d);
+      double kk = d <= rng ? d : INFINITY;
+      any = any || kk != INFINITY;
+      if (mode == kSenseSurvey && kk != INFINITY && ((sh.sighted[l >> 5] >> (l & 31)) & 1u))
+        kk = kk + 1e6;
+      key[j] = kk;
+      if (mode == kSenseAll) key[j] = d;  // (the ADD / DELETE test below)
+    }
+  }
+  __syncthreads();  // sh.bx / sh.by of every lane before the survey fallback reads them
+  int k = 0;
+  if (mode == kSenseAll) {
+    k = L;  // every landmark, in id order (L ≤ kMaxChunk, checked on the host)
+    if (lane < L) sh.sel[lane] = lane;
+  } else {
+    if (mode == kSenseSurvey && !__any(any)) {  // never empty: the nearest, out of range
+      for (int o = 32; o > 0; o >>= 1) dmin = fmin(dmin, __shfl_xor(dmin, o, 64));
+#pragma unroll
+      for (int j = 0; j < kPerLane; ++j) {
+        const int l = lane + 64 * j;
+        if (l < L) key[j] = hypot(sh.bx[l], sh.by[l]) == dmin ? dmin : INFINITY;
+      }
+    }
+    // the m smallest keys, ties to the lower index (synth: a stable argsort)
+    unsigned taken = 0;
+    for (; k < A.m; ++k) {
+      double best = INFINITY;
+      int bi = INT_MAX;
+#pragma unroll
+      for (int j = 0; j < kPerLane; ++j) {
+        const int l = lane + 64 * j;
+        if (!((taken >> j) & 1u) && (key[j] < best || (key[j] == best && l < bi)) && l < L) {
+          best = key[j];
+          bi = l;
+        }
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob < best || (ob == best && oi < bi)) {
+          best = ob;
+          bi = oi;
+        }
+      }
+      if (best == INFINITY) break;  // wave-uniform
+      if ((bi & 63) == lane) taken |= 1u << (bi >> 6);
+      if (lane == 0) sh.sel[k] = bi;
+    }
+  }
+  __syncthreads();
+  return k;
+}
+
+// Marker `lane` < k of message `msg`: its landmark, the noisy body-frame position (draws
+// 2·(msg·M + lane) and + 1 of stream 2) and ADD / DELETE (beyond range, mode ALL).
+__device__ __forceinline__ void marker(const SimArgs& A, unsigned long long seed, long long msg,
+                                       int mode, int k, const SimShared& sh, int lane, int* id,
+                                       int* act, double* rx, double* ry) {
+  *id = -1;
+  *act = 0;
+  *rx = *ry = 0.0;
+  if (lane < k) {
+    *id = sh.sel[lane];
+    const unsigned long long idx = (static_cast<unsigned long long>(msg) * A.M + lane) * 2;
+    *rx = sh.bx[*id] + A.sigma * normal(seed, kNoiseStream, idx);
+    *ry = sh.by[*id] + A.sigma * normal(seed, kNoiseStream, idx + 1);
+    *act = mode == kSenseAll && !(hypot(sh.bx[*id], sh.by[*id]) <= A.range) ? 2 : 0;  // DELETE
+  }
+}
+
+// the message's markers as ekf_replay takes them (row `rowo` = t·F + f of the record arrays)
+__device__ __forceinline__ void record_markers(const SimArgs& A, size_t rowo, int k, int id,
+                                               int act, double rx, double ry, int lane) {
+  const int M = A.M;
+  for (int i = lane; i < M; i += 64) {
+    const size_t o = rowo * M + i;
+    A.out_ids[o] = i < k ? __shfl(id, i, 64) : -1;
+    A.out_act[o] = i < k ? __shfl(act, i, 64) : 0;
+    A.out_rel[2 * o] = i < k ? __shfl(rx, i, 64) : 0.0;
+    A.out_rel[2 * o + 1] = i < k ? __shfl(ry, i, 64) : 0.0;
+  }
+  if (lane == 0) A.out_cnt[rowo] = k;
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
   __shared__ SimShared sh;
   const int f = blockIdx.x, lane = threadIdx.x;
-  const int L = A.L, M = A.M;
+  const int L = A.L;
   const unsigned long long seed = A.seed + static_cast<unsigned long long>(A.f0 + f);
   SimState& S = A.st[f];
   const double* lm = A.lm + static_cast<size_t>(f) * L * 2;
@@ -101,119 +227,22 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
   long prev_t = -1;      // its message index, for the row hand-off
   for (int t = 0; t < A.T; ++t) {
     const long long msg = A.msg0 + t;
-    // ---- wheels: lane j < tpm is tick j of the message (nusim.cpp:222-230, slam.cpp:599-634) ----
-    {
-      Pose2 dt{0.0, 0.0, 0.0}, dot{0.0, 0.0, 0.0};  // identity past the message's ticks
-      if (lane < A.tpm) {
-        const size_t k = static_cast<size_t>(t) * A.tpm + lane;
-        const double cl = A.cmd[2 * k], cr = A.cmd[2 * k + 1];
-        const unsigned long long g = static_cast<unsigned long long>(A.tick0) + k;
-        const double sl = cl * (1.0 + A.slip * (2.0 * uniform(seed, kSlipStream, 2 * g) - 1.0));
-        const double sr = cr * (1.0 + A.slip * (2.0 * uniform(seed, kSlipStream, 2 * g + 1) - 1.0));
-        dt = arc(sl, sr, A.radius, A.track);
-        dot = arc(cl, cr, A.radius, A.track);
-      }
-      dt = scan_compose(dt, lane);
-      dot = scan_compose(dot, lane);
-      const int last = A.tpm - 1;
-      truth = compose(truth, Pose2{bcast(dt.theta, last), bcast(dt.x, last), bcast(dt.y, last)});
-      odo = compose(odo, Pose2{bcast(dot.theta, last), bcast(dot.x, last), bcast(dot.y, last)});
-    }
+    wheels(A, seed, t, lane, truth, odo);
     const double th = truth.theta, px = truth.x, py = truth.y;
     const double oth = odo.theta, ox = odo.x, oy = odo.y;
     if (A.out_truth && lane < 3)
       A.out_truth[(static_cast<size_t>(t) * A.F + f) * 3 + lane] = lane == 0 ? th : (lane == 1 ? px : py);
     if (A.out_odom && f == 0 && lane < 3)
       A.out_odom[static_cast<size_t>(t) * 3 + lane] = lane == 0 ? oth : (lane == 1 ? ox : oy);
-    // ---- the fake sensor: every landmark in the true body frame R(θ)ᵀ(p − x) ----
     const int mode = A.sense ? A.sense[t] : kSenseNearest;
-    const double c = cos(th), s = sin(th);
-    const double rng = mode == kSenseSurvey ? kSurveyRange * A.range : A.range;
-    double key[kPerLane];
-    double dmin = INFINITY;
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < kPerLane; ++j) {
-      const int l = lane + 64 * j;
-      key[j] = INFINITY;
-      if (l < L) {
-        const double dx = lm[2 * l] - px, dy = lm[2 * l + 1] - py;
-        const double bx = c * dx + s * dy, by = -s * dx + c * dy;
-        const double d = hypot(bx, by);
-        sh.bx[l] = bx;
-        sh.by[l] = by;
-        dmin = fmin(dmin, d);
-        double kk = d <= rng ? d : INFINITY;
-        any = any || kk != INFINITY;
-        if (mode == kSenseSurvey && kk != INFINITY && ((sh.sighted[l >> 5] >> (l & 31)) & 1u))
-          kk = kk + 1e6;
-        key[j] = kk;
-        if (mode == kSenseAll) key[j] = d;  // (the ADD / DELETE test below)
-      }
-    }
-    __syncthreads();  // sh.bx / sh.by of every lane before the survey fallback reads them
-    int k = 0;
-    if (mode == kSenseAll) {
-      k = L;  // every landmark, in id order (L ≤ kMaxChunk, checked on the host)
-      if (lane < L) sh.sel[lane] = lane;
-    } else {
-      if (mode == kSenseSurvey && !__any(any)) {  // never empty: the nearest, out of range
-        for (int o = 32; o > 0; o >>= 1) dmin = fmin(dmin, __shfl_xor(dmin, o, 64));
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-          const int l = lane + 64 * j;
-          if (l < L) key[j] = hypot(sh.bx[l], sh.by[l]) == dmin ? dmin : INFINITY;
-        }
-      }
-      // the m smallest keys, ties to the lower index (synth: a stable argsort)
-      unsigned taken = 0;
-      for (; k < A.m; ++k) {
-        double best = INFINITY;
-        int bi = INT_MAX;
-#pragma unroll
-        for (int j = 0; j < kPerLane; ++j) {
-          const int l = lane + 64 * j;
-          if (!((taken >> j) & 1u) && (key[j] < best || (key[j] == best && l < bi)) && l < L) {
-            best = key[j];
-            bi = l;
-          }
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-          const double ob = __shfl_xor(best, o, 64);
-          const int oi = __shfl_xor(bi, o, 64);
-          if (ob < best || (ob == best && oi < bi)) {
-            best = ob;
-            bi = oi;
-          }
-        }
-        if (best == INFINITY) break;  // wave-uniform
-        if ((bi & 63) == lane) taken |= 1u << (bi >> 6);
-        if (lane == 0) sh.sel[k] = bi;
-      }
-    }
-    __syncthreads();
+    const int k = sense(A, lm, mode, th, px, py, sh, lane);
     // ---- markers: noise, record, descriptor ----
     const size_t rowo = static_cast<size_t>(t) * A.F + f;
-    int id = -1, act = 0;
-    double rx = 0.0, ry = 0.0;
-    if (lane < k) {
-      id = sh.sel[lane];
-      const unsigned long long idx = (static_cast<unsigned long long>(msg) * M + lane) * 2;
-      rx = sh.bx[id] + A.sigma * normal(seed, kNoiseStream, idx);
-      ry = sh.by[id] + A.sigma * normal(seed, kNoiseStream, idx + 1);
-      act = mode == kSenseAll && !(hypot(sh.bx[id], sh.by[id]) <= A.range) ? 2 : 0;  // DELETE
-      if (mode == kSenseSurvey) atomicOr(&sh.sighted[id >> 5], 1u << (id & 31));
-    }
-    if (A.out_ids) {
-      for (int i = lane; i < M; i += 64) {
-        const size_t o = rowo * M + i;
-        A.out_ids[o] = i < k ? __shfl(id, i, 64) : -1;
-        A.out_act[o] = i < k ? __shfl(act, i, 64) : 0;
-        A.out_rel[2 * o] = i < k ? __shfl(rx, i, 64) : 0.0;
-        A.out_rel[2 * o + 1] = i < k ? __shfl(ry, i, 64) : 0.0;
-      }
-      if (lane == 0) A.out_cnt[rowo] = k;
-    }
+    int id, act;
+    double rx, ry;
+    marker(A, seed, msg, mode, k, sh, lane, &id, &act, &rx, &ry);
+    if (lane < k && mode == kSenseSurvey) atomicOr(&sh.sighted[id >> 5], 1u << (id & 31));
+    if (A.out_ids) record_markers(A, rowo, k, id, act, rx, ry, lane);
     // the filter's chunk: the non-DELETE markers in order (slam.cpp:205), z as slam.cpp:208-210
     const bool add = lane < k && act != 2;
     const unsigned long long bal = __ballot(add);
@@ -271,8 +300,65 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
   for (int w = lane; w < words; w += 64) A.sighted[static_cast<size_t>(f) * words + w] = sh.sighted[w];
 }
 
+// ---- runs without SURVEY messages: every message sensed in parallel ----------------------------
+// Only the survey's sighted set carries sensing state from one message to the next; without it a
+// message's markers depend on its true pose alone. Pass 1 (k_sim_pose, one wave per filter) walks
+// the wheels message by message — the only sequential part, a scan per message — and writes every
+// message's true pose and odometry; pass 2 (k_sim_sense, one wave per message and filter, T·F in
+// flight instead of F) senses and records the markers as ekf_replay takes them, and the device
+// planner of ekf_replay_device (plan_kernels.hip) writes the descriptors from those. Same
+// functions, draws and order as k_sim, so the same bits.
+__global__ __launch_bounds__(64) void k_sim_pose(SimArgs A, double* truth_all, double* odom_all) {
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const unsigned long long seed = A.seed + static_cast<unsigned long long>(A.f0 + f);
+  SimState& S = A.st[f];
+  Pose2 truth{S.truth[0], S.truth[1], S.truth[2]};
+  Pose2 odo{S.odom[0], S.odom[1], S.odom[2]};
+  for (int t = 0; t < A.T; ++t) {
+    wheels(A, seed, t, lane, truth, odo);
+    const size_t o = (static_cast<size_t>(t) * A.F + f) * 3;
+    if (lane < 3) {
+      const double tv = lane == 0 ? truth.theta : (lane == 1 ? truth.x : truth.y);
+      const double ov = lane == 0 ? odo.theta : (lane == 1 ? odo.x : odo.y);
+      truth_all[o + lane] = tv;
+      odom_all[o + lane] = ov;
+      if (A.out_truth) A.out_truth[o + lane] = tv;
+      if (A.out_odom && f == 0) A.out_odom[static_cast<size_t>(t) * 3 + lane] = ov;
+    }
+  }
+  if (lane == 0) {
+    S.truth[0] = truth.theta;
+    S.truth[1] = truth.x;
+    S.truth[2] = truth.y;
+    S.odom[0] = odo.theta;
+    S.odom[1] = odo.x;
+    S.odom[2] = odo.y;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_sim_sense(SimArgs A, const double* truth_all) {
+  __shared__ SimShared sh;
+  const int t = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  const unsigned long long seed = A.seed + static_cast<unsigned long long>(A.f0 + f);
+  const size_t rowo = static_cast<size_t>(t) * A.F + f;
+  const double th = truth_all[rowo * 3], px = truth_all[rowo * 3 + 1], py = truth_all[rowo * 3 + 2];
+  const int mode = A.sense ? A.sense[t] : kSenseNearest;  // (never SURVEY here)
+  const int k = sense(A, A.lm + static_cast<size_t>(f) * A.L * 2, mode, th, px, py, sh, lane);
+  int id, act;
+  double rx, ry;
+  marker(A, seed, A.msg0 + t, mode, k, sh, lane, &id, &act, &rx, &ry);
+  record_markers(A, rowo, k, id, act, rx, ry, lane);
+}
+
 hipError_t launch_sim(const SimArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_sim, dim3(a.F), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sim_parallel(const SimArgs& a, double* truth_all, double* odom_all, hipStream_t s) {
+  hipLaunchKernelGGL(k_sim_pose, dim3(a.F), dim3(64), 0, s, a, truth_all, odom_all);
+  hipLaunchKernelGGL(k_sim_sense, dim3(a.T, a.F), dim3(64), 0, s, a,
+                     static_cast<const double*>(truth_all));
   return hipGetLastError();
 }
 

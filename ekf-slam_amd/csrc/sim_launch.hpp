@@ -37,5 +37,9 @@ struct SimArgs {
 };
 
 hipError_t launch_sim(const SimArgs& a, hipStream_t s);
+// A run without SURVEY messages (no sighted set carried between messages): k_sim_pose walks the
+// wheels per filter into truth_all / odom_all [T][F][3], then k_sim_sense senses every (t, f) in
+// parallel into the record arrays (out_ids / out_act / out_rel / out_cnt, required); no descriptors.
+hipError_t launch_sim_parallel(const SimArgs& a, double* truth_all, double* odom_all, hipStream_t s);
 
 }  // namespace ekfslam

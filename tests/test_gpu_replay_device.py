@@ -56,8 +56,11 @@ def _run(scs, N, F, spans, kinds, dtype=pyekf.EKF_F64, warm=None, holes=False):
             x, S, tmo, c = warm
             e.set_state(x, S, tmo=tmo, counter=c, f=f)
     keep = []
+    # the whole drive's inputs (holes at absolute message indices), cut into the spans
+    full = _inputs(scs, F, spans[0][0], spans[-1][1], holes)
     for (t0, t1), kind in zip(spans, kinds):
-        cnt, ids, act, rel, od = _inputs(scs, F, t0, t1, holes)
+        cnt, ids, act, rel, od = (np.ascontiguousarray(a[t0 - spans[0][0]:t1 - spans[0][0]])
+                                  for a in full)
         if kind == "device":
             g = _to_gpu((cnt, ids, act, rel, od))
             keep.append(g)

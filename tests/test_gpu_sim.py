@@ -173,6 +173,77 @@ def test_sim_then_host_call_predicts_from_the_sims_odometry():
     e.close()
 
 
+def _runs(sim, sw, bounds):
+    tpm = sw.wheel.shape[1]
+    parts = []
+    for a, b in bounds:
+        sim.run(sw.cmd[a * tpm:b * tpm], sw.sense[a:b])
+        parts.append(_check_inputs(sim, sw, a))
+    return [np.concatenate(p) for p in zip(*parts)]
+
+
+def test_sim_parallel_form_equals_sequential(monkeypatch):
+    """Runs without SURVEY messages take the parallel form on the pipeline (the wheels per filter,
+    then every (message, filter) sensed at once, planned by ekf_replay_device's planner): markers
+    and poses equal synth's as the sequential kernel's do, and the filter equals the sequential
+    form's to rounding (EKF_SIM_PARALLEL=0 plans each run on the host mirror: its first chunk gathers
+    Σ_in from HBM where the device planner's rebuilds it from the chunk before, kLook, and the
+    rebuild's MFMA sums D − K'·M' in another order than the Σ pass: ≤ 1e-14 relative, measured
+    7e-15 on the state) and the oracle fed the markers. N = 128, 8 filters: the survey in one run
+    (sequential), the circle in two runs."""
+    N, F = 128, 8
+    sw = synth.swarm(N, F, 14)
+    w = sw.n_warm
+    assert (sw.sense[:w] == synth.SENSE_SURVEY).any() and not (sw.sense[w:] == synth.SENSE_SURVEY).any()
+    bounds = ((0, w), (w, w + 6), (w + 6, w + 14))
+    out = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("EKF_SIM_PARALLEL", env)
+        e = pyekf.EKF(n_landmarks=N, n_filters=F)
+        sim = _sim_for(e, sw)
+        inputs = _runs(sim, sw, bounds)
+        out.append(([e.state(f) for f in range(F)], [e.status(f) for f in range(F)]))
+        sim.close()
+        e.close()
+    cnt, ids, act, rel, odom = inputs
+    for f in range(F):
+        (xa, Sa, ca), (xb, Sb, cb) = out[0][0][f], out[1][0][f]
+        assert out[0][1][f] == 0 and out[1][1][f] == 0
+        assert np.all(np.abs(xa - xb) <= 1e-12 * np.maximum(1.0, np.abs(xb))), f
+        assert np.all(np.abs(Sa - Sb) <= 1e-12 * np.maximum(1.0, np.abs(Sb))), f
+        assert ca == cb
+        if f in (0, 5):
+            xr, Sr, _, cr = _oracle(N, cnt, ids, act, rel, odom, f)
+            assert ca == cr
+            assert np.abs(xa - xr).max() < STATE_TOL_POPULATED, f
+            assert np.abs(Sa - Sr).max() < SIGMA_TOL, f
+
+
+def test_sim_parallel_form_sense_all_on_the_pipeline(monkeypatch):
+    """basic_world (every landmark reported, DELETE beyond range: SENSE_ALL) forced onto the HBM
+    pipeline (EKF_RESIDENT=0), so the parallel form runs it: inputs equal synth's, the filter the
+    oracle's (1e-8), across two runs that continue one another."""
+    monkeypatch.setenv("EKF_RESIDENT", "0")
+    F, T1, T2 = 16, 12, 10
+    drive = synth.circle_drive(T1 + T2, 0.3, sense=synth.SENSE_ALL)
+    seeds = np.uint64(4242) + np.arange(F, dtype=np.uint64)
+    sw = synth._generate(50, drive, seeds, synth.BASIC_WORLD_LANDMARKS,
+                         start_pose=(synth.BASIC_WORLD_THETA0, 0.0, 0.0), max_range=0.8)
+    assert (sw.actions == synth.DELETE).any()
+    e = pyekf.EKF(n_landmarks=50, n_filters=F)
+    assert e.path == pyekf.EKF_PATH_PIPELINE
+    sim = _sim_for(e, sw, max_range=0.8)
+    cnt, ids, act, rel, odom = _runs(sim, sw, ((0, T1), (T1, T1 + T2)))
+    for f in (0, 9, 15):
+        assert e.status(f) == 0
+        x, S, _ = e.state(f)
+        xr, Sr, _, _ = _oracle(50, cnt, ids, act, rel, odom, f)
+        assert np.abs(x - xr).max() < POSE_TOL, f
+        assert np.abs(S - Sr).max() < POSE_TOL, f
+    sim.close()
+    e.close()
+
+
 def test_sim_refuses_joseph_on_the_pipeline():
     """ekf_set_joseph on an HBM-pipeline handle (fp32): the device planner cannot write the
     one-marker chunks the form needs there, so ekf_sim_run returns EKF_E_ARG instead of running

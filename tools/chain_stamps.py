@@ -26,12 +26,17 @@ odom = pyekf.odometry(sc)
 w = sc.n_warm
 
 
+# EKF_STAMP_F=<filters>: the same messages replayed by that many filters of one handle (the swarm's
+# schedule: event hand-offs beyond 32 filters); the stamps are filter 0's
+F = int(os.environ.get("EKF_STAMP_F", "1"))
+
+
 def replay(e, sl):
-    e.replay(sc.count[sl, None], sc.rel[sl, None], odom[sl, None], ids=sc.ids[sl, None],
-             actions=sc.actions[sl, None])
+    rep = lambda a: np.ascontiguousarray(np.repeat(a[sl, None], F, axis=1))  # noqa: E731
+    e.replay(rep(sc.count), rep(sc.rel), rep(odom), ids=rep(sc.ids), actions=rep(sc.actions))
 
 
-e64 = pyekf.EKF(n_landmarks=N)
+e64 = pyekf.EKF(n_landmarks=N, n_filters=F)
 replay(e64, slice(0, w))
 if DT == "f32":
     x, S, cnt = e64.state()
