@@ -20,6 +20,7 @@
 #include <cmath>
 
 #include "ekf_device.hpp"
+#include "ekf_math.hpp"
 #include "geom.hpp"
 #include "sim_launch.hpp"
 
@@ -82,9 +83,10 @@ struct SimShared {
 };
 
 // One message's wheels (nusim.cpp:222-230, slam.cpp:599-634): lane j < tpm is tick j, the wave
-// composes the ticks' arcs by a scan, then the true pose and the odometry advance by the product.
-__device__ __forceinline__ void wheels(const SimArgs& A, unsigned long long seed, int t, int lane,
-                                       Pose2& truth, Pose2& odo) {
+// composes the ticks' arcs by a scan into the message's products (true, odometry; wave-uniform),
+// which the true pose and the odometry then advance by.
+__device__ __forceinline__ void arc_products(const SimArgs& A, unsigned long long seed, int t,
+                                             int lane, Pose2& pt, Pose2& po) {
   Pose2 dt{0.0, 0.0, 0.0}, dot{0.0, 0.0, 0.0};  // identity past the message's ticks
   if (lane < A.tpm) {
     const size_t k = static_cast<size_t>(t) * A.tpm + lane;
@@ -98,8 +100,15 @@ __device__ __forceinline__ void wheels(const SimArgs& A, unsigned long long seed
   dt = scan_compose(dt, lane);
   dot = scan_compose(dot, lane);
   const int last = A.tpm - 1;
-  truth = compose(truth, Pose2{bcast(dt.theta, last), bcast(dt.x, last), bcast(dt.y, last)});
-  odo = compose(odo, Pose2{bcast(dot.theta, last), bcast(dot.x, last), bcast(dot.y, last)});
+  pt = Pose2{bcast(dt.theta, last), bcast(dt.x, last), bcast(dt.y, last)};
+  po = Pose2{bcast(dot.theta, last), bcast(dot.x, last), bcast(dot.y, last)};
+}
+__device__ __forceinline__ void wheels(const SimArgs& A, unsigned long long seed, int t, int lane,
+                                       Pose2& truth, Pose2& odo) {
+  Pose2 pt, po;
+  arc_products(A, seed, t, lane, pt, po);
+  truth = compose(truth, pt);
+  odo = compose(odo, po);
 }
 
 // The fake sensor of one message at the true pose (th, px, py) (nusim.cpp:317-346): every
@@ -159,14 +168,9 @@ __device__ __forceinline__ int sense(const SimArgs& A, const double* lm, int mod
           bi = l;
         }
       }
-      for (int o = 32; o > 0; o >>= 1) {
-        const double ob = __shfl_xor(best, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ob < best || (ob == best && oi < bi)) {
-          best = ob;
-          bi = oi;
-        }
-      }
+      // (smaller key, ties to the lower index: a strict total order, so the DPP tree of
+      // ekf_math.hpp gives the pair the shuffle butterfly gave)
+      wave_argmin(best, bi);
       if (best == INFINITY) break;  // wave-uniform
       if ((bi & 63) == lane) taken |= 1u << (bi >> 6);
       if (lane == 0) sh.sel[k] = bi;
@@ -302,21 +306,36 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
 
 // ---- runs without SURVEY messages: every message sensed in parallel ----------------------------
 // Only the survey's sighted set carries sensing state from one message to the next; without it a
-// message's markers depend on its true pose alone. Pass 1 (k_sim_pose, one wave per filter) walks
-// the wheels message by message — the only sequential part, a scan per message — and writes every
-// message's true pose and odometry; pass 2 (k_sim_sense, one wave per message and filter, T·F in
+// message's markers depend on its true pose alone. Pass 1 (k_sim_arcs, one wave per message and
+// filter: each message's tick scan; then k_sim_pose, one wave per filter: the products composed in
+// message order — the only sequential part) writes every message's true pose and odometry; pass 2 (k_sim_sense, one wave per message and filter, T·F in
 // flight instead of F) senses and records the markers as ekf_replay takes them, and the device
 // planner of ekf_replay_device (plan_kernels.hip) writes the descriptors from those. Same
 // functions, draws and order as k_sim, so the same bits.
+// Pass 1a: each message's tick products (one wave per (message, filter), in parallel) into
+// truth_all / odom_all; pass 1b (k_sim_pose) composes them in message order over them.
+__global__ __launch_bounds__(64) void k_sim_arcs(SimArgs A, double* truth_all, double* odom_all) {
+  const int t = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  const unsigned long long seed = A.seed + static_cast<unsigned long long>(A.f0 + f);
+  Pose2 pt, po;
+  arc_products(A, seed, t, lane, pt, po);
+  const size_t o = (static_cast<size_t>(t) * A.F + f) * 3;
+  if (lane < 3) {
+    truth_all[o + lane] = lane == 0 ? pt.theta : (lane == 1 ? pt.x : pt.y);
+    odom_all[o + lane] = lane == 0 ? po.theta : (lane == 1 ? po.x : po.y);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_sim_pose(SimArgs A, double* truth_all, double* odom_all) {
   const int f = blockIdx.x, lane = threadIdx.x;
-  const unsigned long long seed = A.seed + static_cast<unsigned long long>(A.f0 + f);
   SimState& S = A.st[f];
   Pose2 truth{S.truth[0], S.truth[1], S.truth[2]};
   Pose2 odo{S.odom[0], S.odom[1], S.odom[2]};
   for (int t = 0; t < A.T; ++t) {
-    wheels(A, seed, t, lane, truth, odo);
     const size_t o = (static_cast<size_t>(t) * A.F + f) * 3;
+    // the message's products (k_sim_arcs), then the poses after it over them (same slot, same wave)
+    truth = compose(truth, Pose2{truth_all[o], truth_all[o + 1], truth_all[o + 2]});
+    odo = compose(odo, Pose2{odom_all[o], odom_all[o + 1], odom_all[o + 2]});
     if (lane < 3) {
       const double tv = lane == 0 ? truth.theta : (lane == 1 ? truth.x : truth.y);
       const double ov = lane == 0 ? odo.theta : (lane == 1 ? odo.x : odo.y);
@@ -356,6 +375,7 @@ hipError_t launch_sim(const SimArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_sim_parallel(const SimArgs& a, double* truth_all, double* odom_all, hipStream_t s) {
+  hipLaunchKernelGGL(k_sim_arcs, dim3(a.T, a.F), dim3(64), 0, s, a, truth_all, odom_all);
   hipLaunchKernelGGL(k_sim_pose, dim3(a.F), dim3(64), 0, s, a, truth_all, odom_all);
   hipLaunchKernelGGL(k_sim_sense, dim3(a.T, a.F), dim3(64), 0, s, a,
                      static_cast<const double*>(truth_all));
