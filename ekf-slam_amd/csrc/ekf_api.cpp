@@ -1089,8 +1089,11 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipMalloc(&h->mcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->ctl, sizeof(FilterCtl) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->rec, 2 * sizeof(ChunkRec) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
-  const char* rows_env = std::getenv("EKF_ROWS");  // EKF_ROWS=0: always gather (tests)
-  if (cfg.dtype == EKF_F64 && !(rows_env && std::atoi(rows_env) == 0) &&
+  // the Σ-pass → factor-kernel row hand-off (EKF_ROWS=1): coalesced Σ_in[i, U] for the factor
+  // kernel's row waves. Off by default since the fp64 pass is symmetric (the row waves read
+  // Σ_in[U, i], the same 128 B lines, without the pass's extra stores)
+  const char* rows_env = std::getenv("EKF_ROWS");
+  if (cfg.dtype == EKF_F64 && rows_env && std::atoi(rows_env) != 0 &&
       // fp32's U block is rewritten after its pass (k_patch_stage): gathered there
       hipMalloc(&h->rows, sizeof(double) * kRowW * h->ldk * h->F) != hipSuccess)
     return fail(EKF_E_NOMEM);
@@ -1668,7 +1671,10 @@ int ekf_diag_am_stamps(unsigned long long* out) { return ekfslam_diag_read_am_st
 
 double ekf_sigma_pass_bytes(ekf_t h, int nf) {
   if (!h) return 0.0;
-  return 2.0 * static_cast<double>(h->n) * h->n * static_cast<double>(h->w) * nf;
+  const double n = h->n;
+  // fp64: the symmetric pass (k_sigma_pass, SigmaTile64) reads the upper triangle of Σ_in only
+  const double elems = h->w == 8 ? n * (n + 1) / 2 + n * n : 2.0 * n * n;
+  return elems * static_cast<double>(h->w) * nf;
 }
 
 }  // extern "C"

@@ -1883,6 +1883,50 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
   const int row_tiles = (n + 15) / 16;
   const int ks = lane >> 4, l16 = lane & 15;
   const double s00 = sh.s00;
+  // Mcat columns j = C0 + l16 of a wave from Σ_in[U, j] (raw) and Σ_in[0, j] (c0t)
+  auto columns = [&](int j, const T (&raw)[9], T c0t) {
+    const bool vj = j < n;
+    const double c0raw = vj ? static_cast<double>(c0t) : 0.0;
+    const double aj = first ? alpha_of(j, sh.a1, sh.a2) : 0.0;
+    double bv[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      double v = (vj && k < nu) ? static_cast<double>(raw[s]) : 0.0;
+      if (first && vj && k < nu) {
+        v = v + sh.alphaU[k] * c0raw;
+        v = v + (sh.col0raw[k] + sh.alphaU[k] * s00) * aj;
+        if (sh.u[k] == j && j < 3) v += A.q;
+      }
+      bv[s] = v;
+    }
+    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      const double y0 = k < kMaxU ? sh.Y[l16][k] : 0.0;
+      const double y1 = k < kMaxU ? sh.Y[16 + l16][k] : 0.0;
+      acc0 = mfma_f64(y0, bv[s], acc0);
+      acc1 = mfma_f64(y1, bv[s], acc1);
+    }
+    if (vj && ks == 0) {
+      mc[0 * ldk + j] = static_cast<T>(first ? c0raw : 0.0);
+      mc[1 * ldk + j] = static_cast<T>(first ? aj : 0.0);
+    }
+    if (vj) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kr = ks + 4 * r;
+        if (!(joseph && (kr == 2 || kr == 3)))  // (Joseph: the row waves write K there)
+          mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
+        mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
+      }
+    }
+  };
+  // fp64 without the row hand-off: Σ_in is symmetric, so a row wave's Σ_in[U, i] are also its
+  // columns' — one wave per 16 indices builds both Kcat rows and Mcat columns (half the waves
+  // and half the Σ_in reads of separate row and column waves, the same values)
+  const bool merged = sizeof(T) == 8 && A.rows == nullptr;
   if (wg < row_tiles) {
     const int R0 = wg * 16;
     const int i = R0 + l16;
@@ -1897,6 +1941,14 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
       r0t = rr[0];  // u_0 = 0
 #pragma unroll
       for (int s = 0; s < 9; ++s) raw[s] = rr[static_cast<size_t>(4 * s + ks) * A.ldk];
+    } else if (sizeof(T) == 8) {
+      // fp64 Σ is symmetric (the symmetric Σ pass mirrors every element below the diagonal), so
+      // Σ_in[i, U] is read as Σ_in[U, i]: 16 consecutive i per row of U (128 B) instead of one
+      // scattered element per lane and column of U
+      r0t = S[vi ? i : 0];
+#pragma unroll
+      for (int s = 0; s < 9; ++s)
+        raw[s] = S[static_cast<size_t>(sh.u[min(4 * s + ks, kMaxU - 1)]) * ld + (vi ? i : 0)];
     } else {
       r0t = rowp[0];
 #pragma unroll
@@ -1946,7 +1998,8 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
         }
       }
     }
-  } else if (wg < 2 * row_tiles) {
+    if (merged) columns(i, raw, r0t);
+  } else if (!merged && wg < 2 * row_tiles) {
     const int C0 = (wg - row_tiles) * 16;
     const int j = C0 + l16;
     const bool vj = j < n;
@@ -1956,42 +2009,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
 #pragma unroll
     for (int s = 0; s < 9; ++s)
       raw[s] = S[static_cast<size_t>(sh.u[min(4 * s + ks, kMaxU - 1)]) * ld + jj];
-    const double c0raw = vj ? static_cast<double>(c0t) : 0.0;
-    const double aj = first ? alpha_of(j, sh.a1, sh.a2) : 0.0;
-    double bv[9];
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      const int k = 4 * s + ks;
-      double v = (vj && k < nu) ? static_cast<double>(raw[s]) : 0.0;
-      if (first && vj && k < nu) {
-        v = v + sh.alphaU[k] * c0raw;
-        v = v + (sh.col0raw[k] + sh.alphaU[k] * s00) * aj;
-        if (sh.u[k] == j && j < 3) v += A.q;
-      }
-      bv[s] = v;
-    }
-    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      const int k = 4 * s + ks;
-      const double y0 = k < kMaxU ? sh.Y[l16][k] : 0.0;
-      const double y1 = k < kMaxU ? sh.Y[16 + l16][k] : 0.0;
-      acc0 = mfma_f64(y0, bv[s], acc0);
-      acc1 = mfma_f64(y1, bv[s], acc1);
-    }
-    if (vj && ks == 0) {
-      mc[0 * ldk + j] = static_cast<T>(first ? c0raw : 0.0);
-      mc[1 * ldk + j] = static_cast<T>(first ? aj : 0.0);
-    }
-    if (vj) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kr = ks + 4 * r;
-        if (!(joseph && (kr == 2 || kr == 3)))  // (Joseph: the row waves write K there)
-          mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
-        mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
-      }
-    }
+    columns(j, raw, c0t);
   }
 }
 
@@ -2123,18 +2141,31 @@ struct SigmaTile<float> {
 #ifndef EKF_SIG_POL
 #define EKF_SIG_POL 2
 #endif
+// Symmetric: Σ_out is symmetric (Σ_in + Q̄ − Kcatᵀ·Mcat is, the predict's A·Σ·Aᵀ and every
+// correction's K·S·Kᵀ are), so an fp64 pass computes only the tiles holding an element on or above
+// the diagonal (first tile column of tile row tr: ⌊32·tr / kCols⌋) and writes every element (r, c),
+// r > c, as the mirror of (c, r): Σ_in is read in those tiles only (≈ 0.58 of Σ at the swarm's n),
+// the MFMA work of the strictly-lower tiles is skipped, and Σ_out stays exactly symmetric. The
+// mirror goes out through the wave's LDS (the tile transposed, then row by row: a direct
+// transposed store is 16 rows × 32 B per instruction, measured 1.5× slower than the whole pass).
+// Swarm pass 445 → 379 µs standalone, bit-identical in the upper triangle (tools/pass64_lab.hip).
+constexpr int kTS = 34;  // transposed tile row stride (doubles; 16 B aligned rows)
 template <int TJ_>
 struct SigmaTile64 {
   static constexpr int TJ = TJ_;
   // cache policy of the swarm tile's Σ_in loads / Σ_out stores (the swarm's Σ streams through HBM)
   static constexpr int kPol = TJ == 4 ? EKF_SIG_POL : 0;
   static constexpr int kRows = 32, kCols = 16 * TJ;
+  static constexpr int kLds = kCols * kTS;  // doubles of the wave's transposed tile
   // rows ≠ null (kRowsOut): also Σ_out[i, U_next] → rows[b·ldk + i] for the next chunk's factor
-  // kernel, b = the first position of the column in U_next (nxt[0..nnu))
+  // kernel, b = the first position of the column in U_next (nxt[0..nnu)); (i, u) comes from the
+  // upper element (min, max), so a tile hands off its columns in U_next on and above the diagonal
+  // and its rows in U_next right of it
   static __device__ __forceinline__ void run(const double* Sin, double* Sout, const double* kc,
                                              const double* mc, int n, int ld, int ldk, int kw,
                                              bool first, double q, int R0, int C0, int lane,
-                                             double* rows, const int* nxt, int nnu, int* map) {
+                                             double* rows, const int* nxt, int nnu, int* map,
+                                             int* rmap, double* tT) {
     const int kr = lane >> 4, kcol = lane & 15;
     // descriptors based at the wave's row panel: offsets stay 32-bit for any n (a filter's Σ
     // may exceed 4 GiB), and the records end at row n
@@ -2142,6 +2173,9 @@ struct SigmaTile64 {
     const unsigned sbytes = static_cast<unsigned>(min(n - R0, kRows)) * ld * 8u;
     const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 8u;
     const auto rin = buf_rsrc(Sin + pbase, sbytes), rout = buf_rsrc(Sout + pbase, sbytes);
+    // the mirror: rows C0 … C0 + kCols − 1 of Σ_out from column R0
+    const auto rmir = buf_rsrc(Sout + static_cast<size_t>(C0) * ld + R0,
+                               static_cast<unsigned>(min(n - C0, kCols)) * ld * 8u);
     const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
     double a[2][9], b[TJ][9], sv[2][TJ][4];
     const int uk = rows ? nxt[min(lane, kMaxU)] : 0;  // issued with the operand loads
@@ -2185,19 +2219,32 @@ struct SigmaTile64 {
           acc[ti][tj] = mfma_f64(live ? a[ti][s] : 0.0, live ? b[tj][s] : 0.0, acc[ti][tj]);
     }
     SIG_STAMP(2);
-    int bpos[TJ];
+    int bpos[TJ], rpos[2][4];
 #pragma unroll
     for (int tj = 0; tj < TJ; ++tj) bpos[tj] = -1;
-    if (rows) {  // wave-uniform: positions of the tile's columns in U_next through this wave's LDS
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rpos[ti][r] = -1;
+    if (rows) {  // wave-uniform: positions of the tile's columns and rows in U_next (this wave's LDS)
       map[lane] = kMaxU + 1;
+      if (lane < kRows) rmap[lane] = kMaxU + 1;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       if (lane < nnu && uk >= C0 && uk < C0 + kCols) atomicMin(&map[uk - C0], lane);
+      if (lane < nnu && uk >= R0 && uk < R0 + kRows) atomicMin(&rmap[uk - R0], lane);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) {
-        const int b = map[16 * tj + kcol];
-        bpos[tj] = b <= kMaxU ? b : -1;
+        const int bb = map[16 * tj + kcol];
+        bpos[tj] = bb <= kMaxU ? bb : -1;
       }
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int bb = rmap[16 * ti + kr + 4 * r];
+          rpos[ti][r] = bb <= kMaxU ? bb : -1;
+        }
     }
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
@@ -2205,15 +2252,53 @@ struct SigmaTile64 {
       for (int tj = 0; tj < TJ; ++tj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = R0 + 16 * ti + kr + 4 * r, col = C0 + 16 * tj + kcol;
+          const int rl = 16 * ti + kr + 4 * r, cl = 16 * tj + kcol;
+          const int row = R0 + rl, col = C0 + cl;
           double v = sv[ti][tj][r] - acc[ti][tj][r];
           if (first && row == col && row < 3) v += q;
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rout,
-                                                so[tj] + (16 * ti + 4 * r) * rstride, 0, kPol);
-          if (bpos[tj] >= 0 && row < n) rows[static_cast<size_t>(bpos[tj]) * ldk + row] = v;
+                                                col >= row ? so[tj] + (16 * ti + 4 * r) * rstride : kOOB,
+                                                0, kPol);
+          tT[cl * kTS + rl] = v;
+          if (col >= row && row < n && col < n) {
+            if (bpos[tj] >= 0) rows[static_cast<size_t>(bpos[tj]) * ldk + row] = v;
+            if (col > row && rpos[ti][r] >= 0) rows[static_cast<size_t>(rpos[ti][r]) * ldk + col] = v;
+          }
         }
+    // the mirror, two rows of the transposed tile per store (LDS in order within the wave)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int rl = lane & 31;
+#pragma unroll
+    for (int i = 0; i < kCols / 2; ++i) {
+      const int cl = 2 * i + (lane >> 5);
+      const double v = tT[cl * kTS + rl];
+      const int row = R0 + rl, col = C0 + cl;
+      const unsigned mo2 = col > row && col < n ? static_cast<unsigned>(cl * ld + rl) * 8u : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rmir, mo2, 0, kPol);
+    }
   }
 };
+// the tiles of a symmetric pass: tile row tr holds tile columns ⌊32·tr / kCols⌋ … tcols − 1
+template <int kCols>
+__host__ __device__ inline int sym_first(int tr) { return 32 * tr / kCols; }
+template <int kCols>
+__host__ __device__ inline int sym_tiles(int trows, int tcols) {
+  int t = 0;
+  for (int tr = 0; tr < trows; ++tr) t += tcols - sym_first<kCols>(tr);
+  return t;
+}
+// the t-th of them, row-major (wave-uniform t: a scalar walk over the tile rows)
+template <int kCols>
+__device__ __forceinline__ bool sym_tile(int t, int trows, int tcols, int& tr, int& tc) {
+  int base = 0;
+  for (tr = 0; tr < trows; ++tr) {
+    const int c = tcols - sym_first<kCols>(tr);
+    if (t < base + c) break;
+    base += c;
+  }
+  tc = tr < trows ? sym_first<kCols>(tr) + (t - base) : 0;
+  return tr < trows;
+}
 template <>
 struct SigmaTile<double> : SigmaTile64<2> {};
 // the tile a Σ pass of T runs: WIDE (swarms) takes the 32 × 64 fp64 tile
@@ -2249,7 +2334,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
     if (fb >= nf) return;
   }
   const MsgDesc& d = A.desc[fb];
+  constexpr bool kSym = sizeof(T) == 8;  // fp64: the symmetric tiles (SigmaTile64)
   __shared__ int cmap[4][64];  // per wave: kRowsOut column → position in U_next
+  __shared__ int rmap[kSym ? 4 : 1][32];  // … and row (the symmetric tiles)
+  __shared__ double tT[kSym ? 4 : 1][kSym ? 16 * (WIDE ? 4 : 2) * kTS : 1];  // (SigmaTile64::kLds)
   const int lane = threadIdx.x & 63;
   const int trows = (A.n + Tile::kRows - 1) / Tile::kRows;
   // the wave's tile index, provably wave-uniform (readfirstlane): the buffer descriptors built
@@ -2257,7 +2345,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
   int t = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   int tr = 0, tc = 0;
   bool ok;
-  if (xcd_b < 0) {
+  if constexpr (kSym) {
+    // the upper tiles row-major; xcd_b < 0: XCD x takes the x-th eighth of them
+    if (xcd_b < 0) {
+      const int x = blockIdx.x & 7, w = (blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+      const int T8 = sym_tiles<Tile::kCols>(trows, tcols);
+      const int lo = x * T8 / 8, hi = (x + 1) * T8 / 8;
+      t = __builtin_amdgcn_readfirstlane(lo + w);
+      ok = t < hi;
+    } else {
+      ok = true;
+    }
+    ok = ok && sym_tile<Tile::kCols>(t, trows, tcols, tr, tc);
+  } else if (xcd_b < 0) {
     const int x = blockIdx.x & 7, w = (blockIdx.x >> 3) * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int hx = x / kRegCols, qx = x % kRegCols;
     const int r0 = hx * trows / kRegRows, r1 = (hx + 1) * trows / kRegRows;
@@ -2300,7 +2400,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
                       A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
                       (d.flags & kFirst) != 0, A.q, tr * Tile::kRows,
                       tc * Tile::kCols, lane, rows, d.nxt_u, d.nxt_nu,
-                      cmap[threadIdx.x >> 6]);
+                      cmap[threadIdx.x >> 6], rmap[threadIdx.x >> 6], tT[threadIdx.x >> 6]);
   }
   SIG_STAMP(3);
 }
@@ -2608,7 +2708,8 @@ hipError_t launch_chain(const PassArgs<T>& a, int nf, int nchunks, hipStream_t s
 template <typename T>
 hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1) {
-  const int waves = 2 * ((a.n + 15) / 16);  // 16 rows or 16 columns per wave
+  // 16 rows or 16 columns per wave; fp64 without the row hand-off: both (k_factors `merged`)
+  const int waves = (sizeof(T) == 8 && !a.rows ? 1 : 2) * ((a.n + 15) / 16);
   const int per_filter = (waves + 3) / 4;
   if (nf >= 16) {  // XCD-aware 1-D grid, as the swarm's Σ pass
     launch(k_factors<T>, dim3(8 * ((nf + 7) / 8) * per_filter), dim3(256), s, e0, e1, a,
@@ -2623,11 +2724,16 @@ template <typename T>
 hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool stage, hipStream_t s,
                              hipEvent_t e0, hipEvent_t e1) {
   constexpr int wpb = 4;  // waves per workgroup
+  // the tiles per filter: all of them, or (fp64, symmetric) those on or above the diagonal
+  auto tiles = [](int trows, int tcols, auto tile) {
+    using Tile = decltype(tile);
+    return sizeof(T) == 8 ? sym_tiles<Tile::kCols>(trows, tcols) : trows * tcols;
+  };
   if (nf >= 16) {  // XCD-aware 1-D grid (see k_sigma_pass), wide fp64 tiles
     using Tile = PassTile<T, true>;
     const int trows = (a.n + Tile::kRows - 1) / Tile::kRows;
     const int tcols = (a.n + Tile::kCols - 1) / Tile::kCols;
-    const int per_filter = (trows * tcols + wpb - 1) / wpb;
+    const int per_filter = (tiles(trows, tcols, Tile{}) + wpb - 1) / wpb;
     const dim3 grid(8 * ((nf + 7) / 8) * per_filter);
     launch(k_sigma_pass<T, true>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, per_filter, nf);
   } else {
@@ -2635,10 +2741,11 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool st
     const int trows = (a.n + Tile::kRows - 1) / Tile::kRows;
     const int tcols = (a.n + Tile::kCols - 1) / Tile::kCols;
     if (trows >= 2 * kRegRows && tcols >= 2 * kRegCols) {  // XCD regions (k_sigma_pass)
-      const dim3 grid(8 * ((region_tiles(trows, tcols) + wpb - 1) / wpb), nf);
+      const int per_x = sizeof(T) == 8 ? (tiles(trows, tcols, Tile{}) + 7) / 8 : region_tiles(trows, tcols);
+      const dim3 grid(8 * ((per_x + wpb - 1) / wpb), nf);
       launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, -1, nf);
     } else {
-      const int per_filter = (trows * tcols + wpb - 1) / wpb;
+      const int per_filter = (tiles(trows, tcols, Tile{}) + wpb - 1) / wpb;
       const dim3 grid(per_filter, nf);
       launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
     }

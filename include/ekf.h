@@ -207,7 +207,8 @@ double ekf_normalize_angle(double rad);
  * execution, on the stream it runs on). Off by default. */
 int ekf_profile_enable(ekf_t h, int enable);
 int ekf_profile_read(ekf_t h, int kernel, long long* launches, double* total_ms);
-/* Bytes the Σ pass must move per launch for the current handle (2·n²·w·F). */
+/* Bytes the Σ pass must move per launch for the current handle: fp32 2·n²·w·F (Σ_in read, Σ_out
+ * written); fp64 (n(n+1)/2 + n²)·w·F (the symmetric pass reads Σ_in's upper triangle). */
 double ekf_sigma_pass_bytes(ekf_t h, int filters_in_launch);
 
 /* ---- diagnostics ---- */

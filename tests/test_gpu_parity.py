@@ -306,15 +306,17 @@ def test_many_filters_match_small_batch(F, devsync, monkeypatch):
                          ids=["1filter", "4filters", "40filters", "1filter_devsync",
                               "4filters_devsync"])
 def test_rows_handoff_is_bit_identical(monkeypatch, F, env):
-    """fp64: a Σ pass hands the next chunk's factor kernel Σ_in[i, U] as contiguous rows
-    (kRowsOut / kRowsIn) — the very values it stores into Σ_out, so the replay equals the strided
-    gather (EKF_ROWS=0) bit for bit, including messages longer than one chunk; in the event-
-    synchronised schedule and the (default) device-epoch one (LDS poisoned first)."""
+    """fp64: with EKF_ROWS=1 a Σ pass hands the next chunk's factor kernel Σ_in[i, U] as contiguous
+    rows (kRowsOut / kRowsIn) — the very values it stores into Σ_out (the symmetric pass: from a
+    tile's columns in U on and above the diagonal, and its rows in U right of it), so the replay
+    equals the default's reads of Σ_in[U, i] (EKF_ROWS=0) bit for bit, including messages longer
+    than one chunk; in the event-synchronised schedule and the (default) device-epoch one (LDS
+    poisoned first)."""
     if env.get("EKF_DEVSYNC") != "0":
         pyekf.poison_lds()
     sc = synth.synthetic(96, 14, max_markers=24)
     assert sc.count.max() > 16  # some messages span two chunks
-    monkeypatch.delenv("EKF_ROWS", raising=False)
+    monkeypatch.setenv("EKF_ROWS", "1")
     on = _pipelined_final(sc, monkeypatch, env, F=F)
     monkeypatch.setenv("EKF_ROWS", "0")
     off = _pipelined_final(sc, monkeypatch, env, F=F)

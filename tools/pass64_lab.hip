@@ -315,6 +315,170 @@ __global__ __launch_bounds__(256) void k_sigma_stream(PassArgs<double> A, int tc
 }
 #pragma clang diagnostic pop
 
+// ---- symmetric pass: only the tiles holding an element on or above the diagonal -----------------
+// Σ_out is symmetric, so element (r, c), r > c, is the mirror of (c, r): a tile computes as the
+// product's does, stores its elements with c ≥ r in place and those with c > r mirrored to (c, r)
+// (16 rows × 32 B per store instruction, four instructions fill 128 B of each mirrored row).
+// Σ_in is read in the upper tiles only, the MFMA work of the strictly-lower tiles is skipped.
+// kRowsOut: (i, u) for u ∈ U_next comes from the upper element (min, max), so a tile also hands
+// off its rows that are in U_next, at the columns right of the diagonal.
+__device__ __forceinline__ void sym_tile(int t, int trows, int tcols, int& tr, int& tc, bool& ok) {
+  tr = 0;
+  int base = 0;
+  for (; tr < trows; ++tr) {
+    const int c = tcols - tr / 2;
+    if (t < base + c) break;
+    base += c;
+  }
+  ok = tr < trows;
+  tc = tr / 2 + (t - base);
+}
+constexpr int kTS = 34;  // transposed tile row stride (doubles): 16 B aligned rows
+template <int MIR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_sym(PassArgs<double> A, int tcols, int xcd_b, int nf) {
+  const int L = blockIdx.x, j = L >> 3;
+  const int fb = (L & 7) + 8 * (j / xcd_b), bx = j % xcd_b;
+  if (fb >= nf) return;
+  const MsgDesc& d = A.desc[fb];
+  __shared__ int cmap[4][64], rmap[4][32];
+  __shared__ double tT[MIR ? 4 : 1][MIR ? 64 * kTS : 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int trows = (A.n + 31) / 32;
+  const int t = __builtin_amdgcn_readfirstlane(bx * 4 + wv);
+  int tr, tc;
+  bool ok;
+  sym_tile(t, trows, tcols, tr, tc, ok);
+  if (!ok || !(d.flags & kActive)) return;
+  const int R0 = tr * 32, C0 = tc * 64;
+  const int f = A.f0 + fb;
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const double* Sin = A.sig[d.parity] + f * A.sig_stride;
+  double* Sout = A.sig[d.parity ^ 1] + f * A.sig_stride;
+  const double* kc = A.kcat + f * A.km_stride;
+  const double* mc = A.mcat + f * A.km_stride;
+  constexpr int TJ = 4;
+  const int kr = lane >> 4, kcol = lane & 15;
+  const size_t pbase = static_cast<size_t>(R0) * ld;
+  const unsigned sbytes = static_cast<unsigned>(min(n - R0, 32)) * ld * 8u;
+  const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 8u;
+  const auto rin = buf_rsrc(Sin + pbase, sbytes), rout = buf_rsrc(Sout + pbase, sbytes);
+  // the mirror: rows C0 … C0+63 of Σ_out, columns R0 …
+  const size_t mbase = static_cast<size_t>(C0) * ld + R0;
+  const unsigned mbytes = static_cast<unsigned>(min(n - C0, 64)) * ld * 8u;
+  const auto rmir = buf_rsrc(Sout + mbase, mbytes);
+  const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
+  double a[2][9], b[TJ][9], sv[2][TJ][4];
+  const bool rows_on = (d.flags & kRowsOut) != 0;
+  const int uk = rows_on ? d.nxt_u[min(lane, kMaxU)] : 0;
+  const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 8u;
+  unsigned mo[TJ], so[TJ];
+  const unsigned rstride = static_cast<unsigned>(ld) * 8u;
+#pragma unroll
+  for (int tj = 0; tj < TJ; ++tj) {
+    const int col = C0 + 16 * tj + kcol;
+    mo[tj] = static_cast<unsigned>(kr * ldk + min(col, n - 1)) * 8u;
+    so[tj] = col < n ? static_cast<unsigned>(kr * ld + col) * 8u : kOOB;
+  }
+  const unsigned kstep = 4u * ldk * 8u;
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    a[0][s] = ld_f64(rk, ko, s * kstep);
+    a[1][s] = ld_f64(rk, ko + 16 * 8, s * kstep);
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) b[tj][s] = ld_f64(rm, mo[tj], s * kstep);
+  }
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sv[ti][tj][r] = __builtin_bit_cast(
+            double, __builtin_amdgcn_raw_buffer_load_b64(rin, so[tj] + (16 * ti + 4 * r) * rstride, 0, 2));
+  d4 acc[2][TJ];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = d4{0, 0, 0, 0};
+  const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    const bool live = 4 * s < kw;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+        acc[ti][tj] = mfma_f64(live ? a[ti][s] : 0.0, live ? b[tj][s] : 0.0, acc[ti][tj]);
+  }
+  int bpos[TJ], rpos[2][4];
+#pragma unroll
+  for (int tj = 0; tj < TJ; ++tj) bpos[tj] = -1;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rpos[ti][r] = -1;
+  if (rows_on) {
+    int* map = cmap[wv];
+    int* rmp = rmap[wv];
+    map[lane] = kMaxU + 1;
+    if (lane < 32) rmp[lane] = kMaxU + 1;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int nnu = d.nxt_nu;
+    if (lane < nnu && uk >= C0 && uk < C0 + 64) atomicMin(&map[uk - C0], lane);
+    if (lane < nnu && uk >= R0 && uk < R0 + 32) atomicMin(&rmp[uk - R0], lane);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj) {
+      const int bb = map[16 * tj + kcol];
+      bpos[tj] = bb <= kMaxU ? bb : -1;
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int bb = rmp[16 * ti + kr + 4 * r];
+        rpos[ti][r] = bb <= kMaxU ? bb : -1;
+      }
+  }
+  const bool first = (d.flags & kFirst) != 0;
+  const double q = A.q;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = 16 * ti + kr + 4 * r, cl = 16 * tj + kcol;
+        const int row = R0 + rl, col = C0 + cl;
+        double v = sv[ti][tj][r] - acc[ti][tj][r];
+        if (first && row == col && row < 3) v += q;
+        const u2v w = __builtin_bit_cast(u2v, v);
+        __builtin_amdgcn_raw_buffer_store_b64(w, rout, col >= row ? so[tj] + (16 * ti + 4 * r) * rstride : kOOB, 0, 2);
+        if (MIR) {
+          tT[wv][cl * kTS + rl] = v;
+        } else {
+          const unsigned mo2 = col > row && col < n ? static_cast<unsigned>(cl * ld + rl) * 8u : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b64(w, rmir, mo2, 0, 2);
+        }
+        if (col >= row && row < n && col < n) {
+          if (bpos[tj] >= 0) A.rows[f * A.rows_stride + static_cast<size_t>(bpos[tj]) * ldk + row] = v;
+          if (col > row && rpos[ti][r] >= 0) A.rows[f * A.rows_stride + static_cast<size_t>(rpos[ti][r]) * ldk + col] = v;
+        }
+      }
+  if (MIR) {  // the mirror: row cl of the transposed tile → Σ_out row C0 + cl, columns R0 …, 2 rows per store
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int rl = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int cl = 2 * i + (lane >> 5);
+      const double v = tT[wv][cl * kTS + rl];
+      const int row = R0 + rl, col = C0 + cl;
+      const unsigned mo2 = col > row && col < n ? static_cast<unsigned>(cl * ld + rl) * 8u : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rmir, mo2, 0, 2);
+    }
+  }
+}
+
 template <typename V>
 __global__ void k_copy(const V* __restrict__ in, V* __restrict__ out, size_t nv) {
   for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) out[i] = in[i];
@@ -432,13 +596,44 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(k_sigma_stream, dim3(blocks), dim3(256), 0, st, a, tcols, trows * tcols, F);
     };
   };
+  int sym_tiles = 0;
+  for (int tr = 0; tr < trows; ++tr) sym_tiles += tcols - tr / 2;
+  const int sym_pf = (sym_tiles + 3) / 4;
+  auto sym = [&](hipStream_t st) {
+    constexpr int MIRV = 1;
+    hipLaunchKernelGGL(k_sym<MIRV>, dim3(8 * ((F + 7) / 8) * sym_pf), dim3(256), 0, st, a, tcols, sym_pf, F);
+  };
+  auto sym_check = [&]() {  // Σ_out(r, c) = product's (min, max); rows(b, i) = product's (min(i, u), max)
+    size_t bad = 0, rbad = 0;
+    for (int f = 0; f < F; ++f) {
+      for (int r = 0; r < n; ++r)
+        for (int c = 0; c < n; ++c) {
+          const size_t o = f * stride + static_cast<size_t>(r) * ld + c;
+          const size_t oe = f * stride + static_cast<size_t>(std::min(r, c)) * ld + std::max(r, c);
+          if (std::memcmp(&out[o], &ref[oe], 8)) ++bad;
+        }
+      if (hd[f].flags & kRowsOut)
+        for (int bb = 0; bb < hd[f].nxt_nu; ++bb) {
+          bool firstpos = true;
+          for (int k = 0; k < bb; ++k) firstpos = firstpos && hd[f].nxt_u[k] != hd[f].nxt_u[bb];
+          if (!firstpos) continue;
+          const int u = hd[f].nxt_u[bb];
+          for (int i = 0; i < n; ++i) {
+            const size_t o = f * a.rows_stride + static_cast<size_t>(bb) * ldk + i;
+            const size_t oe = f * stride + static_cast<size_t>(std::min(i, u)) * ld + std::max(i, u);
+            if (std::memcmp(&rout[o], &ref[oe], 8)) ++rbad;
+          }
+        }
+    }
+    printf("  symmetric check vs product's upper triangle: mismatches %zu rows %zu (%d of %d tiles)\n", bad, rbad,
+           sym_tiles, trows * tcols);
+  };
   for (int round = 0; round < 2; ++round) {
-    time_it("stream 1 wg/cu", stream(dev_cus), true);
-    time_it("stream 0.75 wg/cu", stream(dev_cus * 3 / 4 / 8 * 8), true);
+    time_it("symmetric k_sym (LDS transpose)", sym, false);
+    sym_check();
     time_it("product k_sigma_pass", prod, true);
     time_it("ablate: copy of product", abl(k_ablate<0>), false);
     time_it("ablate: no mfma", abl(k_ablate<kNoMfma>), false);
-    time_it("ablate: no operands", abl(k_ablate<kNoOps>), false);
     time_it("ablate: sigma only", abl(k_ablate<kNoMfma | kNoOps>), false);
   }
   return 0;
