@@ -1975,27 +1975,28 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
       const double z0 = k < kMaxU ? sh.Z[k][l16] : 0.0;
       const double z1 = k < kMaxU ? sh.Z[k][16 + l16] : 0.0;
       const double zx = (k < kMaxU && l16 == 0) ? sh.Zx[k] : 0.0;
-      acc0 = mfma_f64(av[s], z0, acc0);
-      acc1 = mfma_f64(av[s], z1, acc1);
-      acc2 = mfma_f64(av[s], zx, acc2);
+      // Zᵀ·R rather than R·Z: the lane then holds Kcat[c = ks + 4r][i = R0 + l16], so each store
+      // covers 4 factor rows × 128 B instead of 16 rows × 32 B (the same products and sums)
+      acc0 = mfma_f64(z0, av[s], acc0);
+      acc1 = mfma_f64(z1, av[s], acc1);
+      acc2 = mfma_f64(zx, av[s], acc2);
     }
     const int rbase = bx * 64;
     if (vi && ks == 0) {  // the predict's two rank-1 factors (slam.cpp:198)
       kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
       kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
+      // rows of U take the chain's x (first position of the row in U)
+      const int pos = sh.pos64[i - rbase];
+      xout[i] = pos < nu ? xfin[pos] : xin[i] + acc2[0];
     }
+    if (vi) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = R0 + ks + 4 * r;
-      if (row < n) {
-        kc[(2 + l16) * ldk + row] = static_cast<T>(acc0[r]);
-        kc[(18 + l16) * ldk + row] = static_cast<T>(acc1[r]);
+      for (int r = 0; r < 4; ++r) {
+        const int c = ks + 4 * r;
+        kc[(2 + c) * ldk + i] = static_cast<T>(acc0[r]);
+        kc[(18 + c) * ldk + i] = static_cast<T>(acc1[r]);
         // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
-        if (joseph && l16 < 2) mc[(4 + l16) * ldk + row] = static_cast<T>(acc0[r]);
-        if (l16 == 0) {  // rows of U take the chain's x (first position of the row in U)
-          const int pos = sh.pos64[row - rbase];
-          xout[row] = pos < nu ? xfin[pos] : xin[row] + acc2[r];
-        }
+        if (joseph && c < 2) mc[(4 + c) * ldk + i] = static_cast<T>(acc0[r]);
       }
     }
     if (merged) columns(i, raw, r0t);
