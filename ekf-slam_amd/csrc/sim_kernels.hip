@@ -112,10 +112,13 @@ __device__ __forceinline__ void wheels(const SimArgs& A, unsigned long long seed
 }
 
 // The fake sensor of one message at the true pose (th, px, py) (nusim.cpp:317-346): every
-// landmark of the map `lm` in the true body frame R(θ)ᵀ(p − x) into sh.bx / sh.by, the selected
-// landmarks into sh.sel (nearest first, or id order for ALL). Returns their count k.
+// landmark of the map `lm` in the true body frame R(θ)ᵀ(p − x) into sh.bx / sh.by (kMap), the
+// selected landmarks into sh.sel (nearest first, or id order for ALL). Returns their count k.
+// Without the map (k_sim_sense: no SURVEY message) `marker` recomputes a selected landmark's body
+// frame position by the same expressions (the same bits), and the wave needs 64 B of LDS, not 16 KB.
+template <bool kMap = true, typename Sh>
 __device__ __forceinline__ int sense(const SimArgs& A, const double* lm, int mode, double th,
-                                     double px, double py, SimShared& sh, int lane) {
+                                     double px, double py, Sh& sh, int lane) {
   const int L = A.L;
   const double c = cos(th), s = sin(th);
   const double rng = mode == kSenseSurvey ? kSurveyRange * A.range : A.range;
@@ -130,29 +133,35 @@ __device__ __forceinline__ int sense(const SimArgs& A, const double* lm, int mod
       const double dx = lm[2 * l] - px, dy = lm[2 * l + 1] - py;
       const double bx = c * dx + s * dy, by = -s * dx + c * dy;
       const double d = hypot(bx, by);
-      sh.bx[l] = bx;
-      sh.by[l] = by;
+      if constexpr (kMap) {
+        sh.bx[l] = bx;
+        sh.by[l] = by;
+      }
       dmin = fmin(dmin, d);
       double kk = d <= rng ? d : INFINITY;
       any = any || kk != INFINITY;
-      if (mode == kSenseSurvey && kk != INFINITY && ((sh.sighted[l >> 5] >> (l & 31)) & 1u))
-        kk = kk + 1e6;
+      if constexpr (kMap) {  // (SURVEY: a run with the map)
+        if (mode == kSenseSurvey && kk != INFINITY && ((sh.sighted[l >> 5] >> (l & 31)) & 1u))
+          kk = kk + 1e6;
+      }
       key[j] = kk;
       if (mode == kSenseAll) key[j] = d;  // (the ADD / DELETE test below)
     }
   }
-  __syncthreads();  // sh.bx / sh.by of every lane before the survey fallback reads them
+  if constexpr (kMap) __syncthreads();  // every lane's sh.bx / sh.by before the survey fallback
   int k = 0;
   if (mode == kSenseAll) {
     k = L;  // every landmark, in id order (L ≤ kMaxChunk, checked on the host)
     if (lane < L) sh.sel[lane] = lane;
   } else {
-    if (mode == kSenseSurvey && !__any(any)) {  // never empty: the nearest, out of range
+    if (kMap && mode == kSenseSurvey && !__any(any)) {  // never empty: the nearest, out of range
       for (int o = 32; o > 0; o >>= 1) dmin = fmin(dmin, __shfl_xor(dmin, o, 64));
+      if constexpr (kMap) {
 #pragma unroll
-      for (int j = 0; j < kPerLane; ++j) {
-        const int l = lane + 64 * j;
-        if (l < L) key[j] = hypot(sh.bx[l], sh.by[l]) == dmin ? dmin : INFINITY;
+        for (int j = 0; j < kPerLane; ++j) {
+          const int l = lane + 64 * j;
+          if (l < L) key[j] = hypot(sh.bx[l], sh.by[l]) == dmin ? dmin : INFINITY;
+        }
       }
     }
     // the m smallest keys, ties to the lower index (synth: a stable argsort)
@@ -182,18 +191,31 @@ __device__ __forceinline__ int sense(const SimArgs& A, const double* lm, int mod
 
 // Marker `lane` < k of message `msg`: its landmark, the noisy body-frame position (draws
 // 2·(msg·M + lane) and + 1 of stream 2) and ADD / DELETE (beyond range, mode ALL).
+// (kMap false: the body frame position from the map `lm` at the true pose (th, px, py), as sense)
+template <bool kMap = true, typename Sh>
 __device__ __forceinline__ void marker(const SimArgs& A, unsigned long long seed, long long msg,
-                                       int mode, int k, const SimShared& sh, int lane, int* id,
-                                       int* act, double* rx, double* ry) {
+                                       int mode, int k, const Sh& sh, int lane, int* id,
+                                       int* act, double* rx, double* ry, const double* lm = nullptr,
+                                       double th = 0.0, double px = 0.0, double py = 0.0) {
   *id = -1;
   *act = 0;
   *rx = *ry = 0.0;
   if (lane < k) {
     *id = sh.sel[lane];
+    double bx, by;
+    if constexpr (kMap) {
+      bx = sh.bx[*id];
+      by = sh.by[*id];
+    } else {
+      const double c = cos(th), s = sin(th);
+      const double dx = lm[2 * *id] - px, dy = lm[2 * *id + 1] - py;
+      bx = c * dx + s * dy;
+      by = -s * dx + c * dy;
+    }
     const unsigned long long idx = (static_cast<unsigned long long>(msg) * A.M + lane) * 2;
-    *rx = sh.bx[*id] + A.sigma * normal(seed, kNoiseStream, idx);
-    *ry = sh.by[*id] + A.sigma * normal(seed, kNoiseStream, idx + 1);
-    *act = mode == kSenseAll && !(hypot(sh.bx[*id], sh.by[*id]) <= A.range) ? 2 : 0;  // DELETE
+    *rx = bx + A.sigma * normal(seed, kNoiseStream, idx);
+    *ry = by + A.sigma * normal(seed, kNoiseStream, idx + 1);
+    *act = mode == kSenseAll && !(hypot(bx, by) <= A.range) ? 2 : 0;  // DELETE
   }
 }
 
@@ -355,17 +377,21 @@ __global__ __launch_bounds__(64) void k_sim_pose(SimArgs A, double* truth_all, d
   }
 }
 
+struct SenseShared {
+  int sel[kMaxChunk];
+};
 __global__ __launch_bounds__(64) void k_sim_sense(SimArgs A, const double* truth_all) {
-  __shared__ SimShared sh;
+  __shared__ SenseShared sh;
   const int t = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
   const unsigned long long seed = A.seed + static_cast<unsigned long long>(A.f0 + f);
   const size_t rowo = static_cast<size_t>(t) * A.F + f;
   const double th = truth_all[rowo * 3], px = truth_all[rowo * 3 + 1], py = truth_all[rowo * 3 + 2];
   const int mode = A.sense ? A.sense[t] : kSenseNearest;  // (never SURVEY here)
-  const int k = sense(A, A.lm + static_cast<size_t>(f) * A.L * 2, mode, th, px, py, sh, lane);
+  const double* lm = A.lm + static_cast<size_t>(f) * A.L * 2;
+  const int k = sense<false>(A, lm, mode, th, px, py, sh, lane);
   int id, act;
   double rx, ry;
-  marker(A, seed, A.msg0 + t, mode, k, sh, lane, &id, &act, &rx, &ry);
+  marker<false>(A, seed, A.msg0 + t, mode, k, sh, lane, &id, &act, &rx, &ry, lm, th, px, py);
   record_markers(A, rowo, k, id, act, rx, ry, lane);
 }
 
