@@ -995,6 +995,212 @@ __device__ void chain_builder(const PassArgs<T>& A, int nchunks, int fy, ChainSh
   }
 }
 
+struct FactorShared {
+  int u[kMaxU + 1];
+  double alphaU[kMaxU], row0raw[kMaxU], col0raw[kMaxU], Zx[kMaxU], xU[kMaxU];
+  double Z[kMaxU][kZC + 1];
+  double Y[kZC][kMaxU + 1];
+  double a1, a2, s00;
+  int nu;
+};
+
+// The factor kernel's two halves: a chunk's record into LDS, then one wave's 16 indices of Kcat = R_pred·Z (rows) and
+// Mcat = Y·C_pred (columns) on f64 MFMA, plus the new state.
+// R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j].
+__device__ __forceinline__ void factor_record(const ChunkRec* rec, FactorShared& sh, int tid) {
+  {  // the record into LDS: every load of a thread issued before its first LDS store
+    constexpr int kPer = (kMaxU * kZC + 255) / 256;  // 5
+    double vz[kPer], vy[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = min(tid + 256 * i, kMaxU * kZC - 1);
+      vz[i] = (&rec->Z[0][0])[e];
+      vy[i] = (&rec->Y[0][0])[e];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = tid + 256 * i;
+      if (e < kMaxU * kZC) {
+        const int b = e / kZC, k = e - b * kZC;
+        sh.Z[b][k] = vz[i];
+        const int k2 = e / kMaxU, b2 = e - k2 * kMaxU;
+        sh.Y[k2][b2] = vy[i];
+      }
+    }
+  }
+  if (tid < kMaxU) {
+    sh.u[tid] = rec->u[tid];
+    sh.alphaU[tid] = rec->alphaU[tid];
+    sh.row0raw[tid] = rec->row0raw[tid];
+    sh.col0raw[tid] = rec->col0raw[tid];
+    sh.Zx[tid] = rec->Zx[tid];
+    sh.xU[tid] = rec->xU[tid];
+  }
+  if (tid == 0) {
+    sh.a1 = rec->a1;
+    sh.a2 = rec->a2;
+    sh.s00 = rec->s00;
+    sh.nu = rec->nu;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc& d, int f, int wg,
+                                            const FactorShared& sh, int lane) {
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const T* S = A.sig[d.parity] + f * A.sig_stride;
+  const double* xin = A.x[d.parity] + f * A.x_stride;
+  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
+  T* kc = A.kcat + f * A.km_stride;
+  T* mc = A.mcat + f * A.km_stride;
+  const bool first = (d.flags & kFirst) != 0;
+  const bool joseph = (d.flags & kJoseph) != 0;
+  const int nu = sh.nu;
+  const double* xfin = sh.xU;
+  // ---- phase B: Kcat = R_pred·Z, Mcat = Y·C_pred on f64 MFMA, 16 rows (or columns) per wave ----
+  // R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j] (predict folded in as above).
+  const int row_tiles = (n + 15) / 16;
+  const int ks = lane >> 4, l16 = lane & 15;
+  const double s00 = sh.s00;
+  // Mcat columns j = C0 + l16 of a wave from Σ_in[U, j] (raw) and Σ_in[0, j] (c0t)
+  auto columns = [&](int j, const T (&raw)[9], T c0t) {
+    const bool vj = j < n;
+    const double c0raw = vj ? static_cast<double>(c0t) : 0.0;
+    const double aj = first ? alpha_of(j, sh.a1, sh.a2) : 0.0;
+    double bv[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      double v = (vj && k < nu) ? static_cast<double>(raw[s]) : 0.0;
+      if (first && vj && k < nu) {
+        v = v + sh.alphaU[k] * c0raw;
+        v = v + (sh.col0raw[k] + sh.alphaU[k] * s00) * aj;
+        if (sh.u[k] == j && j < 3) v += A.q;
+      }
+      bv[s] = v;
+    }
+    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      const double y0 = k < kMaxU ? sh.Y[l16][k] : 0.0;
+      const double y1 = k < kMaxU ? sh.Y[16 + l16][k] : 0.0;
+      acc0 = mfma_f64(y0, bv[s], acc0);
+      acc1 = mfma_f64(y1, bv[s], acc1);
+    }
+    if (vj && ks == 0) {
+      mc[0 * ldk + j] = static_cast<T>(first ? c0raw : 0.0);
+      mc[1 * ldk + j] = static_cast<T>(first ? aj : 0.0);
+    }
+    if (vj) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kr = ks + 4 * r;
+        if (!(joseph && (kr == 2 || kr == 3)))  // (Joseph: the row waves write K there)
+          mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
+        mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
+      }
+    }
+  };
+  // fp64 without the row hand-off: Σ_in is symmetric, so a row wave's Σ_in[U, i] are also its
+  // columns' — one wave per 16 indices builds both Kcat rows and Mcat columns (half the waves
+  // and half the Σ_in reads of separate row and column waves, the same values)
+  const bool merged = sizeof(T) == 8 && A.rows == nullptr;
+  if (wg < row_tiles) {
+    const int R0 = wg * 16;
+    const int i = R0 + l16;
+    const bool vi = i < n;
+    const T* rowp = S + static_cast<size_t>(vi ? i : 0) * ld;
+    // every gather issued unconditionally (clamped index; padding u = 0 stays in bounds), then
+    // masked: a predicated load would be a branch with its own wait, one round trip per load
+    T raw[9];
+    T r0t;
+    if (d.flags & kRowsIn) {  // Σ_in[i, U] written contiguously by the previous chunk's Σ pass
+      const T* rr = A.rows + f * A.rows_stride + (vi ? i : 0);  // [kRowW][ldk]: 16 rows = 128 B
+      r0t = rr[0];  // u_0 = 0
+#pragma unroll
+      for (int s = 0; s < 9; ++s) raw[s] = rr[static_cast<size_t>(4 * s + ks) * A.ldk];
+    } else if (sizeof(T) == 8) {
+      // fp64 Σ is symmetric (the symmetric Σ pass mirrors every element below the diagonal), so
+      // Σ_in[i, U] is read as Σ_in[U, i]: 16 consecutive i per row of U (128 B) instead of one
+      // scattered element per lane and column of U
+      r0t = S[vi ? i : 0];
+#pragma unroll
+      for (int s = 0; s < 9; ++s)
+        raw[s] = S[static_cast<size_t>(sh.u[min(4 * s + ks, kMaxU - 1)]) * ld + (vi ? i : 0)];
+    } else {
+      r0t = rowp[0];
+#pragma unroll
+      for (int s = 0; s < 9; ++s) raw[s] = rowp[sh.u[min(4 * s + ks, kMaxU - 1)]];
+    }
+    const double r0raw = vi ? static_cast<double>(r0t) : 0.0;
+    const double ai = first ? alpha_of(i, sh.a1, sh.a2) : 0.0;
+    double av[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      double v = (vi && k < nu) ? static_cast<double>(raw[s]) : 0.0;
+      if (first && vi && k < nu) {
+        v = v + ai * sh.row0raw[k];
+        v = v + (r0raw + ai * s00) * sh.alphaU[k];
+        if (i == sh.u[k] && i < 3) v += A.q;
+      }
+      av[s] = v;
+    }
+    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const int k = 4 * s + ks;
+      const double z0 = k < kMaxU ? sh.Z[k][l16] : 0.0;
+      const double z1 = k < kMaxU ? sh.Z[k][16 + l16] : 0.0;
+      const double zx = (k < kMaxU && l16 == 0) ? sh.Zx[k] : 0.0;
+      // Zᵀ·R rather than R·Z: the lane then holds Kcat[c = ks + 4r][i = R0 + l16], so each store
+      // covers 4 factor rows × 128 B instead of 16 rows × 32 B (the same products and sums)
+      acc0 = mfma_f64(z0, av[s], acc0);
+      acc1 = mfma_f64(z1, av[s], acc1);
+      acc2 = mfma_f64(zx, av[s], acc2);
+    }
+    if (vi && ks == 0) {  // the predict's two rank-1 factors (slam.cpp:198)
+      kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
+      kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
+      // rows of U take the chain's x (first position of the row in U)
+      int pos = kMaxU;
+#pragma unroll
+      for (int k = kMaxU - 1; k >= 0; --k) pos = (k < nu && sh.u[k] == i) ? k : pos;
+      xout[i] = pos < nu ? xfin[pos] : xin[i] + acc2[0];
+    }
+    if (vi) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = ks + 4 * r;
+        kc[(2 + c) * ldk + i] = static_cast<T>(acc0[r]);
+        kc[(18 + c) * ldk + i] = static_cast<T>(acc1[r]);
+        // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
+        if (joseph && c < 2) mc[(4 + c) * ldk + i] = static_cast<T>(acc0[r]);
+      }
+    }
+    if (merged) columns(i, raw, r0t);
+  } else if (!merged && wg < 2 * row_tiles) {
+    const int C0 = (wg - row_tiles) * 16;
+    const int j = C0 + l16;
+    const bool vj = j < n;
+    const int jj = vj ? j : 0;
+    T raw[9];
+    const T c0t = S[jj];
+#pragma unroll
+    for (int s = 0; s < 9; ++s)
+      raw[s] = S[static_cast<size_t>(sh.u[min(4 * s + ks, kMaxU - 1)]) * ld + jj];
+    columns(j, raw, c0t);
+  }
+}
+
+// 16 rows or 16 columns per wave (fp64 without the row hand-off: both), per_filter workgroups of
+// 4 waves per filter
+template <typename T>
+__host__ __device__ inline int factor_waves(const PassArgs<T>& a) {
+  return (sizeof(T) == 8 && !a.rows ? 1 : 2) * ((a.n + 15) / 16);
+}
+
 // One workgroup per filter, persistent over the `nchunks` chunks of a launch (descriptors
 // A.desc[i·desc_stride + filter]): per chunk the m sequential corrections on the |U|×|U| block.
 // Every chunk of a launch after the first rebuilds its block from the chunk before (kLook): the
@@ -1790,18 +1996,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
 }
 
-struct FactorShared {
-  int u[kMaxU + 1];
-  double alphaU[kMaxU], row0raw[kMaxU], col0raw[kMaxU], Zx[kMaxU], xU[kMaxU];
-  double Z[kMaxU][kZC + 1];
-  double Y[kZC][kMaxU + 1];
-  double a1, a2, s00;
-  int nu;
-  int pos64[64];  // row waves: position in U of each of the workgroup's 64 rows (≥ nu: none)
-};
-
-// Kcat = R_pred·Z (rows) and Mcat = Y·C_pred (columns) on f64 MFMA, plus the new state.
-// 16 rows or 16 columns per wave; R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j].
 template <typename T>
 __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int nf) {
   __shared__ FactorShared sh;
@@ -1822,198 +2016,16 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
   if (!(d.flags & kActive)) return;
   const int f = A.f0 + fb;
   const int tid = threadIdx.x;
-  const int n = A.n, ld = A.ld, ldk = A.ldk;
-  const T* S = A.sig[d.parity] + f * A.sig_stride;
-  const double* xin = A.x[d.parity] + f * A.x_stride;
-  double* xout = A.x[d.parity ^ 1] + f * A.x_stride;
-  T* kc = A.kcat + f * A.km_stride;
-  T* mc = A.mcat + f * A.km_stride;
   const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
-  const bool first = (d.flags & kFirst) != 0;
-  const bool joseph = (d.flags & kJoseph) != 0;
   // the chain of this chunk runs on the other stream: wait for its record
-  if (tid < 64) sh.pos64[tid] = kMaxU;
   if (A.polls && tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
     flag_timeout(&A.ctl[f].status, A.fatal);
   drain_stores();
   __syncthreads();
-  {  // the record into LDS: every load of a thread issued before its first LDS store
-    constexpr int kPer = (kMaxU * kZC + 255) / 256;  // 5
-    double vz[kPer], vy[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = min(tid + 256 * i, kMaxU * kZC - 1);
-      vz[i] = (&rec->Z[0][0])[e];
-      vy[i] = (&rec->Y[0][0])[e];
-    }
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = tid + 256 * i;
-      if (e < kMaxU * kZC) {
-        const int b = e / kZC, k = e - b * kZC;
-        sh.Z[b][k] = vz[i];
-        const int k2 = e / kMaxU, b2 = e - k2 * kMaxU;
-        sh.Y[k2][b2] = vy[i];
-      }
-    }
-  }
-  if (tid < kMaxU) {
-    const int ub = rec->u[tid], rnu = rec->nu, rbase = bx * 64;
-    sh.u[tid] = ub;
-    if (tid < rnu && ub >= rbase && ub < rbase + 64) atomicMin(&sh.pos64[ub - rbase], tid);
-    sh.alphaU[tid] = rec->alphaU[tid];
-    sh.row0raw[tid] = rec->row0raw[tid];
-    sh.col0raw[tid] = rec->col0raw[tid];
-    sh.Zx[tid] = rec->Zx[tid];
-    sh.xU[tid] = rec->xU[tid];
-  }
-  if (tid == 0) {
-    sh.a1 = rec->a1;
-    sh.a2 = rec->a2;
-    sh.s00 = rec->s00;
-    sh.nu = rec->nu;
-  }
+  factor_record(rec, sh, tid);
   __syncthreads();
-  const int nu = sh.nu;
-  const double* xfin = sh.xU;
-  // ---- phase B: Kcat = R_pred·Z, Mcat = Y·C_pred on f64 MFMA, 16 rows (or columns) per wave ----
-  // R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j] (predict folded in as above).
-  const int lane = tid & 63;
-  const int wg = bx * (blockDim.x >> 6) + (tid >> 6);  // the filter's wave index
-  const int row_tiles = (n + 15) / 16;
-  const int ks = lane >> 4, l16 = lane & 15;
-  const double s00 = sh.s00;
-  // Mcat columns j = C0 + l16 of a wave from Σ_in[U, j] (raw) and Σ_in[0, j] (c0t)
-  auto columns = [&](int j, const T (&raw)[9], T c0t) {
-    const bool vj = j < n;
-    const double c0raw = vj ? static_cast<double>(c0t) : 0.0;
-    const double aj = first ? alpha_of(j, sh.a1, sh.a2) : 0.0;
-    double bv[9];
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      const int k = 4 * s + ks;
-      double v = (vj && k < nu) ? static_cast<double>(raw[s]) : 0.0;
-      if (first && vj && k < nu) {
-        v = v + sh.alphaU[k] * c0raw;
-        v = v + (sh.col0raw[k] + sh.alphaU[k] * s00) * aj;
-        if (sh.u[k] == j && j < 3) v += A.q;
-      }
-      bv[s] = v;
-    }
-    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      const int k = 4 * s + ks;
-      const double y0 = k < kMaxU ? sh.Y[l16][k] : 0.0;
-      const double y1 = k < kMaxU ? sh.Y[16 + l16][k] : 0.0;
-      acc0 = mfma_f64(y0, bv[s], acc0);
-      acc1 = mfma_f64(y1, bv[s], acc1);
-    }
-    if (vj && ks == 0) {
-      mc[0 * ldk + j] = static_cast<T>(first ? c0raw : 0.0);
-      mc[1 * ldk + j] = static_cast<T>(first ? aj : 0.0);
-    }
-    if (vj) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kr = ks + 4 * r;
-        if (!(joseph && (kr == 2 || kr == 3)))  // (Joseph: the row waves write K there)
-          mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
-        mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
-      }
-    }
-  };
-  // fp64 without the row hand-off: Σ_in is symmetric, so a row wave's Σ_in[U, i] are also its
-  // columns' — one wave per 16 indices builds both Kcat rows and Mcat columns (half the waves
-  // and half the Σ_in reads of separate row and column waves, the same values)
-  const bool merged = sizeof(T) == 8 && A.rows == nullptr;
-  if (wg < row_tiles) {
-    const int R0 = wg * 16;
-    const int i = R0 + l16;
-    const bool vi = i < n;
-    const T* rowp = S + static_cast<size_t>(vi ? i : 0) * ld;
-    // every gather issued unconditionally (clamped index; padding u = 0 stays in bounds), then
-    // masked: a predicated load would be a branch with its own wait, one round trip per load
-    T raw[9];
-    T r0t;
-    if (d.flags & kRowsIn) {  // Σ_in[i, U] written contiguously by the previous chunk's Σ pass
-      const T* rr = A.rows + f * A.rows_stride + (vi ? i : 0);  // [kRowW][ldk]: 16 rows = 128 B
-      r0t = rr[0];  // u_0 = 0
-#pragma unroll
-      for (int s = 0; s < 9; ++s) raw[s] = rr[static_cast<size_t>(4 * s + ks) * A.ldk];
-    } else if (sizeof(T) == 8) {
-      // fp64 Σ is symmetric (the symmetric Σ pass mirrors every element below the diagonal), so
-      // Σ_in[i, U] is read as Σ_in[U, i]: 16 consecutive i per row of U (128 B) instead of one
-      // scattered element per lane and column of U
-      r0t = S[vi ? i : 0];
-#pragma unroll
-      for (int s = 0; s < 9; ++s)
-        raw[s] = S[static_cast<size_t>(sh.u[min(4 * s + ks, kMaxU - 1)]) * ld + (vi ? i : 0)];
-    } else {
-      r0t = rowp[0];
-#pragma unroll
-      for (int s = 0; s < 9; ++s) raw[s] = rowp[sh.u[min(4 * s + ks, kMaxU - 1)]];
-    }
-    const double r0raw = vi ? static_cast<double>(r0t) : 0.0;
-    const double ai = first ? alpha_of(i, sh.a1, sh.a2) : 0.0;
-    double av[9];
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      const int k = 4 * s + ks;
-      double v = (vi && k < nu) ? static_cast<double>(raw[s]) : 0.0;
-      if (first && vi && k < nu) {
-        v = v + ai * sh.row0raw[k];
-        v = v + (r0raw + ai * s00) * sh.alphaU[k];
-        if (i == sh.u[k] && i < 3) v += A.q;
-      }
-      av[s] = v;
-    }
-    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      const int k = 4 * s + ks;
-      const double z0 = k < kMaxU ? sh.Z[k][l16] : 0.0;
-      const double z1 = k < kMaxU ? sh.Z[k][16 + l16] : 0.0;
-      const double zx = (k < kMaxU && l16 == 0) ? sh.Zx[k] : 0.0;
-      // Zᵀ·R rather than R·Z: the lane then holds Kcat[c = ks + 4r][i = R0 + l16], so each store
-      // covers 4 factor rows × 128 B instead of 16 rows × 32 B (the same products and sums)
-      acc0 = mfma_f64(z0, av[s], acc0);
-      acc1 = mfma_f64(z1, av[s], acc1);
-      acc2 = mfma_f64(zx, av[s], acc2);
-    }
-    const int rbase = bx * 64;
-    if (vi && ks == 0) {  // the predict's two rank-1 factors (slam.cpp:198)
-      kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
-      kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
-      // rows of U take the chain's x (first position of the row in U)
-      const int pos = sh.pos64[i - rbase];
-      xout[i] = pos < nu ? xfin[pos] : xin[i] + acc2[0];
-    }
-    if (vi) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = ks + 4 * r;
-        kc[(2 + c) * ldk + i] = static_cast<T>(acc0[r]);
-        kc[(18 + c) * ldk + i] = static_cast<T>(acc1[r]);
-        // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
-        if (joseph && c < 2) mc[(4 + c) * ldk + i] = static_cast<T>(acc0[r]);
-      }
-    }
-    if (merged) columns(i, raw, r0t);
-  } else if (!merged && wg < 2 * row_tiles) {
-    const int C0 = (wg - row_tiles) * 16;
-    const int j = C0 + l16;
-    const bool vj = j < n;
-    const int jj = vj ? j : 0;
-    T raw[9];
-    const T c0t = S[jj];
-#pragma unroll
-    for (int s = 0; s < 9; ++s)
-      raw[s] = S[static_cast<size_t>(sh.u[min(4 * s + ks, kMaxU - 1)]) * ld + jj];
-    columns(j, raw, c0t);
-  }
+  factor_wave<T>(A, d, f, bx * (blockDim.x >> 6) + (tid >> 6), sh, tid & 63);
 }
-
 
 // ---- Σ pass on MFMA -------------------------------------------------------------------------
 // Σ_out = Σ_in + Q̄ − Σ_k Kcat[k]ᵀ ⊗ Mcat[k], one tile per wave, four waves per workgroup.
@@ -2709,9 +2721,7 @@ hipError_t launch_chain(const PassArgs<T>& a, int nf, int nchunks, hipStream_t s
 template <typename T>
 hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1) {
-  // 16 rows or 16 columns per wave; fp64 without the row hand-off: both (k_factors `merged`)
-  const int waves = (sizeof(T) == 8 && !a.rows ? 1 : 2) * ((a.n + 15) / 16);
-  const int per_filter = (waves + 3) / 4;
+  const int per_filter = (factor_waves(a) + 3) / 4;
   if (nf >= 16) {  // XCD-aware 1-D grid, as the swarm's Σ pass
     launch(k_factors<T>, dim3(8 * ((nf + 7) / 8) * per_filter), dim3(256), s, e0, e1, a,
            per_filter, nf);

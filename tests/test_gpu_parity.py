@@ -299,6 +299,9 @@ def test_many_filters_match_small_batch(F, devsync, monkeypatch):
         assert cs == cb
         np.testing.assert_array_equal(xs, xb)
         np.testing.assert_array_equal(Ss, Sb)
+        # the symmetric fp64 Σ pass (wide tiles here, narrow in the 8-filter handle) leaves Σ
+        # exactly symmetric
+        np.testing.assert_array_equal(Sb, Sb.T)
 
 
 @pytest.mark.parametrize("F,env", [(1, {"EKF_DEVSYNC": "0"}), (4, {"EKF_DEVSYNC": "0"}), (40, {}),
