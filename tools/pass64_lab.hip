@@ -1,6 +1,7 @@
 // Dev tool (not shipped): the swarm's fp64 Σ pass (512 filters, N = 256: n = 515, 2.2 GB of Σ per
 // message) A/B'd standalone against the product's k_sigma_pass<double, true> on the same buffers,
-// outputs (Σ_out and the kRowsOut rows) compared bit for bit.
+// outputs (Σ_out and the kRowsOut rows) compared bit for bit. Since round 4 the product is the
+// symmetric pass (k_sym here is its prototype; the ablations are of the full pass's tile).
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../include -I../ekf-slam_amd/csrc pass64_lab.hip -o pass64_lab
 #include "../ekf-slam_amd/csrc/ekf_kernels.hip"
 
@@ -531,9 +532,11 @@ int main(int argc, char** argv) {
   const double bytes = 2.0 * n * n * 8 * F;
   std::vector<double> ref(stride * F), out(stride * F), rref(a.rows_stride * F), rout(a.rows_stride * F);
   const int trows = (n + 31) / 32, tcols = (n + 63) / 64, per_filter = (trows * tcols + 3) / 4;
+  // the product's pass is symmetric since round 4: its grid covers the upper tiles only
+  const int prod_pf = (sym_tiles<64>(trows, tcols) + 3) / 4;
   auto prod = [&](hipStream_t st) {
-    hipLaunchKernelGGL((k_sigma_pass<double, true>), dim3(8 * ((F + 7) / 8) * per_filter), dim3(256), 0, st,
-                       a, tcols, per_filter, F);
+    hipLaunchKernelGGL((k_sigma_pass<double, true>), dim3(8 * ((F + 7) / 8) * prod_pf), dim3(256), 0, st,
+                       a, tcols, prod_pf, F);
   };
   auto time_it = [&](const char* name, auto&& fn, bool check_rows) {
     CK(hipMemset(S1, 0, stride * F * 8));
