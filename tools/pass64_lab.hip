@@ -334,7 +334,7 @@ __device__ __forceinline__ void sym_tile(int t, int trows, int tcols, int& tr, i
   ok = tr < trows;
   tc = tr / 2 + (t - base);
 }
-constexpr int kTS = 34;  // transposed tile row stride (doubles): 16 B aligned rows
+// (transposed tile row stride: ekfslam::kTS)
 template <int MIR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_sym(PassArgs<double> A, int tcols, int xcd_b, int nf) {
   const int L = blockIdx.x, j = L >> 3;
