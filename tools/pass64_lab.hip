@@ -480,6 +480,120 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
+// ---- symmetric pass, two vertically adjacent tiles per wave (the M operand loaded once) -------
+// Column-major over the upper tiles: column tc holds tile rows 0 … min(trows, 2·tc + 2) − 1, in
+// pairs (2j, 2j + 1); the wave loads the column's M operand once and runs the two tiles in turn.
+__device__ __forceinline__ bool pair_slot(int t, int trows, int tcols, int& tc, int& r0, int& cnt) {
+  int base = 0;
+  for (tc = 0; tc < tcols; ++tc) {
+    cnt = min(trows, 2 * tc + 2);
+    const int p = (cnt + 1) / 2;
+    if (t < base + p) break;
+    base += p;
+  }
+  r0 = 2 * (t - base);
+  return tc < tcols;
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_sym_pair(PassArgs<double> A, int tcols, int xcd_b, int nf) {
+  const int L = blockIdx.x, j = L >> 3;
+  const int fb = (L & 7) + 8 * (j / xcd_b), bx = j % xcd_b;
+  if (fb >= nf) return;
+  const MsgDesc& d = A.desc[fb];
+  __shared__ double tTs[4][64 * kTS];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int trows = (A.n + 31) / 32;
+  const int t = __builtin_amdgcn_readfirstlane(bx * 4 + wv);
+  int tc, r0, cnt;
+  if (!pair_slot(t, trows, tcols, tc, r0, cnt) || !(d.flags & kActive)) return;
+  const int C0 = tc * 64;
+  const int f = A.f0 + fb;
+  const int n = A.n, ld = A.ld, ldk = A.ldk;
+  const double* Sin = A.sig[d.parity] + f * A.sig_stride;
+  double* Sout = A.sig[d.parity ^ 1] + f * A.sig_stride;
+  constexpr int TJ = 4;
+  const int kr = lane >> 4, kcol = lane & 15;
+  const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 8u;
+  const auto rk = buf_rsrc(A.kcat + f * A.km_stride, kbytes), rm = buf_rsrc(A.mcat + f * A.km_stride, kbytes);
+  const auto rmir = buf_rsrc(Sout + static_cast<size_t>(C0) * ld, static_cast<unsigned>(min(n - C0, 64)) * ld * 8u);
+  double b[TJ][9];
+  unsigned so[TJ];
+  const unsigned kstep = 4u * ldk * 8u;
+#pragma unroll
+  for (int tj = 0; tj < TJ; ++tj) {
+    const int col = C0 + 16 * tj + kcol;
+    const unsigned mo = static_cast<unsigned>(kr * ldk + min(col, n - 1)) * 8u;
+    so[tj] = col < n ? static_cast<unsigned>(kr * ld + col) * 8u : kOOB;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) b[tj][s] = ld_f64(rm, mo, s * kstep);
+  }
+  const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
+  const bool first = (d.flags & kFirst) != 0;
+  const double q = A.q;
+  const unsigned rstride = static_cast<unsigned>(ld) * 8u;
+  double* tT = tTs[wv];
+  for (int h = 0; h < 2; ++h) {
+    const int tr = r0 + h;
+    if (tr >= cnt) break;
+    const int R0 = tr * 32;
+    const auto rin = buf_rsrc(Sin + static_cast<size_t>(R0) * ld, static_cast<unsigned>(min(n - R0, 32)) * ld * 8u);
+    const auto rout = buf_rsrc(Sout + static_cast<size_t>(R0) * ld, static_cast<unsigned>(min(n - R0, 32)) * ld * 8u);
+    double a[2][9], sv[2][TJ][4];
+    const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 8u;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      a[0][s] = ld_f64(rk, ko, s * kstep);
+      a[1][s] = ld_f64(rk, ko + 16 * 8, s * kstep);
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sv[ti][tj][r] = __builtin_bit_cast(
+              double, __builtin_amdgcn_raw_buffer_load_b64(rin, so[tj] + (16 * ti + 4 * r) * rstride, 0, 2));
+    d4 acc[2][TJ];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = d4{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      const bool live = 4 * s < kw;
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < TJ; ++tj)
+          acc[ti][tj] = mfma_f64(live ? a[ti][s] : 0.0, live ? b[tj][s] : 0.0, acc[ti][tj]);
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = 16 * ti + kr + 4 * r, cl = 16 * tj + kcol;
+          const int row = R0 + rl, col = C0 + cl;
+          double v = sv[ti][tj][r] - acc[ti][tj][r];
+          if (first && row == col && row < 3) v += q;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rout,
+                                                col >= row ? so[tj] + (16 * ti + 4 * r) * rstride : kOOB, 0, 2);
+          tT[cl * kTS + rl] = v;
+        }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int rl = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int cl = 2 * i + (lane >> 5);
+      const double v = tT[cl * kTS + rl];
+      const int row = R0 + rl, col = C0 + cl;
+      const unsigned mo2 = col > row && col < n ? static_cast<unsigned>(cl * ld + R0 + rl) * 8u : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), rmir, mo2, 0, 2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
 template <typename V>
 __global__ void k_copy(const V* __restrict__ in, V* __restrict__ out, size_t nv) {
   for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) out[i] = in[i];
@@ -631,7 +745,15 @@ int main(int argc, char** argv) {
     printf("  symmetric check vs product's upper triangle: mismatches %zu rows %zu (%d of %d tiles)\n", bad, rbad,
            sym_tiles, trows * tcols);
   };
+  int pairs = 0;
+  for (int tc = 0; tc < tcols; ++tc) pairs += (std::min(trows, 2 * tc + 2) + 1) / 2;
+  const int pair_pf = (pairs + 3) / 4;
+  auto sym_pair = [&](hipStream_t st) {
+    hipLaunchKernelGGL(k_sym_pair, dim3(8 * ((F + 7) / 8) * pair_pf), dim3(256), 0, st, a, tcols, pair_pf, F);
+  };
   for (int round = 0; round < 2; ++round) {
+    time_it("symmetric, 2 tiles per wave", sym_pair, false);
+    sym_check();
     time_it("symmetric k_sym (LDS transpose)", sym, false);
     sym_check();
     time_it("product k_sigma_pass", prod, true);
