@@ -261,6 +261,13 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
   // a builder workgroup per filter beside each chain (k_chain): multi-chunk device-epoch launches
   a.build = a.polls && h->build && nchunks > 1 ? 1 : 0;
   a.nf_launch = nf;
+  {  // dev A/B: stream-ordered chains gather their (complete) Σ_in instead of rebuilding
+    static const bool g = [] {
+      const char* e = std::getenv("EKF_SERIAL_GATHER");
+      return e && std::atoi(e) != 0;
+    }();
+    a.gather = g && ms == bs && !a.polls ? 1 : 0;
+  }
   if (pipelined && !nolook) {
     // events: a rebuilding (kLook) chain needs the Σ pass two launches back
     if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s0 & 1], 0));

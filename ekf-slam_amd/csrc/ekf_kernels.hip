@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   const MsgDesc& d = sdesc[ci & 1];
   auto& P = sh.P[ci & 1];
   const bool active = (d.flags & kActive) != 0;
-  const bool look = (d.flags & kLook) != 0;
+  const bool look = (d.flags & kLook) != 0 && !A.gather;
   // Publish the previous chunk's record before this chunk waits on anything the bulk stream
   // produces (its factor kernel needs that record).
   if (pending) {

@@ -44,6 +44,8 @@ struct PassArgs {
                         // f mod 8, builder 8 later, both on XCD f mod 8); 0 (default): every
                         // chunk's prologue rebuilds its own
   int nf_launch;        // filters of the launch (build: the 1-D grid's bound)
+  int gather;           // chain (dev A/B, EKF_SERIAL_GATHER=1): in stream order every chunk
+                        // gathers its complete Σ_in instead of a kLook rebuild
   BuildRec* bout;       // [2][rec_stride] the builder's blocks
   BuildChan* chan;      // [rec_stride] the chain's predict parameters for the builder
   const MsgDesc* desc;
