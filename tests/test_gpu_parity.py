@@ -386,3 +386,51 @@ def test_empty_and_all_delete_messages(monkeypatch, resident):
         assert np.abs(x - xr).max() < POSE_TOL, f
         assert np.abs(S - Sr).max() < SIGMA_TOL, f
     e.close()
+
+
+@pytest.mark.gpu
+def test_serial_gather_matches_small_batch(monkeypatch):
+    """EKF_SERIAL_GATHER=1 (opt-in): the chains of a stream-ordered handle (> 32
+    filters: one stream) gather their complete Σ_in instead of rebuilding it from the chunk before
+    (kLook). Filter f replays scenario f % 8 and equals the same scenario in an 8-filter handle
+    (events, kLook) to rounding — the gather and the rebuild round differently — and Σ stays
+    exactly symmetric."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_SERIAL_GATHER"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("EKF_DEVSYNC", "0")
+    N, T = 64, 12
+    scs = [synth.synthetic(N, T, seed=100 + k) for k in range(8)]
+    odo = [pyekf.odometry(s) for s in scs]
+    M = max(s.ids.shape[1] for s in scs)
+
+    def run(nf):
+        cnt = np.zeros((T, nf), np.int32)
+        ids = np.full((T, nf, M), -1, np.int32)
+        act = np.zeros((T, nf, M), np.int32)
+        rel = np.zeros((T, nf, M, 2))
+        od = np.zeros((T, nf, 3))
+        for f in range(nf):
+            s = scs[f % 8]
+            k = s.ids.shape[1]
+            cnt[:, f] = s.count
+            ids[:, f, :k] = s.ids
+            act[:, f, :k] = s.actions
+            rel[:, f, :k] = s.rel
+            od[:, f] = odo[f % 8]
+        e = pyekf.EKF(n_landmarks=N, n_filters=nf)
+        e.replay(cnt, rel, od, ids=ids, actions=act)
+        out = [e.state(f) for f in range(nf)]
+        assert [e.status(f) for f in range(nf)] == [0] * nf
+        e.close()
+        return out
+
+    small = run(8)
+    monkeypatch.setenv("EKF_SERIAL_GATHER", "1")
+    big = run(40)
+    for f in range(40):
+        xs, Ss, cs = small[f % 8]
+        xb, Sb, cb = big[f]
+        assert cs == cb
+        np.testing.assert_allclose(xb, xs, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(Sb, Ss, rtol=1e-12, atol=1e-9)
+        np.testing.assert_array_equal(Sb, Sb.T)
