@@ -2110,9 +2110,13 @@ struct SigmaTile<float> {
     finish(g, Sout, n, ld, kw, first, qd, R0, C0, lane);
   }
   // the MFMAs on the tile's operands, Σ_in − K·M (+ Q̄), the stores
+  // pm (≠ null: the chunk's record holds the chain's fp64 Σ[U, U], kPendValid): the first position
+  // in U of each tile row (pm[0..32)) and column (pm[32..64)), > kMaxU − 1 for none — those
+  // entries take the record's value instead (what k_patch_stage wrote after the pass before)
   static __device__ __forceinline__ void finish(const F32TileRegs& g, float* Sout, int n, int ld,
                                                 int kw, bool first, double qd, int R0, int C0,
-                                                int lane) {
+                                                int lane, const int* pm = nullptr,
+                                                const ChunkRec* rec = nullptr) {
     const int kr = lane >> 5, col = C0 + (lane & 31);
     const auto rout = panel(Sout, n, ld, R0);
     const unsigned so = soff(n, ld, C0, lane);
@@ -2133,11 +2137,16 @@ struct SigmaTile<float> {
     }
     SIG_STAMP(2);
     const float q = static_cast<float>(qd);
+    const int pc = pm ? pm[32 + (lane & 31)] : kMaxU;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * kr, row = R0 + rl;
       float v = sv[r] - acc[r];
       if (first && row == col && row < 3) v += q;
+      if (pm) {
+        const int pr = pm[rl];
+        if (pr < kMaxU && pc < kMaxU) v = static_cast<float>(rec->Pend[pr][pc]);
+      }
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout,
                                             so + ((r & 3) + 8 * (r >> 2)) * rstride, 0, 0);
     }
@@ -2391,6 +2400,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
     // behind them (≈ 0.3 µs of a 9 µs pass, tools/pass_lab.hip)
     if (!ok) return;
     const int f = A.f0 + fb;
+    // the patch test's record flags of both parities, issued with the operands (not a scalar round
+    // trip behind the descriptor's parity: that wait cost ≈ 0.4 µs of the pass)
+    const int rf0 = A.rec[f].flags, rf1 = A.rec[A.rec_stride + f].flags;
     F32TileRegs g;
     Tile::load_ops(g, A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ldk,
                    tr * Tile::kRows, tc * Tile::kCols, lane);
@@ -2400,8 +2412,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
       const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
       Tile::load_sig(g, A.sig[d.parity] + f * A.sig_stride, A.n, A.ld, tr * Tile::kRows,
                      tc * Tile::kCols, lane);
+      // the fp32 patch (see k_patch_stage): the chain's fp64 Σ[U, U] over this tile's entries
+      // there, for the chunks that initialised a landmark (the pass's 1e7 − (1e7 − δ) loses δ)
+      const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
+      const int* pm = nullptr;
+      if ((d.parity ? rf1 : rf0) & kPendValid) {  // wave-uniform
+        const int R0 = tr * Tile::kRows, C0 = tc * Tile::kCols;
+        int* map = cmap[threadIdx.x >> 6];
+        map[lane] = kMaxU;
+        const int nu = rec->nu, u = rec->u[min(lane, kMaxU - 1)];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane < nu && u >= R0 && u < R0 + 32) atomicMin(&map[u - R0], lane);
+        if (lane < nu && u >= C0 && u < C0 + 32) atomicMin(&map[32 + u - C0], lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        pm = map;
+      }
       Tile::finish(g, A.sig[d.parity ^ 1] + f * A.sig_stride, A.n, A.ld, kw,
-                   (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane);
+                   (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane, pm,
+                   rec);
     }
   } else if ((d.flags & kActive) && ok) {
     SIG_STAMP(1);
@@ -2431,7 +2459,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
 // CU). Patched entries take the patch's value (the loads would race the scatter's stores).
 template <typename T>
 __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
-  constexpr bool kPatch = sizeof(T) == 4;
+  // (the fp32 patch itself now happens in the Σ pass's tiles, SigmaTile<float>::finish: the
+  // staging below reads the patched Σ_out)
+  constexpr bool kPatch = false;
   const MsgDesc& d = A.desc[blockIdx.x];
   const int flags = d.flags;
   if (!(flags & kActive)) return;
@@ -2761,7 +2791,7 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool st
       launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
     }
   }
-  if (sizeof(T) == 4 || stage) hipLaunchKernelGGL(k_patch_stage<T>, dim3(nf), dim3(256), 0, s, a);
+  if (stage) hipLaunchKernelGGL(k_patch_stage<T>, dim3(nf), dim3(256), 0, s, a);
   // the pass's epoch (otherwise published by the next chunk's factor kernel, PassArgs::pub_sigma)
   if (publish && a.polls) hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();
