@@ -2447,16 +2447,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
 }
 
 
-// fp32 only, right behind the Σ pass on its stream: the chain's fp64 Σ[U, U] (rec->Pend, rounded
-// once) over the pass's values there. The pass's 1e7 − (1e7 − δ) at a first sighting (the
-// reference's prior, slam.cpp:130) loses δ in fp32; the chain computed it in fp64. Other entries
-// carry no such cancellation (the prior has no cross terms). A repeated index takes the entry of
-// its first position in U. One workgroup per filter, ≤ 35 × 35 stores.
-//
-// kStageOut (either dtype): then the rebuild operands of the filter's chunk after next (StageRec),
-// gathered from the Σ_out / x_out just completed — off the chain's critical path, where the same
-// gather at the chain's start cost ≈ 10 µs of a 47 µs message (≈ 1 900 scattered lines through one
-// CU). Patched entries take the patch's value (the loads would race the scatter's stores).
+// Right behind the Σ pass on its stream, for chunks that stage (kStageOut, either dtype): the
+// rebuild operands of the filter's chunk after next (StageRec), gathered from the Σ_out / x_out
+// just completed — off the chain's critical path, where the same gather at the chain's start cost
+// ≈ 10 µs of a 47 µs message (≈ 1 900 scattered lines through one CU). One workgroup per filter.
+// The fp32 patch this kernel also did until round 4 — the chain's fp64 Σ[U, U] (rec->Pend, rounded
+// once) over the pass's values, because the pass's 1e7 − (1e7 − δ) at a first sighting (the
+// reference's prior, slam.cpp:130) loses δ in fp32 — now happens in the pass's tiles
+// (SigmaTile<float>::finish), so Σ_out is already patched here; the patch branches below are off.
 template <typename T>
 __global__ __launch_bounds__(256) void k_patch_stage(PassArgs<T> A) {
   // (the fp32 patch itself now happens in the Σ pass's tiles, SigmaTile<float>::finish: the
