@@ -2137,16 +2137,25 @@ struct SigmaTile<float> {
     }
     SIG_STAMP(2);
     const float q = static_cast<float>(qd);
-    const int pc = pm ? pm[32 + (lane & 31)] : kMaxU;
+    if (!pm) {  // (two loops: the common one keeps the plain store sequence)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = R0 + (r & 3) + 8 * (r >> 2) + 4 * kr;
+        float v = sv[r] - acc[r];
+        if (first && row == col && row < 3) v += q;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout,
+                                              so + ((r & 3) + 8 * (r >> 2)) * rstride, 0, 0);
+      }
+      return;
+    }
+    const int pc = pm[32 + (lane & 31)];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rl = (r & 3) + 8 * (r >> 2) + 4 * kr, row = R0 + rl;
       float v = sv[r] - acc[r];
       if (first && row == col && row < 3) v += q;
-      if (pm) {
-        const int pr = pm[rl];
-        if (pr < kMaxU && pc < kMaxU) v = static_cast<float>(rec->Pend[pr][pc]);
-      }
+      const int pr = pm[rl];
+      if (pr < kMaxU && pc < kMaxU) v = static_cast<float>(rec->Pend[pr][pc]);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rout,
                                             so + ((r & 3) + 8 * (r >> 2)) * rstride, 0, 0);
     }
