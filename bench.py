@@ -349,6 +349,18 @@ class HipBackend:
     def sync(self):
         self.torch.cuda.synchronize()
 
+    def device_info(self):
+        """This rank's GPU as the runtime sees it (the line's rank map: which GPU each rank ran)."""
+        torch = self.torch
+        d = torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(d)
+        info = {"device": d, "name": p.name}
+        for k in ("pci_bus_id", "pci_device_id", "uuid"):
+            v = getattr(p, k, None)
+            if v is not None:
+                info[k] = str(v)
+        return info
+
 
 def build_inputs(N, F, T, seed, m, rank, n_map=None):
     """SURVEY.md §8d inputs for this rank's F filters: global filter g = rank·F + f is seeded
@@ -409,6 +421,18 @@ def run(args, rank, world, local, backend=None):
     local = getattr(be, "local", local)  # (EKF_BENCH_SHARE_GPU: the GPU this rank shares)
     if world > 1:
         dist.init_process_group(be.dist_backend)
+    # which rank ran where, gathered once before any timing (so the line shows that the collective
+    # saw N ranks, each on its own GPU)
+    me = {"rank": rank, "local_rank": local, "pid": os.getpid()}
+    if hasattr(be, "device_info"):
+        me.update(be.device_info())
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        dist_info = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+                     "ranks": ranks}
+    else:
+        dist_info = {"world_size": 1, "backend": None, "ranks": [me]}
     dtype = be.F32 if dt == "f32" else be.F64
     W, K = args.warmup, args.steps
     t_gen = time.perf_counter()
@@ -612,7 +636,8 @@ def run(args, rank, world, local, backend=None):
                        "status_flags_rank0": sorted(set(status)),
                        "host_input_generation_s": t_gen,
                        "inputs": inputs,
-                       "parallelism": f"independent filters x{world} ranks"},
+                       "parallelism": f"independent filters x{world} ranks",
+                       "distributed": dist_info},
             "roofline": {
                 "kernel": "k_sigma_pass", "bound": "hbm", "achieved": achieved,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

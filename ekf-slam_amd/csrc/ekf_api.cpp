@@ -58,22 +58,22 @@ struct ekf_ctx {
   hipStream_t stream = nullptr;  // chain + factors (+ association, posterior)
   hipStream_t bulk = nullptr;    // Σ passes: chunk t's pass overlaps chunk t+1's chain
   bool serial = false;           // EKF_SERIAL=1: every kernel on one stream (per-dispatch PMC)
-  bool build = false;            // EKF_BUILD=1: chain launches of > 1 chunk take a builder
-                                 // workgroup per filter (k_chain, PassArgs::build)
   bool resident = false;         // n ≤ kResidentMaxN, fp64: Σ in registers (ekf_resident.hip)
   bool defer = false;            // ekf_defer: plan now, upload and launch later
   bool joseph = false;           // ekf_set_joseph (resident: its own kernel; pipeline: kJoseph chunks)
   bool assoc_msg = true;         // unknown association by chunks (k_assoc_msg); EKF_ASSOC_MSG=0:
                                  // one association kernel + launch pair per marker
   bool main_dirty = false;       // work on the main stream since the bulk stream last joined it
+  bool main_unordered = false;   // the main stream ran descriptor-reading work (k_posterior) that
+                                 // nothing on the bulk stream is ordered after: a device planner
+                                 // on the bulk stream must wait for it before rewriting ddesc
   bool epoch_owed = false;       // the last Σ pass published no device epoch (the flush's last
                                  // launch: the next flush joins the bulk stream on the host)
   AmArgs am{};                   // k_assoc_msg scratch (allocated at the first association chunk)
   int am_route = 0;              // unknown association: EKF_ASSOC_* (fixed at ekf_create)
+  int am_group = 1;              // filters per k_assoc_msg launch (co-resident, assoc_msg_group)
   int bulk_cus_per_xcd = 0;      // CUs the bulk stream may use on each XCD
   int main_cus_per_xcd = 0;      // CUs the main stream may use on each XCD (0: every CU, no mask)
-  BuildRec* bout = nullptr;      // [2][F] the builders' blocks
-  BuildChan* chan = nullptr;     // [F] the chains' predict parameters for the builders
   unsigned* fatal_h = nullptr;   // host-mapped: a device poll timed out (EKF_E_TIMEOUT)
   unsigned* fatal_d = nullptr;   // its device address (PassArgs::fatal)
   hipEvent_t ev_chain = nullptr;          // main → bulk: the chunk's chain is done
@@ -88,7 +88,6 @@ struct ekf_ctx {
   void* mcat = nullptr;
   FilterCtl* ctl = nullptr;
   ChunkRec* rec = nullptr;
-  void* rows = nullptr;  // fp64: Σ_in[i, U] from a Σ pass to the next chunk's factor kernel
   void* stage = nullptr; // StageRec<T>[2][F]: a kLook chain's rebuild operands (kStageIn)
   MsgDesc* ddesc = nullptr;
   size_t sig_stride = 0, x_stride = 0, km_stride = 0;
@@ -107,8 +106,6 @@ struct ekf_ctx {
   std::vector<char> pending;
   std::vector<int> prev_m;       // ≥ 0: last chunk was a pipelined pair (its record is valid)
   std::vector<std::array<int, kMaxChunk>> prev_ids;  // that chunk's landmark ids
-  std::vector<long> last_desc;   // plan_d index of the filter's last known-association chunk in
-                                 // the current (not yet uploaded) plan, −1: none
   std::vector<std::array<long, 2>> stg_desc;  // plan_d indices of its last two pipelined chunks
                                               // ([0] the last), −1: none (kStageOut planning)
   // launch plan: descriptors for a whole call (or a whole replay) uploaded with ONE copy
@@ -155,12 +152,8 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.rec = h->rec;
   a.rec_stride = static_cast<size_t>(h->F);
   a.stage = static_cast<StageRec<T>*>(h->stage);
-  a.rows = static_cast<T*>(h->rows);
-  a.rows_stride = static_cast<size_t>(h->ldk) * kRowW;
   a.sync = h->sync;
   a.fatal = h->fatal_d;
-  a.bout = h->bout;
-  a.chan = h->chan;
   a.desc = desc;
   a.n = h->n;
   a.ld = h->ld;
@@ -213,11 +206,8 @@ void fill_desc(MsgDesc* d, int m, int flags, int parity, const Pose2& odom) {
 }
 
 // The filter's next chunk has no planned predecessor in this plan (upload, association, posterior,
-// reset, device plan): no row hand-off, no staged rebuild operands.
-void forget_desc(ekf_ctx* h, int f) {
-  h->last_desc[f] = -1;
-  h->stg_desc[f] = {-1L, -1L};
-}
+// reset, device plan): no staged rebuild operands.
+void forget_desc(ekf_ctx* h, int f) { h->stg_desc[f] = {-1L, -1L}; }
 
 // slam.cpp:208-210 (host, glibc, as the reference)
 inline void measure(double rx, double ry, double* zr, double* zb) {
@@ -258,9 +248,6 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
   a.need_plan = a.polls ? h->need_plan : 0u;
   h->need_plan = 0;
   a.first_ready = h->epoch_owed ? 1 : 0;  // (the host joined the bulk stream since that pass)
-  // a builder workgroup per filter beside each chain (k_chain): multi-chunk device-epoch launches
-  a.build = a.polls && h->build && nchunks > 1 ? 1 : 0;
-  a.nf_launch = nf;
   {  // dev A/B: stream-ordered chains gather their (complete) Σ_in instead of rebuilding
     static const bool g = [] {
       const char* e = std::getenv("EKF_SERIAL_GATHER");
@@ -399,14 +386,6 @@ int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, bool poll) {
   });
 }
 
-// The chain's column of position a of a chunk's U (pose 0..2, marker c → 3+2·id, 4+2·id, a bad
-// id → slot 0's columns 3, 4).
-int ucol(const int* ids, int a, int N) {
-  if (a < 3) return a;
-  const int id = ids[(a - 3) >> 1];
-  return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
-}
-
 // Known association, one message per filter in [f0, f0+nf): msgs[k] holds filter f0+k's markers.
 // Predict + chunks of ≤ kMaxChunk corrections + posterior (slam.cpp:180-316), appended to the plan.
 // absent[k] (batch paths): filter f0+k receives no message this step — its descriptor is inactive,
@@ -447,16 +426,6 @@ void plan_known(ekf_ctx* h, int f0, int nf, bool predict, const char* absent = n
         d->z[i][0] = mk[b + i].zr;
         d->z[i][1] = mk[b + i].zb;
       }
-      // fp64: the previous chunk's Σ pass (same plan, not uploaded yet) hands this chunk's factor
-      // kernel Σ_in[i, U] as contiguous rows instead of a gather strided by ld
-      if (h->rows && !h->resident && h->last_desc[f] >= 0 && m > 0) {
-        MsgDesc* pd = &h->plan_d[h->last_desc[f]];
-        pd->flags |= kRowsOut;
-        pd->nxt_nu = 3 + 2 * m;
-        for (int a = 0; a < kMaxU + 1; ++a) pd->nxt_u[a] = a < pd->nxt_nu ? ucol(d->ids, a, h->cfg.n_landmarks) : 0;
-        d->flags |= kRowsIn;
-      }
-      h->last_desc[f] = m > 0 ? static_cast<long>(off + k) : -1;
       // the k_patch_stage behind the Σ pass two chunks back gathers this chain's rebuild operands
       // (the Σ_in' it reads is that pass's output)
       if ((flags & kLook) && h->stage && h->stg_desc[f][1] >= 0) {
@@ -519,15 +488,18 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
 }
 
 // Which path unknown association takes (EKF_ASSOC_*). k_assoc_msg's G workgroups per filter spin
-// on each other's granules, so all G must be resident at once on the CUs the bulk stream may use.
-// Workgroups are dispatched in order, block b on XCD b mod 8, and a filter's blocks come before the
-// next filter's on every XCD, so the earliest unfinished filter is always whole: progress needs G
-// workgroups on one XCD (XCD-local placement) or ⌈G / 8⌉ on each (agent placement), whatever the
-// number of filters. Beyond that the markers go one per launch (k_assoc + a launch pair).
+// on each other's granules, so all G must be resident at once on the CUs of the stream it runs on
+// (the bulk stream; the main stream with EKF_SERIAL, whose CU mask may be narrower): G workgroups
+// on one XCD (XCD-local placement) or ⌈G / 8⌉ on each (agent placement). A launch holds only as
+// many filters as the CUs hold at once (assoc_msg_group: co-resident by construction). Beyond
+// that the markers go one per launch (k_assoc + a launch pair).
+int assoc_cus_per_xcd(const ekf_ctx* h) {
+  return h->serial && h->main_cus_per_xcd > 0 ? h->main_cus_per_xcd : h->bulk_cus_per_xcd;
+}
 int am_route(ekf_ctx* h) {
   if (h->resident || !h->assoc_msg) return EKF_ASSOC_MARKER;
   const int G = (h->cfg.n_landmarks + kAmSlots - 1) / kAmSlots;
-  const int per_xcd = assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32) * h->bulk_cus_per_xcd;
+  const int per_xcd = assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32) * assoc_cus_per_xcd(h);
   const char* e = std::getenv("EKF_AM_XCD");  // EKF_AM_XCD=0: the agent placement only
   if (G > 1 && G <= per_xcd && !(e && std::atoi(e) == 0)) return EKF_ASSOC_CHUNK_XCD;
   if ((G + 7) / 8 <= per_xcd) return EKF_ASSOC_CHUNK;
@@ -564,6 +536,8 @@ int ensure_am(ekf_ctx* h) {
     return EKF_E_HIP;
   }
   h->am = b;
+  const int slots_x = assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32) * assoc_cus_per_xcd(h);
+  h->am_group = b.xcd ? 8 * std::max(1, slots_x / G) : std::max(1, 8 * slots_x / G);
   return EKF_OK;
 }
 
@@ -632,17 +606,30 @@ int assoc_msg_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, bool publis
     HIPCHK(hipEventRecord(h->ev_chain, h->stream));
     HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
     h->main_dirty = false;
+    h->main_unordered = false;
   }
   const unsigned seq = static_cast<unsigned>(h->seq);
+  // A filter's G workgroups spin on each other, so a launch holds only as many filters as the
+  // stream's CUs hold at once (workgroups are not guaranteed to be dispatched in order): XCD-local
+  // placement ⌊slots per XCD / G⌋ filters on each of the 8 XCDs (filter k of a launch on XCD
+  // k mod 8), agent placement ⌊slots / G⌋ filters spread over all of them. Filters are
+  // independent, so any grouping gives the same bits.
+  const int group_nf = h->am_group;
   auto run = [&](auto tag) -> int {
     using T = decltype(tag);
     PassArgs<T> a = args<T>(h, dptr, f0);
     a.seq = seq;
     a.polls = h->devsync && !h->serial ? 1 : 0;
-    int rc = timed(h, 2, bs, [&](hipEvent_t e0, hipEvent_t e1) {
-      return launch_assoc_msg<T>(a, h->am, nf, bs, e0, e1);
-    });
-    if (rc) return rc;
+    for (int g0 = 0; g0 < nf; g0 += group_nf) {
+      PassArgs<T> ag = args<T>(h, dptr + g0, f0 + g0);
+      ag.seq = a.seq;
+      ag.polls = a.polls;
+      const int gn = std::min(group_nf, nf - g0);
+      const int rc = timed(h, 2, bs, [&](hipEvent_t e0, hipEvent_t e1) {
+        return launch_assoc_msg<T>(ag, h->am, gn, bs, e0, e1);
+      });
+      if (rc) return rc;
+    }
     return timed(h, 0, bs, [&](hipEvent_t e0, hipEvent_t e1) {
       return launch_sigma_pass<T>(a, nf, publish_end, false, bs, e0, e1);
     });
@@ -769,6 +756,7 @@ int flush(ekf_ctx* h) {
   HIPCHK(hipEventRecord(h->ev_chain, h->stream));
   HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
   h->main_dirty = false;
+  h->main_unordered = false;
   HIPCHK(hipEventRecord(sl.ev, h->stream));
   sl.used = true;
   int rc = EKF_OK;
@@ -816,6 +804,7 @@ int flush(ekf_ctx* h) {
       if (join_bulk(h)) return EKF_E_HIP;
       rc = posterior_launch(h, dp, L.f0, L.nf);
       h->main_dirty = true;
+      h->main_unordered = true;  // (k_posterior reads its descriptor; no bulk work follows it)
     }
     ++li;
   }
@@ -941,7 +930,6 @@ int handle_info(ekf_t h, HandleInfo* out) {
   out->dtype = h->cfg.dtype;
   out->device = h->cfg.device;
   out->resident = h->resident;
-  out->rows = h->rows != nullptr && !h->resident;
   out->joseph = h->joseph;
   out->stream = h->stream;
   out->bulk = h->bulk ? h->bulk : h->stream;
@@ -1051,7 +1039,6 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   h->parity.assign(h->F, 0);
   h->pending.assign(h->F, 0);
   h->prev_m.assign(h->F, -1);
-  h->last_desc.assign(h->F, -1L);
   h->stg_desc.assign(h->F, std::array<long, 2>{-1L, -1L});
   h->prev_ids.assign(h->F, std::array<int, kMaxChunk>{});
   h->msgs.resize(h->F);
@@ -1099,14 +1086,6 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   if (hipMalloc(&h->mcat, km_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->ctl, sizeof(FilterCtl) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMalloc(&h->rec, 2 * sizeof(ChunkRec) * h->F) != hipSuccess) return fail(EKF_E_NOMEM);
-  // the Σ-pass → factor-kernel row hand-off (EKF_ROWS=1): coalesced Σ_in[i, U] for the factor
-  // kernel's row waves. Off by default since the fp64 pass is symmetric (the row waves read
-  // Σ_in[U, i], the same 128 B lines, without the pass's extra stores)
-  const char* rows_env = std::getenv("EKF_ROWS");
-  if (cfg.dtype == EKF_F64 && rows_env && std::atoi(rows_env) != 0 &&
-      // fp32's U block is rewritten after its pass (k_patch_stage): gathered there
-      hipMalloc(&h->rows, sizeof(double) * kRowW * h->ldk * h->F) != hipSuccess)
-    return fail(EKF_E_NOMEM);
   // staged rebuild operands (EKF_STAGE=0: every kLook chain gathers its own, tests compare the two)
   // The same many-filter handles skip it by default (EKF_STAGE=1 keeps it): there every message's
   // k_patch_stage runs on the serial critical path (≈ 18 µs for 512 filters), more than the chains'
@@ -1120,18 +1099,9 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     if (hipMalloc(&h->stage, stage_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
     if (hipMemset(h->stage, 0, stage_bytes) != hipSuccess) return fail(EKF_E_HIP);
   }
-  const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + kSyncKinds * h->F);
+  const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + h->F);
   if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
-  {  // the block builders: device epochs, staged operands, and room on the main stream's CUs of
-     // every XCD for the chain and the builder of its filters (one workgroup per CU: LDS)
-    const char* e = std::getenv("EKF_BUILD");  // opt-in (EKF_BUILD=1): measured slower, DESIGN.md
-    h->build = h->devsync && !h->serial && h->stage && !h->resident &&
-               h->main_cus_per_xcd >= 2 * ((h->F + 7) / 8) && e && std::atoi(e) != 0;
-    if (h->build && (hipMalloc(&h->bout, 2 * sizeof(BuildRec) * h->F) != hipSuccess ||
-                     hipMalloc(&h->chan, sizeof(BuildChan) * h->F) != hipSuccess))
-      return fail(EKF_E_NOMEM);
-  }
   h->ddesc_cap = std::max(kDescInit, static_cast<size_t>(h->F) * 4);
   if (hipMalloc(&h->ddesc, sizeof(MsgDesc) * h->ddesc_cap) != hipSuccess) return fail(EKF_E_NOMEM);
   for (int i = 0; i < kRing; ++i)
@@ -1144,11 +1114,9 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     if (hipMemsetAsync(h->x[p], 0, h->x_stride * h->F * sizeof(double), h->stream) != hipSuccess)
       return fail(EKF_E_HIP);
   }
-  // chunk records and the rows hand-off start zeroed: no kernel ever sees a previous process's
-  // bytes, whatever the stream interleaving
-  if (hipMemsetAsync(h->rec, 0, 2 * sizeof(ChunkRec) * h->F, h->stream) != hipSuccess ||
-      (h->rows && hipMemsetAsync(h->rows, 0, sizeof(double) * kRowW * h->ldk * h->F,
-                                 h->stream) != hipSuccess))
+  // chunk records start zeroed: no kernel ever sees a previous process's bytes, whatever the
+  // stream interleaving
+  if (hipMemsetAsync(h->rec, 0, 2 * sizeof(ChunkRec) * h->F, h->stream) != hipSuccess)
     return fail(EKF_E_HIP);
   if (hipMemsetAsync(h->kcat, 0, km_bytes, h->stream) != hipSuccess ||
       hipMemsetAsync(h->mcat, 0, km_bytes, h->stream) != hipSuccess ||
@@ -1177,7 +1145,6 @@ int ekf_destroy(ekf_t h) {
   if (h->mcat) hipFree(h->mcat);
   if (h->ctl) hipFree(h->ctl);
   if (h->rec) hipFree(h->rec);
-  if (h->rows) hipFree(h->rows);
   if (h->stage) hipFree(h->stage);
   if (h->ddesc) hipFree(h->ddesc);
   for (PlanState* p : h->dstate)
@@ -1199,8 +1166,6 @@ int ekf_destroy(ekf_t h) {
   if (h->ev_chain) hipEventDestroy(h->ev_chain);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->sync) hipFree(h->sync);
-  if (h->bout) hipFree(h->bout);
-  if (h->chan) hipFree(h->chan);
   for (hipEvent_t e : h->ev_sig)
     if (e) hipEventDestroy(e);
   if (h->bulk) hipStreamDestroy(h->bulk);
@@ -1360,12 +1325,21 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
       return EKF_E_NOMEM;
   }
   if (int rc = reserve_device(h, static_cast<size_t>(T) * F)) return rc;  // (no host staging)
-  // the bulk stream may still read the last descriptors (an idle one reads nothing: no hop)
-  if (hipStreamQuery(h->bulk) != hipSuccess && join_bulk(h)) return EKF_E_HIP;
   // device epochs: the planner runs on the bulk stream — ahead of the group's factor kernels and
   // Σ passes in stream order — and counts its descriptors, which the chain launch polls: the chain
   // starts beside the planner instead of behind a main → bulk event hop (≈ 6 µs of each replay)
-  const bool beside = h->devsync && !h->serial && !h->build;
+  const bool beside = h->devsync && !h->serial;
+  // the bulk stream may still read the last descriptors (an idle one reads nothing: no hop)
+  if (hipStreamQuery(h->bulk) != hipSuccess && join_bulk(h)) return EKF_E_HIP;
+  // ... and the main stream: work there that the bulk stream is not ordered after (a k_posterior
+  // of ekf_posterior reads its descriptor in ddesc) must end before a planner on the bulk stream
+  // rewrites ddesc. (Chains are covered: the bulk stream's factor kernels follow every chain
+  // through its epoch or an event, so a planner enqueued behind them runs after it.)
+  if (beside && h->main_unordered) {
+    HIPCHK(hipEventRecord(h->ev_chain, h->stream));
+    HIPCHK(hipStreamWaitEvent(h->bulk, h->ev_chain, 0));
+    h->main_unordered = false;
+  }
   hipStream_t ps = beside ? h->bulk : h->stream;
   if (!h->dev_plan) {  // the host mirror goes down once; later device replays chain on the device
     for (size_t f = 0; f < F; ++f) {
@@ -1396,7 +1370,6 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   a.F = h->F;
   a.M = m_max;
   a.N = h->cfg.n_landmarks;
-  a.rows = h->rows != nullptr;
   a.stage = h->stage != nullptr;
   a.plan_count = beside ? h->sync + kSyncPlan : nullptr;
   HIPCHK(launch_plan_replay(a, ps));
@@ -1494,8 +1467,7 @@ int ekf_sync(ekf_t h) {
 
 int ekf_get_schedule(ekf_t h, int* flags) {
   if (!h || !flags) return EKF_E_ARG;
-  *flags = (h->devsync ? EKF_SCHED_DEVSYNC : 0) | (h->build ? EKF_SCHED_BUILDER : 0) |
-           (h->serial ? EKF_SCHED_SERIAL : 0);
+  *flags = (h->devsync ? EKF_SCHED_DEVSYNC : 0) | (h->serial ? EKF_SCHED_SERIAL : 0);
   return EKF_OK;
 }
 
@@ -1597,10 +1569,14 @@ int ekf_set_state(ekf_t h, int f, const double* state, const double* sigma, cons
                      hipMemcpyHostToDevice));
   if (sigma) {
     std::vector<char> buf(h->sig_stride * h->w, 0);
+    // fp64 pipeline: Σ is kept exactly symmetric (the symmetric Σ pass mirrors its upper triangle
+    // and the factor kernel reads Σ_in[U, i] for Σ_in[i, U]), so the upper triangle is taken
+    const bool sym = h->w == 8 && !h->resident;
     for (int i = 0; i < h->n; ++i)
       for (int j = 0; j < h->n; ++j) {
         const size_t e = static_cast<size_t>(i) * h->ld + j;
-        const double v = sigma[static_cast<size_t>(i) * h->n + j];
+        const double v = sym && i > j ? sigma[static_cast<size_t>(j) * h->n + i]
+                                      : sigma[static_cast<size_t>(i) * h->n + j];
         if (h->w == 4)
           reinterpret_cast<float*>(buf.data())[e] = static_cast<float>(v);
         else

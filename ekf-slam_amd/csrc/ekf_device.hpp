@@ -20,13 +20,10 @@ constexpr int kZC = 2 * kMaxChunk;               // correction columns of Z / ro
 
 // Device epochs (unsigned words of the handle's sync buffer, each polled word on its own line):
 constexpr int kSyncSigma = 0;    // epoch (seq + 1) of the last complete Σ pass (k_sigma_epoch)
-constexpr int kSyncPlan = 1;     // (t, f) descriptors device replays have planned so far (a count)
+constexpr int kSyncPlan = 32;    // (t, f) descriptors device replays have planned so far (a count;
+                                 // its own 128-B line: the planner waves' fetch_adds do not contend
+                                 // with the polls of the Σ epoch in word 0)
 constexpr int kSyncChain = 64;   // [F]: epoch of each filter's last complete chain
-// Further [F] arrays behind kSyncChain (word kSyncChain + kind·F + f), the block builder's
-// hand-offs (k_chain, PassArgs::build): the chain's Z / Y progress ((seq << 5) | steps done), its
-// predict parameters (seq + 1) and the builder's finished block (seq + 1 of the block's chunk).
-constexpr int kSyncKindZ = 1, kSyncKindY = 2, kSyncKindPro = 3, kSyncKindBuilt = 4;
-constexpr int kSyncKinds = 5;
 
 // MsgDesc.flags
 constexpr int kFirst = 1;    // chunk carries the predict (slam.cpp:184-198) for this message
@@ -35,11 +32,6 @@ constexpr int kNoInit = 4;   // association path: no first-sighting init in the 
 constexpr int kActive = 8;   // filter takes part in this launch
 constexpr int kLook = 16;    // Σ_in not materialised yet: rebuild the chain's block from the
                              // previous chunk's Σ_in (other buffer) and ChunkRec
-constexpr int kRowsOut = 32; // Σ pass (fp64): also write Σ_out[i, U_next] to the rows buffer
-                             // (U_next = MsgDesc::nxt_u, the filter's next chunk's index set)
-constexpr int kRowsIn = 64;  // factor kernel: r(i) = Σ_in[i, U] from the rows buffer (written
-                             // by the previous chunk's Σ pass) instead of a strided gather
-constexpr int kRowW = kMaxU + 1;  // rows buffer: kRowW × ldk per filter (position-major)
 constexpr int kJoseph = 128; // Joseph-form Σ update (ekf_set_joseph): one marker per chunk, the
                              // factor rank 2 + 4 (K·M and (ΣHᵀ − K·S)·Kᵀ, see k_chain)
 constexpr int kStageOut = 256;  // behind this chunk's Σ pass (k_patch_stage): gather the rebuild
@@ -62,9 +54,6 @@ struct alignas(16) MsgDesc {
   int ids[kMaxChunk];        // landmark ids; < 0 ⇒ taken from FilterCtl::assoc_j[assoc_slot + c]
   double z[kMaxChunk][2];    // measured (range, bearing), computed on the host like slam.cpp:208-210
   int prev_ids[kMaxChunk];   // kLook: the previous chunk's ids (its index set U', known up front)
-  int nxt_nu;                   // kRowsOut: |U_next|
-  int pad2;
-  int nxt_u[kMaxU + 1];         // kRowsOut: U_next in the next chain's order (ekf_api index_map)
   int stg_m, stg_pm;            // kStageOut: markers of the filter's chunk after next / next chunk
   int pad3[2];
   int stg_ids[kMaxChunk];       // kStageOut: the chunk after next's ids (its U)
@@ -112,20 +101,6 @@ template <typename T>
 struct alignas(16) StageRec {
   double r0u[kStW], c0u[kStW], r0p[kStW], c0p[kStW], xg[kStW];
   T v[3][kStW * kStW];
-};
-
-// The next chunk's rebuilt block, from the builder workgroup to the chain (PassArgs::build):
-// P = Σ_in[U, U] before the chunk's own predict (the prologue's P after its K'·M' tiles), R =
-// Σ_pred'[U, U'] (x_in[U] = x' + R·Zx' for rows the previous chunk did not touch), xg = x_in'[U].
-// [2][F] by the built chunk's Σ parity. chan: the chain's predict parameters (a1, a2) for the
-// builder of its next chunk.
-struct alignas(16) BuildRec {
-  double P[kMaxU][kMaxU + 1];
-  double R[kMaxU][kMaxU + 1];
-  double xg[kMaxU + 1];
-};
-struct alignas(16) BuildChan {
-  double a1, a2;
 };
 
 // ---- unknown association of a whole chunk in one launch (k_assoc_msg, ekf_assoc.hip) ----

@@ -12,7 +12,6 @@ namespace ekfslam {
 struct HandleInfo {
   int F, N, n, dtype, device;
   bool resident;  // n ≤ kResidentMaxN fp64: one resident launch per plan
-  bool rows;      // fp64 pipeline: Σ-pass → factor-kernel row hand-off planned
   bool joseph;    // ekf_set_joseph is on (the HBM pipeline then needs one marker per chunk)
   hipStream_t stream;
   hipStream_t bulk;  // the factors / Σ-pass stream (the main stream when serial)

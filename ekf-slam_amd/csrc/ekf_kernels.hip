@@ -52,16 +52,7 @@ __device__ unsigned long long g_stamps[4 * 512];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                   \
       g_stamps[512 * (seq & 3) + (i)] = (v);                                      \
   } while (0)
-// the builder workgroup (block 8 of the build grid: filter 0's), thread t, ring slot of chunk seqv
-#define EKF_BSTAMP(seqv, i, t)                                                    \
-  do {                                                                            \
-    if (A.build && blockIdx.x == 8 && threadIdx.x == (t))                         \
-      g_stamps[512 * ((seqv) & 3) + (i)] = __builtin_amdgcn_s_memrealtime();      \
-  } while (0)
 #else
-#define EKF_BSTAMP(seqv, i, t) \
-  do {                         \
-  } while (0)
 #define EKF_STAMPT(i, t) \
   do {                   \
   } while (0)
@@ -145,8 +136,7 @@ struct ChainShared {
   double row0raw[kMaxU];  // Σ_in[0][u_b]
   double col0raw[kMaxU];  // Σ_in[u_a][0]
   double xU[1][kMaxU];    // x[U], owned by wave 0 during the corrections
-  double P[2][kMaxU][kMaxU + 1];    // Σ[U,U] (rows all, columns live) by chunk parity: waves 1–2
-                                    // rebuild the next chunk's block in the other one
+  double P[1][kMaxU][kMaxU + 1];    // Σ[U,U] (rows all, columns live)
   double Cz[kMaxChunk][4];  // wave 1, step c: C_k = M_k[:, pA_c]·Hᵀ·S⁻¹ (2×2) for k < c
   double Dy[kMaxChunk][4];  // wave 2, step c: D_k = H·K_k[pA_c] (2×2) for k < c
   double KU[kMaxChunk][kMaxU][2];
@@ -186,13 +176,6 @@ struct ChainShared {
   int pub;    // steps whose K, M, H, S⁻¹ wave 0 has published
   int pdone;  // steps wave 3 has applied outside the cross
   int any_init;  // a correction of this chunk initialised its landmark (slam.cpp:213-216)
-  // the builder workgroup (PassArgs::build): the block of its target chunk, rebuilt as the chain of
-  // the chunk before publishes its factors
-  int kdone;       // k-blocks whose K' columns are final (builder wave 0)
-  int mdone;       // k-blocks whose M' rows are final (builder wave 1)
-  int cdone;       // builder wave 1 has stored C̃ and D̃
-  int un[kMaxU];   // the target chunk's U
-  double c0U2[kMaxU];  // Σ_in[u⁺_a][0] (builder wave 1's copy)
 };
 
 
@@ -489,223 +472,6 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
 }
 
 
-// ---- the next chunk's block, rebuilt by the builder workgroup during this chunk's corrections ----
-// (device-epoch launches of more than one chunk, PassArgs::build.) The prologue's rebuild, spread
-// over the corrections: the same formulas and the same MFMA sequence (K' and M' tiles over U',
-// then P̃ −= K'·M' per k-block of 4 factor columns = 2 corrections, in order), so the block is
-// bit-identical to the one the prologue builds. "This chunk" below is the chunk before the target
-// (its U, its predict, its Z and Y); LDS through address-space-3 pointers.
-constexpr int kStE = (kStW * kStW + 63) / 64;  // 21 block entries per lane of one wave
-
-// the next chunk's U (k_chain A0's mapping: bad id → slot 0's columns, padding → 0)
-__device__ __forceinline__ int nb_ucol(LdsDesc* nd, int nun, int a, int N) {
-  if (a < 3) return a;
-  if (a >= nun) return 0;
-  const int id = nd->ids[(a - 3) >> 1];
-  return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
-}
-
-// Wave 1: R̃ = pred(Σ_in[U⁺, U]) into pv.R (the prologue's R), x_in[U⁺] into pv.xg. U⁺ = the next
-// chunk's U (nun entries), U = this chunk's (nu); the predict is this chunk's (first, a1, a2).
-template <typename T>
-__device__ __noinline__ void nb_intake_r(LdsChain* sh, LdsDesc* nd, const StageRec<T>* sgn, int nu,
-                                         int nun, int first, double q, int N) {
-  // lanes exchange values through LDS here: a convergent operation keeps the function convergent,
-  // so the compiler cannot split its call over divergent paths of the caller (it did, around a
-  // one-lane branch, and lane 0 ran the function alone)
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int lane = threadIdx.x & 63;
-  const int t = min(lane, kMaxU - 1);
-  T vr[kStE];  // every load in flight at once: one round trip
-#pragma unroll
-  for (int i = 0; i < kStE; ++i) vr[i] = sgn->v[1][min(lane + 64 * i, kStW * kStW - 1)];
-  const double s00 = sgn->r0u[0];
-  const double r0p = sgn->r0p[t], c0u = sgn->c0u[t], xg = sgn->xg[t];
-  if (lane < kMaxU) {
-    sh->pv.r0P[lane] = r0p;
-    sh->pv.c0U[lane] = c0u;
-    sh->pv.xg[lane] = xg;
-    sh->un[lane] = nb_ucol(nd, nun, lane, N);
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  const double a1 = sh->a1, a2 = sh->a2;
-#pragma unroll
-  for (int i = 0; i < kStE; ++i) {
-    const int e = lane + 64 * i, a = e / kStW, b = e - a * kStW;
-    if (e < kStW * kStW && a < nun) {
-      double v = 0.0;
-      if (b < nu) {
-        v = static_cast<double>(vr[i]);
-        if (first) {
-          const int ua = sh->un[a], ub = sh->u[b];
-          const double ai = alpha_of(ua, a1, a2), ak = alpha_of(ub, a1, a2);
-          v = v + ai * sh->pv.r0P[b];
-          v = v + (sh->pv.c0U[a] + ai * s00) * ak;
-          if (ua == ub && ua < 3) v += q;
-        }
-      }
-      sh->pv.R[a][b] = v;
-    }
-  }
-
-}
-
-// Wave 1: K' = R̃·Z (the prologue's K' tiles) for the complete k-blocks [kb, upto): column tile
-// kb/4, 3 row tiles; a tile's columns of later k-blocks are recomputed once final (a column's bits
-// depend on it alone). Z columns ≥ 2m and its padding row read as the record's zeros. Returns upto.
-__device__ __noinline__ int nb_ktiles(LdsChain* sh, int kb, int upto, int m, int nu) {
-  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
-  while (kb < upto) {
-    const int tj = kb >> 2, col = 16 * tj + i16;
-    for (int ti = 0; ti < 3; ++ti) {
-      double av[9], bv[9];
-      const int ar = min(16 * ti + i16, kMaxU - 1);
-#pragma unroll
-      for (int s0 = 0; s0 < 9; ++s0) {
-        const int k = 4 * s0 + k4;
-        av[s0] = sh->pv.R[ar][k];
-        bv[s0] = (k < kMaxU && col < 2 * m) ? sh->Z[min(k, kMaxU - 1)][col] : 0.0;
-      }
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s0 = 0; s0 < 9; ++s0)
-        if (4 * s0 < nu) acc = mfma_f64(av[s0], bv[s0], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * ti + k4 + 4 * r;
-        if (row < kMaxU) sh->pv.K[row][col] = acc[r];
-      }
-    }
-    kb = min(upto, 4 * tj + 4);
-  }
-  lds_publish3(&sh->kdone, kb);
-  return kb;
-}
-
-// Wave 2: C̃ = pred(Σ_in[U, U⁺]) into pv.C and D̃ = pred(Σ_in[U⁺, U⁺]) into P[pn] (the prologue's
-// C and P before K'·M').
-template <typename T>
-__device__ __noinline__ void nb_intake_cd(LdsChain* sh, LdsDesc* nd, const StageRec<T>* sgn, int pn,
-                                          int nu, int nun, int first, double q, int N) {
-  // lanes exchange values through LDS here: a convergent operation keeps the function convergent,
-  // so the compiler cannot split its call over divergent paths of the caller (it did, around a
-  // one-lane branch, and lane 0 ran the function alone)
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int lane = threadIdx.x & 63;
-  const int t = min(lane, kMaxU - 1);
-  T vc[kStE], vd[kStE];  // every load in flight at once: one round trip
-#pragma unroll
-  for (int i = 0; i < kStE; ++i) {
-    vc[i] = sgn->v[2][min(lane + 64 * i, kStW * kStW - 1)];
-    vd[i] = sgn->v[0][min(lane + 64 * i, kStW * kStW - 1)];
-  }
-  const double s00 = sgn->r0u[0];
-  const double r0u = sgn->r0u[t], c0p = sgn->c0p[t], c0u = sgn->c0u[t];
-  if (lane < kMaxU) {
-    sh->pv.r0U[lane] = r0u;
-    sh->pv.c0P[lane] = c0p;
-    sh->c0U2[lane] = c0u;
-    sh->un[lane] = nb_ucol(nd, nun, lane, N);  // (wave 1 stores the same)
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  const double a1 = sh->a1, a2 = sh->a2;
-#pragma unroll
-  for (int i = 0; i < kStE; ++i) {
-    const int e = lane + 64 * i, a = e / kStW, b = e - a * kStW;
-    if (e < kStW * kStW && a < nun) {
-      double w = 0.0;
-      if (b < nu) {
-        w = static_cast<double>(vc[i]);
-        if (first) {
-          const int ua = sh->un[a], ub = sh->u[b];
-          const double ai = alpha_of(ua, a1, a2), ak = alpha_of(ub, a1, a2);
-          w = w + ak * sh->pv.r0U[a];
-          w = w + (sh->pv.c0P[b] + ak * s00) * ai;
-          if (ua == ub && ua < 3) w += q;
-        }
-      }
-      sh->pv.C[b][a] = w;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < kStE; ++i) {
-    const int e = lane + 64 * i, a = e / kStW, b = e - a * kStW;
-    if (e < kStW * kStW && a < nun && b < nun) {
-      double v = static_cast<double>(vd[i]);
-      if (first) {
-        const int ua = sh->un[a], ub = sh->un[b];
-        const double ai = alpha_of(ua, a1, a2), aj = alpha_of(ub, a1, a2);
-        v = v + ai * sh->pv.r0U[b];
-        v = v + (sh->c0U2[a] + ai * s00) * aj;
-        if (ua == ub && ua < 3) v += q;
-      }
-      sh->P[pn][a][b] = v;
-    }
-  }
-}
-
-// Wave 2: M' = Y·C̃ (the prologue's M' tiles) for k-blocks [mb, upto). Y rows ≥ 2m and its
-// padding column read as the record's zeros. Returns upto.
-__device__ __noinline__ int nb_mtiles(LdsChain* sh, int mb, int upto, int m, int nu) {
-  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
-  while (mb < upto) {  // M' tiles of row tile ti (3 column tiles)
-    const int ti = mb >> 2, row = 16 * ti + i16;
-    for (int tj = 0; tj < 3; ++tj) {
-      double av[9], bv[9];
-      const int bc = min(16 * tj + i16, kMaxU - 1);
-#pragma unroll
-      for (int s0 = 0; s0 < 9; ++s0) {
-        const int k = 4 * s0 + k4;
-        av[s0] = (row < 2 * m && k < kMaxU) ? sh->Y[row][min(k, kMaxU - 1)] : 0.0;
-        bv[s0] = sh->pv.C[k][bc];
-      }
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s0 = 0; s0 < 9; ++s0)
-        if (4 * s0 < nu) acc = mfma_f64(av[s0], bv[s0], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (16 * tj + i16 < kMaxU) sh->pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[r];
-    }
-    mb = min(upto, 4 * ti + 4);
-  }
-  return mb;
-}
-
-// Wave 2: P̃ −= K'·M' over k-block pb (the prologue's P-tile MFMA sequence): all 9 tiles'
-// operands and accumulators read first, then the MFMAs. K' columns of the block from wave 1.
-__device__ __noinline__ void nb_pblock(LdsChain* sh, int pn, int pb, int nun) {
-  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
-  const int k = 4 * pb + k4;
-  double av[3], bv[3];
-  d4 acc[9];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    av[t] = -sh->pv.K[min(16 * t + i16, kMaxU - 1)][k];
-    bv[t] = sh->pv.M[k][min(16 * t + i16, kMaxU - 1)];
-  }
-#pragma unroll
-  for (int tt = 0; tt < 9; ++tt) {
-    const int ti = tt / 3, tj = tt - 3 * ti, cc = min(16 * tj + i16, kMaxU - 1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[tt][r] = sh->P[pn][min(16 * ti + k4 + 4 * r, kMaxU - 1)][cc];
-  }
-#pragma unroll
-  for (int tt = 0; tt < 9; ++tt) acc[tt] = mfma_f64(av[tt / 3], bv[tt % 3], acc[tt]);
-#pragma unroll
-  for (int tt = 0; tt < 9; ++tt) {
-    const int ti = tt / 3, tj = tt - 3 * ti, col = 16 * tj + i16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row2 = 16 * ti + k4 + 4 * r;
-      if (row2 < nun && col < nun) sh->P[pn][row2][col] = acc[tt][r];
-    }
-  }
-}
-
-
 // The previous chunk's predict on the gathered rebuild operands: v + α_i·Σ[0][j] +
 // (Σ[i][0] + α_i·Σ00)·α_j + Q̄, for D = Σ_in'[U, U] → P, R = Σ_in'[U, U'] → pv.R and
 // C = Σ_in'[U', U] → pv.C (R / C columns k ≥ |U'| up to 36 zeroed: MFMA k padding). Thread tid's
@@ -768,230 +534,6 @@ __device__ __forceinline__ void rebuild_rcd(ChainShared& sh, double (&P)[kMaxU][
       sh.pv.R[a][b] = vR;
       sh.pv.C[b][a] = wC;
     }
-  }
-}
-
-// P̃ −= K'·M' over k-blocks [pb0, pb1) in order (the prologue's P-tile MFMA sequence, a k-block at
-// a time): the 9 tiles' accumulators read once, one MFMA per tile and k-block, stored once (the
-// LDS round trip of an f64 accumulator is exact, so any split of the k-blocks gives the same bits).
-__device__ __noinline__ void nb_pblocks(LdsChain* sh, int pn, int pb0, int pb1, int nun) {
-  __builtin_amdgcn_wave_barrier();
-  const int lane = threadIdx.x & 63, i16 = lane & 15, k4 = lane >> 4;
-  d4 acc[9];
-#pragma unroll
-  for (int tt = 0; tt < 9; ++tt) {
-    const int ti = tt / 3, tj = tt - 3 * ti, cc = min(16 * tj + i16, kMaxU - 1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[tt][r] = sh->P[pn][min(16 * ti + k4 + 4 * r, kMaxU - 1)][cc];
-  }
-  for (int pb = pb0; pb < pb1; ++pb) {
-    const int k = 4 * pb + k4;
-    double av[3], bv[3];
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      av[t] = -sh->pv.K[min(16 * t + i16, kMaxU - 1)][k];
-      bv[t] = sh->pv.M[k][min(16 * t + i16, kMaxU - 1)];
-    }
-#pragma unroll
-    for (int tt = 0; tt < 9; ++tt) acc[tt] = mfma_f64(av[tt / 3], bv[tt % 3], acc[tt]);
-  }
-#pragma unroll
-  for (int tt = 0; tt < 9; ++tt) {
-    const int ti = tt / 3, tj = tt - 3 * ti, col = 16 * tj + i16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row2 = 16 * ti + k4 + 4 * r;
-      if (row2 < nun && col < nun) sh->P[pn][row2][col] = acc[tt][r];
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-
-// Word `kind` of filter f in the handle's sync buffer (ekf_device.hpp kSyncKind*).
-template <typename T>
-__device__ __forceinline__ unsigned* sync_word(const PassArgs<T>& A, int kind, int f) {
-  return A.sync + kSyncChain + static_cast<size_t>(kind) * A.rec_stride + f;
-}
-
-// A chunk t whose block the builder rebuilds from the chunk p before it: both active, t rebuilds
-// from staged operands (kLook | kStageIn), p is no Joseph chunk (its rank-4 factor stays with the
-// prologue) and has known ids only (A0 maps an association id through FilterCtl). The chain and
-// the builder evaluate it on the same two descriptors.
-__device__ __forceinline__ bool build_pred(const MsgDesc& dp, const MsgDesc& dt) {
-  constexpr int kNeed = kActive | kLook | kStageIn;
-  if (!(dp.flags & kActive) || (dp.flags & kJoseph) || (dt.flags & kNeed) != kNeed) return false;
-  bool ok = true;
-  for (int c = 0; c < dp.m; ++c) ok = ok && dp.ids[c] >= 0;
-  return ok;
-}
-
-// One lane polls a progress word of the chain until it reaches v (wrap-safe), then the wave
-// acquires; false on timeout.
-__device__ __forceinline__ bool wave_wait_acquire(const unsigned* p, unsigned v) {
-  bool ok = true;
-  if ((threadIdx.x & 63) == 0) ok = epoch_wait_acquire(p, v);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
-}
-
-// The builder workgroup of filter f (PassArgs::build). For every chunk t ≥ 1 of the launch whose
-// block its chain would rebuild from staged operands (build_pred), the prologue's rebuild — the
-// same expressions and MFMA sequence, so the same bits — while the chain still runs chunk t − 1
-// on another CU of the same XCD:
-//   intake (all waves, once the stage has landed: the Σ-pass epoch the chain of t would wait
-//     for): R̃, C̃, D̃ = the previous predict on the staged Σ_in' entries (rebuild_rcd);
-//   wave 0  K' = R̃·Z' column tiles, wave 1  M' = Y'·C̃ row tiles, for the k-blocks (two
-//     corrections each) whose Z' / Y' the chain's waves 1–2 have published (write-through record
-//     + progress words): every k-block complete at a poll in one round of loads and tiles;
-//   wave 2  P̃ −= K'·M' over the k-blocks both have finished (nb_pblocks).
-// P̃, R̃ and x_in' at U then go to BuildRec and the epoch kSyncKindBuilt: the chain of t reads them
-// instead of running its prologue's gather, previous predict and MFMA tiles.
-template <typename T>
-__device__ void chain_builder(const PassArgs<T>& A, int nchunks, int fy, ChainShared& sh,
-                              MsgDesc (&sdesc)[2]) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int f = A.f0 + fy;
-  LdsChain* shl = (LdsChain*)(&sh);
-  constexpr int kDV = static_cast<int>(sizeof(MsgDesc) / 16);
-  for (int ci = 1; ci < nchunks; ++ci) {
-    __syncthreads();
-    if (tid < 2 * kDV) {  // the chunk before (p) and the target (t)
-      const int w = tid / kDV, k = tid - w * kDV;
-      reinterpret_cast<uint4*>(&sdesc[w])[k] = reinterpret_cast<const uint4*>(
-          &A.desc[static_cast<size_t>(ci - 1 + w) * A.desc_stride + fy])[k];
-    }
-    __syncthreads();
-    const MsgDesc& dp = sdesc[0];
-    const MsgDesc& dt = sdesc[1];
-    if (!build_pred(dp, dt)) continue;
-    const unsigned seqp = A.seq + static_cast<unsigned>(ci - 1), seqt = seqp + 1u;
-    const int m = dp.m, np = 3 + 2 * m, nu = 3 + 2 * dt.m;
-    const int nk = (m + 1) >> 1;
-    EKF_BSTAMP(seqt, 400, 0);
-    if (tid < kMaxU) {  // U (target) and U' (the chunk before): A0's mapping of known ids
-      const int c = (tid - 3) >> 1, e = (tid - 3) & 1;
-      int u = tid < 3 ? tid : 0, up = u;
-      if (tid >= 3 && tid < nu) u = (dt.ids[c] >= A.N ? 3 : 3 + 2 * dt.ids[c]) + e;
-      if (tid >= 3 && tid < np) up = (dp.ids[c] >= A.N ? 3 : 3 + 2 * dp.ids[c]) + e;
-      sh.u[tid] = u;
-      sh.pv.u[tid] = up;
-    }
-    // Z' and Y' start zero (their columns / rows land k-block by k-block)
-    for (int e = tid; e < kMaxU * (kZC + 1); e += kChainThreads) (&sh.Z[0][0])[e] = 0.0;
-    for (int e = tid; e < kZC * (kMaxU + 1); e += kChainThreads) (&sh.Y[0][0])[e] = 0.0;
-    if (tid == 0) {
-      sh.kdone = 0;
-      sh.mdone = 0;
-      // the stage has landed (the chain of t waits for the same epoch) and the chain of p has
-      // published its predict parameters
-      const unsigned need = seqt - 1u;
-      bool ok = true;
-      if (need && !(A.first_ready && need <= A.seq))
-        ok = epoch_wait_acquire(A.sync + kSyncSigma, need);
-      ok = epoch_wait_acquire(sync_word(A, kSyncKindPro, f), seqp + 1u) && ok;
-      if (!ok) flag_timeout(&A.ctl[f].status, A.fatal);
-      sh.pv.a1 = A.chan[f].a1;
-      sh.pv.a2 = A.chan[f].a2;
-      sh.pv.first = (dp.flags & kFirst) ? 1 : 0;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    EKF_BSTAMP(seqt, 401, 0);
-    {  // intake: the staged entries (as the prologue loads them), then the previous predict
-      const StageRec<T>* sg = A.stage + static_cast<size_t>(dt.parity) * A.rec_stride + f;
-      T vd[kRebPer], vr[kRebPer], vc[kRebPer];
-#pragma unroll
-      for (int i = 0; i < kRebPer; ++i) {
-        const int es = min(tid + i * kChainThreads, kRebW * kRebW - 1);
-        vd[i] = sg->v[0][es];
-        vr[i] = sg->v[1][es];
-        vc[i] = sg->v[2][es];
-      }
-      const int tc = tid < kMaxU ? tid : 0;
-      const double r0u = sg->r0u[tc], c0u = sg->c0u[tc], r0p = sg->r0p[tc], c0p = sg->c0p[tc];
-      const double xg = sg->xg[tc];
-      if (tid < kMaxU) {
-        sh.pv.r0U[tid] = r0u;
-        sh.pv.c0U[tid] = c0u;
-        sh.pv.r0P[tid] = r0p;
-        sh.pv.c0P[tid] = c0p;
-        sh.pv.xg[tid] = xg;
-      }
-      __syncthreads();
-      rebuild_rcd<T>(sh, sh.P[0], vd, vr, vc, tid, nu, np, A.q);
-    }
-    __syncthreads();
-    EKF_BSTAMP(seqt, 402, 0);
-    const ChunkRec* rp = A.rec + static_cast<size_t>(dp.parity) * A.rec_stride + f;
-    bool ok = true;
-    if (wave == 0 || wave == 1) {  // K' (wave 0) / M' (wave 1) as the chain publishes Z' / Y'
-      const bool kz = wave == 0;
-      const unsigned* prog = sync_word(A, kz ? kSyncKindZ : kSyncKindY, f);
-      for (int kb = 0; kb < nk;) {
-        // every k-block complete at this poll (correction c done ⇒ progress (seqp << 5) | c + 1)
-        const unsigned want = (seqp << 5) | static_cast<unsigned>(min(2 * kb + 2, m));
-        unsigned got = want;
-        if (lane == 0) {
-          bool w = epoch_wait_acquire(prog, want);
-          ok = ok && w;
-          got = epoch_load(prog);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        got = __builtin_amdgcn_readfirstlane(got);
-        ok = __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;  // (lane 0 polled)
-        const int steps = static_cast<int>(got - (seqp << 5)) >= m || !ok
-                              ? m : static_cast<int>(got - (seqp << 5));
-        const int kb1 = steps >= m ? nk : max(steps >> 1, kb + 1);
-        const int nc = 4 * (kb1 - kb);  // factor columns (Z') / rows (Y') of these k-blocks
-        if (kz) {
-          for (int e = lane; e < kMaxU * nc; e += 64) {
-            const int row = e / nc, col = 4 * kb + (e - row * nc);
-            if (col < 2 * m) sh.Z[row][col] = rp->Z[row][col];
-          }
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: LDS keeps its order)
-          kb = nb_ktiles(shl, kb, kb1, m, np);
-          EKF_BSTAMP(seqt, 409 + kb, 0);
-        } else {
-          for (int e = lane; e < nc * kMaxU; e += 64) {
-            const int r = 4 * kb + e / kMaxU, col = e % kMaxU;
-            if (r < 2 * m) sh.Y[r][col] = rp->Y[r][col];
-          }
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          kb = nb_mtiles(shl, kb, kb1, m, np);
-          lds_publish(&sh.mdone, kb);
-          EKF_BSTAMP(seqt, 419 + kb, 64);
-        }
-      }
-    } else if (wave == 2) {  // P̃ −= K'·M' as both land
-      for (int pb = 0; pb < nk;) {
-        lds_wait_ge(&sh.kdone, pb + 1);
-        lds_wait_ge(&sh.mdone, pb + 1);
-        const int pb1 = min(__builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                &sh.kdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)),
-                            __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                &sh.mdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)));
-        nb_pblocks(shl, 0, pb, pb1, nu);
-        pb = pb1;
-        EKF_BSTAMP(seqt, 429 + pb, 128);
-      }
-    }
-    if (!ok && lane == 0) flag_timeout(&A.ctl[f].status, A.fatal);
-    __syncthreads();
-    // P̃ (rows / columns < |U|), R̃ (rows < |U|) and x_in' at U to the chain of t
-    BuildRec* bo = A.bout + static_cast<size_t>(dt.parity) * A.rec_stride + f;
-    for (int e = tid; e < kMaxU * kMaxU; e += kChainThreads) {
-      const int a = e / kMaxU, b = e - a * kMaxU;
-      if (a < nu) {
-        if (b < nu) st_wt(&bo->P[a][b], sh.P[0][a][b]);
-        st_wt(&bo->R[a][b], sh.pv.R[a][b]);
-      }
-    }
-    if (tid < nu) st_wt(&bo->xg[tid], sh.pv.xg[tid]);
-    drain_stores();
-    __syncthreads();
-    if (tid == 0) epoch_store(sync_word(A, kSyncKindBuilt, f), seqt + 1u);
-    EKF_BSTAMP(seqt, 440, 0);
   }
 }
 
@@ -1102,10 +644,10 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
       }
     }
   };
-  // fp64 without the row hand-off: Σ_in is symmetric, so a row wave's Σ_in[U, i] are also its
-  // columns' — one wave per 16 indices builds both Kcat rows and Mcat columns (half the waves
-  // and half the Σ_in reads of separate row and column waves, the same values)
-  const bool merged = sizeof(T) == 8 && A.rows == nullptr;
+  // fp64: Σ_in is symmetric, so a row wave's Σ_in[U, i] are also its columns' — one wave per 16
+  // indices builds both Kcat rows and Mcat columns (half the waves and half the Σ_in reads of
+  // separate row and column waves, the same values)
+  constexpr bool merged = sizeof(T) == 8;
   if (wg < row_tiles) {
     const int R0 = wg * 16;
     const int i = R0 + l16;
@@ -1115,12 +657,7 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
     // masked: a predicated load would be a branch with its own wait, one round trip per load
     T raw[9];
     T r0t;
-    if (d.flags & kRowsIn) {  // Σ_in[i, U] written contiguously by the previous chunk's Σ pass
-      const T* rr = A.rows + f * A.rows_stride + (vi ? i : 0);  // [kRowW][ldk]: 16 rows = 128 B
-      r0t = rr[0];  // u_0 = 0
-#pragma unroll
-      for (int s = 0; s < 9; ++s) raw[s] = rr[static_cast<size_t>(4 * s + ks) * A.ldk];
-    } else if (sizeof(T) == 8) {
+    if (sizeof(T) == 8) {
       // fp64 Σ is symmetric (the symmetric Σ pass mirrors every element below the diagonal), so
       // Σ_in[i, U] is read as Σ_in[U, i]: 16 consecutive i per row of U (128 B) instead of one
       // scattered element per lane and column of U
@@ -1194,11 +731,10 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
   }
 }
 
-// 16 rows or 16 columns per wave (fp64 without the row hand-off: both), per_filter workgroups of
-// 4 waves per filter
+// 16 rows or 16 columns per wave (fp64: both), per_filter workgroups of 4 waves per filter
 template <typename T>
 __host__ __device__ inline int factor_waves(const PassArgs<T>& a) {
-  return (sizeof(T) == 8 && !a.rows ? 1 : 2) * ((a.n + 15) / 16);
+  return (sizeof(T) == 8 ? 1 : 2) * ((a.n + 15) / 16);
 }
 
 // One workgroup per filter, persistent over the `nchunks` chunks of a launch (descriptors
@@ -1215,17 +751,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // the next one's (and computes its predicted pose from it).
   __shared__ MsgDesc sdesc[2];
   static_assert(sizeof(MsgDesc) % 16 == 0, "MsgDesc copied as uint4");
-  // build: a 1-D grid, 16 blocks per 8 filters — filter fy's chain is block 16·⌊fy/8⌋ + fy mod 8
-  // and its builder the block 8 after it, so both run on XCD fy mod 8 (dispatch deals blocks
-  // round robin over the XCDs) and hand off through that XCD's L2
-  int fy = blockIdx.y;
-  bool builder = false;
-  if (A.build) {
-    const int L = blockIdx.x;
-    fy = 8 * (L >> 4) + (L & 7);
-    builder = ((L >> 3) & 1) != 0;
-    if (fy >= A.nf_launch) return;
-  }
+  const int fy = blockIdx.y;
   const int f = A.f0 + fy;
   const int tid = threadIdx.x;
   const int ld = A.ld;
@@ -1234,10 +760,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // so padding rows / columns that feed MFMA or dot products as zeros really are zeros
   for (int e = tid; e < static_cast<int>(sizeof(ChainShared) / 8); e += blockDim.x)
     reinterpret_cast<double*>(&sh)[e] = 0.0;
-  if (builder) {
-    chain_builder<T>(A, nchunks, fy, sh, sdesc);
-    return;
-  }
   bool pre = false;        // sdesc[ci & 1] was prefetched by the previous chunk's epilogue
   unsigned pending = 0;    // chain epoch of the previous chunk, not yet published (its record
                            // stores are still in flight; see the epilogue)
@@ -1255,7 +777,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
   pre = false;
   const MsgDesc& d = sdesc[ci & 1];
-  auto& P = sh.P[ci & 1];
+  auto& P = sh.P[0];
   const bool active = (d.flags & kActive) != 0;
   const bool look = (d.flags & kLook) != 0 && !A.gather;
   // Publish the previous chunk's record before this chunk waits on anything the bulk stream
@@ -1272,8 +794,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // stream), and this record parity is free again once that pass is done (its factor kernel read
   // it); a chunk that gathers its own Σ_in needs the pass one back.
   const unsigned need = look ? (seq >= 2 ? seq - 1 : 0u) : seq;
-  // the builder workgroup rebuilt this chunk's block (it waited for the epoch `need` already)
-  const bool built = A.build && ci > 0 && build_pred(sdesc[(ci + 1) & 1], d);
   // A0's associated ids (k_assoc, earlier on this stream), loaded unconditionally (clamped) and
   // here, so that the barrier below completes them: under A0's branch the load was waited for,
   // vmcnt(0), together with every early load below
@@ -1283,18 +803,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // complete (epochs ≤ A.seq), published or not — the launch's second chunk needs the pass just
   // before the launch, whose epoch the flush that issued it did not publish (waiting for a later
   // epoch instead held that chunk until this launch's first pass: ≈ 27 µs)
-  if (A.polls && need && tid == 0 && !built && !(A.first_ready && need <= A.seq) &&
+  if (A.polls && need && tid == 0 && !(A.first_ready && need <= A.seq) &&
       !epoch_wait_acquire(A.sync + kSyncSigma, need))
-    flag_timeout(&ctl->status, A.fatal);
-  if (built && tid == 0 && !epoch_wait_acquire(sync_word(A, kSyncKindBuilt, f), seq + 1u))
     flag_timeout(&ctl->status, A.fatal);
   EKF_STAMP(305);
   // (Z, Φ are set up by wave 1 and Y, Ψ by wave 2 at the start of their step loops)
   if (tid == 0) sh.status = 0;
   __syncthreads();
   EKF_STAMP(0);
-  EKF_STAMPV(306, __builtin_amdgcn_s_memrealtime());  // (the builder's clock: 100 MHz, chip-wide)
-  EKF_STAMPV(304, built ? 1ull : 0ull);  // (EKF_STAMP(305): the builder's epoch acquired)
   const T* S = A.sig[d.parity] + f * A.sig_stride;
   const double* xin = A.x[d.parity] + f * A.x_stride;
   const int m = d.m;
@@ -1312,7 +828,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   constexpr int kPer = (kW * kW + kChainThreads - 1) / kChainThreads;  // 6
   // kLook with staged operands: the loads do not depend on A0's index sets, so they are issued
   // here and land during A0 (whose barrier orders LDS only)
-  const bool early = look && !built && (d.flags & kStageIn);
+  const bool early = look && (d.flags & kStageIn);
   double vz[kPer], vy[kPer];
   T vd[kPer], vr[kPer], vc[kPer];  // (as stored: half the registers at fp32 while A0 runs)
   double r0u = 0.0, c0u = 0.0, r0p = 0.0, c0p = 0.0, x2 = 0.0;
@@ -1368,11 +884,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     sh.u[tid] = u;
   }
   if (tid == 0) sh.nu_cnt = 3 + 2 * m;
-  // the next descriptor: here with a builder (waves 1–2 publish their progress for it when it
-  // builds the next chunk's block), else in the epilogue (off this barrier's path)
-  if (A.build && ci + 1 < nchunks && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
-    reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
-        &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + fy])[tid - 128];
   if (look && tid < kMaxU) {  // the previous chain's mapping of its ids (bad → slot 0)
     const int pm = d.prev_m;
     int u = 0;
@@ -1391,10 +902,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   lds_barrier();
   EKF_STAMP(1);
   const int nu = sh.nu_cnt;
-  // The builder rebuilds the next chunk's block during this chunk's corrections (device-epoch
-  // launches, staged operands, not after a Joseph chunk: its rank-4 factor stays with the prologue)
-  const MsgDesc& nd = sdesc[(ci + 1) & 1];
-  const bool bnext = A.build && ci + 1 < nchunks && build_pred(d, nd);
 
   // ---- A1: every global load of the prologue in one round ---------------------------------------
   // Each thread issues all of its loads before its first LDS store: indices are clamped rather
@@ -1408,28 +915,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const T* Sp = A.sig[d.parity ^ 1] + f * A.sig_stride;
     const double* xp = A.x[d.parity ^ 1] + f * A.x_stride;
     const int np = sh.pv.nu;
-    if (built) {  // the builder's P̃ (before this chunk's predict), R̃ and x_in' at U (its epoch was
-                  // acquired above); x[U'], Zx' of the chunk before and t_map_odom are in LDS already
-      const BuildRec* bo = A.bout + static_cast<size_t>(d.parity) * A.rec_stride + f;
-      constexpr int kBP = (kMaxU * kMaxU + kChainThreads - 1) / kChainThreads;  // 5
-      double bp[kBP], br[kBP];
-#pragma unroll
-      for (int i = 0; i < kBP; ++i) {
-        const int e = min(tid + i * kChainThreads, kMaxU * kMaxU - 1);
-        bp[i] = bo->P[e / kMaxU][e % kMaxU];
-        br[i] = bo->R[e / kMaxU][e % kMaxU];
-      }
-      const double bx = bo->xg[tid < kMaxU ? tid : 0];
-#pragma unroll
-      for (int i = 0; i < kBP; ++i) {
-        const int e = tid + i * kChainThreads, a = e / kMaxU, b = e % kMaxU;
-        if (a < nu && b < nu) P[a][b] = bp[i];
-        if (a < nu) sh.pv.R[a][b] = br[i];
-      }
-      if (tid < kMaxU) sh.pv.xg[tid] = bx;
-      __syncthreads();
-    }
-    if (!built) {  // (built: R̃ and P̃ came from the builder)
     const int tc = tid < kMaxU ? tid : 0;
     if (!early) {  // (early: the staged operands and the record's values are in registers)
 #pragma unroll
@@ -1528,12 +1013,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
     EKF_STAMP(7);
-    }  // !built
     __syncthreads();
     EKF_STAMP(5);
     // a Joseph chunk before: its V'·K'ᵀ term as rank 2..3 (K' columns 2..3 are V' = R·Z'[:, 2..3];
     // M' rows 2..3 become K'ᵀ, the column factor)
-    if (!built) {
     const bool pj = sh.pv.joseph != 0;
     if (pj) {
       for (int e = tid; e < 2 * kW; e += blockDim.x) {
@@ -1569,7 +1052,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         if (row < nu && col < nu) P[row][col] = acc[r];
       }
     }
-    }  // !built
     // waves 2 and 3 (two P tiles against wave 0's three): the predicted pose and x_in[U]
     if (wv == 2 && ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
       double a1, a2;
@@ -1693,7 +1175,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     pending = 0;
   }
   if (wave == 0) {
-    chain_wave0((LdsChain*)(&sh), (LdsDesc*)(&d), ci & 1, m, nu, joseph, A.r, seq);
+    chain_wave0((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, joseph, A.r, seq);
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
     // lane → column 3+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
     const int hb = lane & 31, hr = lane >> 5;
@@ -1744,15 +1226,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
     }
     const int li = lane < kMaxU ? lane : kMaxU - 1;
-    unsigned* zprog = sync_word(A, kSyncKindZ, f);
-    if (bnext) {  // the builder of the next chunk: this chunk's predict parameters
-      if (lane == 0) {
-        st_wt(&A.chan[f].a1, sh.a1);
-        st_wt(&A.chan[f].a2, sh.a2);
-      }
-      drain_stores();
-      if (lane == 0) epoch_store(sync_word(A, kSyncKindPro, f), seq + 1u);
-    }
     double zxa = 0.0;  // Σ_c Z_c ν_c of row `lane`, accumulated as the Z_c come (the record's Zx)
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
@@ -1827,10 +1300,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           }
         }
       }
-      if (bnext) {  // Z_c complete in the record: the builder may take it
-        drain_stores();
-        if (lane == 0) epoch_store(zprog, (seq << 5) | static_cast<unsigned>(c + 1));
-      }
       EKF_STAMPT(320 + c, 64);
     }
     if (lane < kMaxU) sh.Zx[lane] = zxa;
@@ -1841,7 +1310,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     for (int e = lane; e < (kZC - 2 * m) * kMaxU; e += 64)  // rows ≥ 2m of the record's Y are zero
       st_wt(&(&rec->Y[2 * m][0])[e], 0.0);
     const int lj = lane < kMaxU ? lane : kMaxU - 1;
-    unsigned* yprog = sync_word(A, kSyncKindY, f);
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1897,10 +1365,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           st_wt(&rec->Y[2 * c + 1][lane], in ? y1 : 0.0);
         }
       }
-      if (bnext) {  // Y_c complete in the record: the builder may take it
-        drain_stores();
-        if (lane == 0) epoch_store(yprog, (seq << 5) | static_cast<unsigned>(c + 1));
-      }
       EKF_STAMPT(360 + c, 128);
     }
   }
@@ -1947,13 +1411,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         ctl->tmo[0] = tmo.theta;
         ctl->tmo[1] = tmo.x;
         ctl->tmo[2] = tmo.y;
-        sh.tmo[0] = tmo.theta;  // (a built next chunk does not reload it)
+        sh.tmo[0] = tmo.theta;
         sh.tmo[1] = tmo.x;
         sh.tmo[2] = tmo.y;
       }
     }
   } else {
-    if (!A.build && pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
+    if (pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
       reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
           &A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + fy])[tid - 128];
     if (tid == 0 && sh.status) atomicOr(&ctl->status, sh.status);
@@ -1962,10 +1426,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     if (tid < kMaxU) {  // state weights: x_i += r_0(i)[U] · Σ_c Z_c ν_c
       const double zx = sh.Zx[tid];  // (wave 1's sum over the corrections)
       const bool in = tid < nu;
-      if (bnext) {  // what the next chunk's prologue reads from the record
-        sh.pv.Zx[tid] = zx;
-        sh.pv.xU[tid] = in ? xfin[tid] : 0.0;
-      }
       st_wt(&rec->Zx[tid], zx);
       st_wt(&rec->u[tid], sh.u[tid]);
       st_wt(&rec->alphaU[tid], in ? sh.alphaU[tid] : 0.0);
@@ -2104,7 +1564,7 @@ struct SigmaTile<float> {
   static __device__ __forceinline__ void run(const float* Sin, float* Sout, const float* kc,
                                              const float* mc, int n, int ld, int ldk, int kw,
                                              bool first, double qd, int R0, int C0, int lane,
-                                             float*, const int*, int, int*) {
+                                             float*) {
     F32TileRegs g;
     load(g, Sin, kc, mc, n, ld, ldk, R0, C0, lane);
     finish(g, Sout, n, ld, kw, first, qd, R0, C0, lane);
@@ -2188,15 +1648,10 @@ struct SigmaTile64 {
   static constexpr int kPol = TJ == 4 ? EKF_SIG_POL : 0;
   static constexpr int kRows = 32, kCols = 16 * TJ;
   static constexpr int kLds = kCols * kTS;  // doubles of the wave's transposed tile
-  // rows ≠ null (kRowsOut): also Σ_out[i, U_next] → rows[b·ldk + i] for the next chunk's factor
-  // kernel, b = the first position of the column in U_next (nxt[0..nnu)); (i, u) comes from the
-  // upper element (min, max), so a tile hands off its columns in U_next on and above the diagonal
-  // and its rows in U_next right of it
   static __device__ __forceinline__ void run(const double* Sin, double* Sout, const double* kc,
                                              const double* mc, int n, int ld, int ldk, int kw,
                                              bool first, double q, int R0, int C0, int lane,
-                                             double* rows, const int* nxt, int nnu, int* map,
-                                             int* rmap, double* tT) {
+                                             double* tT) {
     const int kr = lane >> 4, kcol = lane & 15;
     // descriptors based at the wave's row panel: offsets stay 32-bit for any n (a filter's Σ
     // may exceed 4 GiB), and the records end at row n
@@ -2209,7 +1664,6 @@ struct SigmaTile64 {
                                static_cast<unsigned>(min(n - C0, kCols)) * ld * 8u);
     const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
     double a[2][9], b[TJ][9], sv[2][TJ][4];
-    const int uk = rows ? nxt[min(lane, kMaxU)] : 0;  // issued with the operand loads
     const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 8u;
     unsigned mo[TJ], so[TJ];
     const unsigned rstride = static_cast<unsigned>(ld) * 8u;
@@ -2250,33 +1704,6 @@ struct SigmaTile64 {
           acc[ti][tj] = mfma_f64(live ? a[ti][s] : 0.0, live ? b[tj][s] : 0.0, acc[ti][tj]);
     }
     SIG_STAMP(2);
-    int bpos[TJ], rpos[2][4];
-#pragma unroll
-    for (int tj = 0; tj < TJ; ++tj) bpos[tj] = -1;
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rpos[ti][r] = -1;
-    if (rows) {  // wave-uniform: positions of the tile's columns and rows in U_next (this wave's LDS)
-      map[lane] = kMaxU + 1;
-      if (lane < kRows) rmap[lane] = kMaxU + 1;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (lane < nnu && uk >= C0 && uk < C0 + kCols) atomicMin(&map[uk - C0], lane);
-      if (lane < nnu && uk >= R0 && uk < R0 + kRows) atomicMin(&rmap[uk - R0], lane);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-      for (int tj = 0; tj < TJ; ++tj) {
-        const int bb = map[16 * tj + kcol];
-        bpos[tj] = bb <= kMaxU ? bb : -1;
-      }
-#pragma unroll
-      for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int bb = rmap[16 * ti + kr + 4 * r];
-          rpos[ti][r] = bb <= kMaxU ? bb : -1;
-        }
-    }
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -2291,10 +1718,6 @@ struct SigmaTile64 {
                                                 col >= row ? so[tj] + (16 * ti + 4 * r) * rstride : kOOB,
                                                 0, kPol);
           tT[cl * kTS + rl] = v;
-          if (col >= row && row < n && col < n) {
-            if (bpos[tj] >= 0) rows[static_cast<size_t>(bpos[tj]) * ldk + row] = v;
-            if (col > row && rpos[ti][r] >= 0) rows[static_cast<size_t>(rpos[ti][r]) * ldk + col] = v;
-          }
         }
     // the mirror, two rows of the transposed tile per store (LDS in order within the wave)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2366,8 +1789,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
   }
   const MsgDesc& d = A.desc[fb];
   constexpr bool kSym = sizeof(T) == 8;  // fp64: the symmetric tiles (SigmaTile64)
-  __shared__ int cmap[4][64];  // per wave: kRowsOut column → position in U_next
-  __shared__ int rmap[kSym ? 4 : 1][32];  // … and row (the symmetric tiles)
+  __shared__ int cmap[4][64];  // per wave (fp32 patch): tile row / column → first position in U
   __shared__ double tT[kSym ? 4 : 1][kSym ? 16 * (WIDE ? 4 : 2) * kTS : 1];  // (SigmaTile64::kLds)
   const int lane = threadIdx.x & 63;
   const int trows = (A.n + Tile::kRows - 1) / Tile::kRows;
@@ -2445,12 +1867,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
     const int f = A.f0 + fb;
     // this filter's rank (Joseph: K·M and V·Kᵀ per marker); rows beyond are stale
     const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
-    T* rows = (d.flags & kRowsOut) ? A.rows + f * A.rows_stride : nullptr;
     Tile::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
-                      A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
-                      (d.flags & kFirst) != 0, A.q, tr * Tile::kRows,
-                      tc * Tile::kCols, lane, rows, d.nxt_u, d.nxt_nu,
-                      cmap[threadIdx.x >> 6], rmap[threadIdx.x >> 6], tT[threadIdx.x >> 6]);
+              A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
+              (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane,
+              tT[threadIdx.x >> 6]);
   }
   SIG_STAMP(3);
 }
@@ -2748,10 +2168,7 @@ void launch(K kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t e0, hipEv
 template <typename T>
 hipError_t launch_chain(const PassArgs<T>& a, int nf, int nchunks, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1) {
-  if (a.build)  // chain + builder per filter, 16 blocks per 8 filters (k_chain)
-    launch(k_chain<T>, dim3(16 * ((nf + 7) / 8)), dim3(kChainThreads), s, e0, e1, a, nchunks);
-  else
-    launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a, nchunks);
+  launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a, nchunks);
   return hipGetLastError();
 }
 

@@ -21,8 +21,6 @@ struct PassArgs {
   T* mcat;              // [KW][ldk] per filter (row k = one rank-1 factor over cols c)
   size_t km_stride;
   int ldk;
-  T* rows;              // fp64: [kRowW][ldk] per filter, Σ_in[i, U] handed from a Σ pass to the
-  size_t rows_stride;   // next chunk's factor kernel (kRowsOut / kRowsIn)
   FilterCtl* ctl;
   ChunkRec* rec;        // [2][rec_stride]: chunk records by Σ parity (chain → factors, next chain)
   size_t rec_stride;
@@ -38,16 +36,8 @@ struct PassArgs {
                         // the bulk stream before it, and the last pass published no epoch)
   int polls;            // 1: the streams hand off through device epochs (kernels poll them);
                         // 0: stream order / events order everything, no poll and no epoch kernel
-  int build;            // chain launches of > 1 chunk with device epochs, EKF_BUILD=1: a builder
-                        // workgroup per filter rebuilds each next chunk's block during the
-                        // corrections (k_chain: 1-D grid, chain of filter f = block 16·⌊f/8⌋ +
-                        // f mod 8, builder 8 later, both on XCD f mod 8); 0 (default): every
-                        // chunk's prologue rebuilds its own
-  int nf_launch;        // filters of the launch (build: the 1-D grid's bound)
   int gather;           // chain (dev A/B, EKF_SERIAL_GATHER=1): in stream order every chunk
                         // gathers its complete Σ_in instead of a kLook rebuild
-  BuildRec* bout;       // [2][rec_stride] the builder's blocks
-  BuildChan* chan;      // [rec_stride] the chain's predict parameters for the builder
   const MsgDesc* desc;
   int desc_stride;      // descriptors between consecutive chunks of a chain launch
   int n, ld, N, f0;
@@ -144,7 +134,6 @@ struct ReplayArgs {
   PlanState* st_out;      // [F]
   MsgDesc* desc;          // [T][F]
   int T, F, M, N;
-  int rows;               // fp64 pipeline: kRowsOut / kRowsIn hand-offs
   int stage;              // staged rebuild operands (kStageOut / kStageIn)
   unsigned* plan_count;   // non-null: every wave adds 1 here once its descriptor is stored (the
                           // chain polls it instead of waiting for the planner's kernel boundary)

@@ -4,8 +4,8 @@
 //
 // One wave per (t, f), all in parallel. What a host plan carries from chunk to chunk is found by
 // scanning the counts instead: the filter's previous active message (its markers are this
-// chunk's U' for the kLook rebuild), the next two (the kRowsOut hand-off to the next chunk, the
-// kStageOut operands of the chunk after next), and the active messages before t (the parity).
+// chunk's U' for the kLook rebuild), the one after next (the kStageOut operands of the chunk
+// after next), and the active messages before t (the parity).
 // A message with count 0 is no message (ekf_batch_sensor: the filter sits the step out); one
 // whose markers are all DELETE is a predict + posterior (slam.cpp:205), as on the host.
 #include <hip/hip_runtime.h>
@@ -16,13 +16,6 @@
 
 namespace ekfslam {
 namespace {
-
-// chain column of position a of U for this marker list (ekf_api.cpp ucol)
-__device__ __forceinline__ int ucol_of(const int* ids, int a, int N) {
-  if (a < 3) return a;
-  const int id = ids[(a - 3) >> 1];
-  return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
-}
 
 struct PlanShared {
   MsgDesc d;
@@ -143,13 +136,6 @@ __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
     if (lane < 3) d.odom[lane] = od;
     if (lane == 0) {
       int flags = kActive | kFirst | kLast | (prev_m >= 0 ? kLook : 0);
-      // fp64: the previous chunk's Σ pass hands this chunk's factor kernel Σ_in[i, U] (plan_known:
-      // only between chunks of this plan, both with markers)
-      if (A.rows && prev >= 0 && sh.m[1] > 0 && m > 0) flags |= kRowsIn;
-      if (A.rows && next >= 0 && m > 0 && sh.m[2] > 0) {
-        flags |= kRowsOut;
-        d.nxt_nu = 3 + 2 * sh.m[2];
-      }
       // the chain two chunks on rebuilds from operands this chunk's Σ pass stages (plan_known:
       // both chunks in this plan); this chunk reads the ones staged two chunks back
       if (A.stage && prev_m >= 0 && prev2 >= 0) flags |= kStageIn;
@@ -163,8 +149,6 @@ __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
       d.parity = s0.parity ^ (before & 1);
       d.prev_m = prev_m;
     }
-    if (A.rows && next >= 0 && m > 0 && sh.m[2] > 0 && lane <= kMaxU)
-      d.nxt_u[lane] = lane < 3 + 2 * sh.m[2] ? ucol_of(sh.ids[2], lane, A.N) : 0;
     if (A.stage && next2 >= 0 && lane < kMaxChunk) {
       d.stg_ids[lane] = sh.ids[3][lane];
       d.stg_pids[lane] = sh.ids[2][lane];

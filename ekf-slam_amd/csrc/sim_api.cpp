@@ -354,7 +354,6 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
   a.m = s->m;
   a.M = s->cfg.marker_stride;
   a.N = s->info.N;
-  a.rows = s->info.rows ? 1 : 0;
   a.slip = s->cfg.slip;
   a.sigma = s->cfg.sensor_sigma;
   a.range = s->cfg.max_range;

@@ -68,13 +68,6 @@ __device__ __forceinline__ Pose2 scan_compose(Pose2 d, int lane) {
   return d;
 }
 
-// chain column of position a of U for this marker list (ekf_api.cpp ucol)
-__device__ __forceinline__ int ucol(const int* ids, int a, int N) {
-  if (a < 3) return a;
-  const int id = ids[(a - 3) >> 1];
-  return (id < 0 || id >= N ? 3 : 3 + 2 * id) + ((a - 3) & 1);
-}
-
 struct SimShared {
   double bx[kSimMaxMap], by[kSimMaxMap];
   unsigned sighted[kSimMaxMap / 32];
@@ -250,7 +243,6 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
   Pose2 odo{S.odom[0], S.odom[1], S.odom[2]};
   int par = A.par[f];
   int prev_m = -1;       // the previous active chunk of this run (−1: the run's first gathers Σ_in)
-  long prev_t = -1;      // its message index, for the row hand-off
   for (int t = 0; t < A.T; ++t) {
     const long long msg = A.msg0 + t;
     wheels(A, seed, t, lane, truth, odo);
@@ -296,21 +288,9 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
     }
     if (lane < kMaxChunk) d->prev_ids[lane] = prev_m >= 0 ? sh.prev_ids[lane] : 0;
     __syncthreads();
-    // fp64 pipeline: the previous chunk's Σ pass hands this chunk's factor kernel Σ_in[i, U]
-    // (ekf_api.cpp plan_known: kRowsOut on that chunk, kRowsIn on this one)
-    if (A.rows && m > 0 && prev_m > 0 && prev_t >= 0) {
-      MsgDesc* pd = A.desc + static_cast<size_t>(prev_t) * A.F + f;
-      if (lane <= kMaxU) pd->nxt_u[lane] = lane < 3 + 2 * m ? ucol(sh.ids, lane, A.N) : 0;
-      if (lane == 0) {
-        pd->flags |= kRowsOut;
-        pd->nxt_nu = 3 + 2 * m;
-        d->flags |= kRowsIn;
-      }
-    }
     if (lane < kMaxChunk) sh.prev_ids[lane] = lane < m ? sh.ids[lane] : 0;
     __syncthreads();
     prev_m = m;
-    prev_t = t;
     par ^= 1;
   }
   // state for the next run

@@ -31,7 +31,6 @@ struct SimArgs {
   unsigned long long seed;
   long long tick0, msg0;   // global tick / message index of this run's first
   int f0, F, L, T, tpm, m, M, N;
-  int rows;                // fp64 pipeline: plan the Σ-pass → factor-kernel row hand-off
   double slip, sigma, range, radius, track;
   double start[3];
 };

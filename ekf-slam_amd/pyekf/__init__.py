@@ -19,7 +19,7 @@ EKF_OK, EKF_E_ARG, EKF_E_RANGE, EKF_E_EMPTY, EKF_E_NUMERIC, EKF_E_HIP, EKF_E_NOM
 EKF_E_TIMEOUT = -7
 EKF_FLAG_RANGE, EKF_FLAG_NUMERIC, EKF_FLAG_TIMEOUT = 1, 2, 4
 EKF_ASSOC_MARKER, EKF_ASSOC_CHUNK, EKF_ASSOC_CHUNK_XCD = 0, 1, 2
-EKF_SCHED_DEVSYNC, EKF_SCHED_BUILDER, EKF_SCHED_SERIAL = 1, 2, 4
+EKF_SCHED_DEVSYNC, EKF_SCHED_SERIAL = 1, 4
 EKF_F64, EKF_F32 = 0, 1
 EKF_PATH_PIPELINE, EKF_PATH_RESIDENT = 0, 1
 ADD, DELETE = 0, 2

@@ -97,15 +97,15 @@ int ekf_get_path(ekf_t h, int* path);
 int ekf_get_assoc_route(ekf_t h, int* route);
 
 /* The handle's schedule (fixed at ekf_create), bit flags:
- *   EKF_SCHED_DEVSYNC  the chain and bulk streams hand off through device epochs (<= 32 filters,
- *                      disjoint CU masks; EKF_DEVSYNC=0 or more filters: HIP events);
- *   EKF_SCHED_BUILDER  multi-chunk chain launches run a builder workgroup per filter that
- *                      rebuilds each next chunk's block during the corrections (opt-in,
- *                      EKF_BUILD=1, <= 16 filters; slower than the chain's own rebuild so far);
- *   EKF_SCHED_SERIAL   every kernel on one stream (EKF_SERIAL=1).
- * Every schedule gives bit-identical results. */
+ *   EKF_SCHED_DEVSYNC  <= 32 filters: the chain and bulk streams get disjoint CU masks and hand off
+ *                      through device epochs (EKF_DEVSYNC=0: HIP events between the two streams);
+ *   EKF_SCHED_SERIAL   every kernel on one stream. The default for > 32 filters (their Σ passes
+ *                      fill every CU, so two streams overlap nothing; the staged rebuild operands
+ *                      are off there too, EKF_STAGE=1 restores them); EKF_SERIAL=1 forces it for
+ *                      any handle, EKF_SERIAL=0 keeps two streams (HIP events) for > 32 filters.
+ * Every schedule gives bit-identical results. (Bit 2, a block-builder schedule of earlier
+ * releases, is retired and never set.) */
 #define EKF_SCHED_DEVSYNC 1
-#define EKF_SCHED_BUILDER 2
 #define EKF_SCHED_SERIAL 4
 int ekf_get_schedule(ekf_t h, int* flags);
 
@@ -191,7 +191,11 @@ int ekf_get_pose(ekf_t h, int filter, double* theta_x_y);
 int ekf_get_map_odom(ekf_t h, int filter, double* theta_x_y); /* t_map_odom */
 /* state[n] (fp64), sigma[n*n] row-major fp64 (nullable), counter (nullable) */
 int ekf_get_state(ekf_t h, int filter, double* state, double* sigma, unsigned* counter);
-/* overwrite a filter (fixtures / resync after an association flip); t_map_odom nullable */
+/* overwrite a filter (fixtures / resync after an association flip); t_map_odom nullable.
+ * fp64 pipeline handles keep Σ exactly symmetric (the Σ pass computes the upper triangle and
+ * mirrors it), so sigma's upper triangle is taken and mirrored below the diagonal; the reference's
+ * own (I − KH)Σ (slam.cpp:264-265) is symmetric up to rounding. fp32 and resident handles store
+ * sigma as given. */
 int ekf_set_state(ekf_t h, int filter, const double* state, const double* sigma,
                   const double* t_map_odom, unsigned counter);
 int ekf_get_status(ekf_t h, int filter, unsigned* flags); /* and clears them */

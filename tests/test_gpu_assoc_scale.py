@@ -6,10 +6,11 @@ every decision equal to the oracle's, the state within the tolerances of tests/t
 (fp64: poses 1e-8, state 5e-8, Σ 1e-7; fp32 Σ: poses 1e-6, state 1e-5, Σ 5e-5).
 
 Also: more filters than the GPU holds workgroups at once (64 filters × 16 = 1 024 workgroups:
-a filter's workgroups spin on each other, so completion relies on in-order dispatch, ekf_api.cpp
-am_route), the one-marker-per-launch route when a filter's workgroups cannot all be resident
-(EKF_CU_SPLIT leaves the bulk stream one CU per XCD), and a forced exchange timeout, which must
-reach the caller as EKF_E_TIMEOUT / EKF_FLAG_TIMEOUT."""
+a filter's workgroups spin on each other, so the host launches them in groups the CUs hold at
+once, ekf_api.cpp assoc_msg_group), the one-marker-per-launch route when a filter's workgroups
+cannot all be resident (EKF_CU_SPLIT leaves the bulk stream one CU per XCD), the single-stream
+schedule (EKF_SERIAL=1: the association runs on the main stream's narrower CU mask), and a forced
+exchange timeout, which must reach the caller as EKF_E_TIMEOUT / EKF_FLAG_TIMEOUT."""
 import json
 import os
 
@@ -202,10 +203,10 @@ def test_assoc_n1024_near_the_gate(map1024, xcd, monkeypatch):
 
 @pytest.mark.parametrize("xcd", ["1", "0"], ids=["xcd_local", "agent"])
 def test_assoc_more_filters_than_resident_workgroups(map1024, xcd, monkeypatch):
-    """64 filters at N = 1024 in one handle: 1 024 workgroups of k_assoc_msg per launch, twice what
-    the GPU's CUs hold at once (two per CU), so later filters' workgroups queue behind earlier
-    ones that spin on each other. Every filter ends bit-identical to a one-filter handle, whose
-    state equals the oracle's (fp32 Σ tolerances)."""
+    """64 filters at N = 1024 in one handle: 1 024 workgroups of k_assoc_msg per chunk, more than
+    the bulk stream's CUs hold at once, so the host splits the chunk into launches of co-resident
+    filters (a filter's workgroups spin on each other). Every filter ends bit-identical to a
+    one-filter handle, whose state equals the oracle's (fp32 Σ tolerances)."""
     sc, odom, ws, (xr, Sr, _, cr), _ = map1024
     w, T, F = sc.n_warm, 4, 64
     x, S, tmo, cnt = ws
@@ -239,6 +240,24 @@ def test_assoc_more_filters_than_resident_workgroups(map1024, xcd, monkeypatch):
     assert c1 == co
     assert np.abs(x1 - xo).max() < F32_STATE_TOL
     assert np.abs(S1 - So).max() < F32_SIGMA_TOL
+
+
+def test_assoc_n1024_serial_schedule(map1024, monkeypatch):
+    """EKF_SERIAL=1 on a one-filter handle: k_assoc_msg runs on the main stream, whose CU mask holds
+    4 CUs per XCD (8 resident workgroups per XCD < G = 16), so the route comes from those CUs —
+    the agent placement, G / 8 workgroups per XCD — not from the bulk stream's (which would pick
+    the XCD-local exchange and spin into its timeout). Every decision equal to the oracle's, fp64
+    tolerances, no timeout."""
+    _env(monkeypatch, EKF_SERIAL="1")
+    sc, odom, ws, (xr, Sr, _, cr), out = map1024
+    perr, xg, Sg, cg, n_new, n_old = _gpu_sensor(1024, sc, odom, ws, out,
+                                                 route=pyekf.EKF_ASSOC_CHUNK)
+    ERRORS["n1024_serial"] = {"new": n_new, "associated": n_old, "pose": perr,
+                              "state": float(np.abs(xg - xr).max())}
+    assert n_new > 0 and n_old > 0 and cg == cr
+    assert perr < POSE_TOL
+    assert np.abs(xg - xr).max() < STATE_TOL
+    assert np.abs(Sg - Sr).max() < SIGMA_TOL
 
 
 @pytest.fixture(scope="module")

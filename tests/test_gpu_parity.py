@@ -221,6 +221,24 @@ def test_pipelined_replay_sync_modes(monkeypatch, F):
     assert np.abs(S - o["sigma"]).max() < 1e-7
 
 
+@pytest.mark.parametrize("F", [1, 4], ids=["1filter", "4filters"])
+def test_pipelined_replay_sync_modes_multichunk(monkeypatch, F):
+    """Messages of up to 24 markers span two chunks (the second chunk of a message rebuilds from
+    the first, kLook within the message): the three schedules bit-identical (LDS poisoned)."""
+    sc = synth.synthetic(96, 14, max_markers=24)
+    assert sc.count.max() > 16  # some messages span two chunks
+    pyekf.poison_lds()
+    dev = _pipelined_final(sc, monkeypatch, {"EKF_DEVSYNC": "1"}, F=F)
+    evt = _pipelined_final(sc, monkeypatch, {"EKF_DEVSYNC": "0"}, F=F)
+    ser = _pipelined_final(sc, monkeypatch, {"EKF_SERIAL": "1"}, F=F)
+    for (xd, Sd, cd), (xe, Se, ce), (xs, Ss, cs) in zip(dev, evt, ser):
+        assert cd == ce == cs
+        np.testing.assert_array_equal(xd, xs)
+        np.testing.assert_array_equal(Sd, Ss)
+        np.testing.assert_array_equal(xe, xs)
+        np.testing.assert_array_equal(Se, Ss)
+
+
 def test_pipelined_replay_fp32_n1024_sync_modes(monkeypatch):
     """Config 3 size, fp32 Σ, 24 messages pipelined: the device-epoch schedule (EKF_DEVSYNC=1,
     LDS poisoned first) and the single stream: bit-identical."""
@@ -302,31 +320,6 @@ def test_many_filters_match_small_batch(F, devsync, monkeypatch):
         # the symmetric fp64 Σ pass (wide tiles here, narrow in the 8-filter handle) leaves Σ
         # exactly symmetric
         np.testing.assert_array_equal(Sb, Sb.T)
-
-
-@pytest.mark.parametrize("F,env", [(1, {"EKF_DEVSYNC": "0"}), (4, {"EKF_DEVSYNC": "0"}), (40, {}),
-                                   (1, {"EKF_DEVSYNC": "1"}), (4, {"EKF_DEVSYNC": "1"})],
-                         ids=["1filter", "4filters", "40filters", "1filter_devsync",
-                              "4filters_devsync"])
-def test_rows_handoff_is_bit_identical(monkeypatch, F, env):
-    """fp64: with EKF_ROWS=1 a Σ pass hands the next chunk's factor kernel Σ_in[i, U] as contiguous
-    rows (kRowsOut / kRowsIn) — the very values it stores into Σ_out (the symmetric pass: from a
-    tile's columns in U on and above the diagonal, and its rows in U right of it), so the replay
-    equals the default's reads of Σ_in[U, i] (EKF_ROWS=0) bit for bit, including messages longer
-    than one chunk; in the event-synchronised schedule and the (default) device-epoch one (LDS
-    poisoned first)."""
-    if env.get("EKF_DEVSYNC") != "0":
-        pyekf.poison_lds()
-    sc = synth.synthetic(96, 14, max_markers=24)
-    assert sc.count.max() > 16  # some messages span two chunks
-    monkeypatch.setenv("EKF_ROWS", "1")
-    on = _pipelined_final(sc, monkeypatch, env, F=F)
-    monkeypatch.setenv("EKF_ROWS", "0")
-    off = _pipelined_final(sc, monkeypatch, env, F=F)
-    for (x1, S1, c1), (x0, S0, c0) in zip(on, off):
-        assert c1 == c0
-        np.testing.assert_array_equal(x1, x0)
-        np.testing.assert_array_equal(S1, S0)
 
 
 @pytest.mark.parametrize("name,dtype,N", [("basic_world_known", pyekf.EKF_F64, 12000),

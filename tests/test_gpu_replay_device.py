@@ -82,13 +82,13 @@ def _close(a, b, tol, stol=SIGMA_TOL):
 
 
 @pytest.mark.parametrize("F,env", [(1, {}), (4, {}), (1, {"EKF_DEVSYNC": "0"}),
-                                   (4, {"EKF_SERIAL": "1"}), (3, {"EKF_STAGE": "0", "EKF_ROWS": "0"})],
+                                   (4, {"EKF_SERIAL": "1"}), (3, {"EKF_STAGE": "0"})],
                          ids=["1filter", "4filters", "1filter_events", "4filters_serial",
                               "3filters_nostage_norows"])
 def test_device_replay_equals_host_replay(monkeypatch, F, env):
     """fp64 N = 96 (the HBM pipeline), 30 messages, every schedule: the device-planned replay ends
     where the host-planned one does, holes (empty and all-DELETE messages) included."""
-    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE", "EKF_ROWS"):
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -114,6 +114,40 @@ def test_device_replay_chains_with_host_calls():
     o = orc.run_scenario(scs[0], False)
     assert np.abs(mixed[0][0] - o["state"]).max() < 1e-7
     assert np.abs(mixed[0][1] - o["sigma"]).max() < 1e-7
+
+
+def test_posterior_then_device_replay(monkeypatch):
+    """ekf_posterior enqueues k_posterior on the main stream, reading its descriptor in the upload
+    buffer; with device epochs the next ekf_replay_device plans on the bulk stream and rewrites that
+    buffer, so it must wait for the posterior first (ekf_api.cpp main_unordered). Four filters:
+    host span, a posterior per filter, device span — against the single-stream schedule (planner
+    and posterior in one stream order): bit-identical state and t_map_odom."""
+    scs = [synth.synthetic(80, 24, seed=31 + k) for k in range(4)]
+    F = 4
+    full = _inputs(scs, F, 0, 24)
+    res = []
+    for env in ({"EKF_DEVSYNC": "1"}, {"EKF_SERIAL": "1"}):
+        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        e = pyekf.EKF(n_landmarks=80, n_filters=F)
+        cnt, ids, act, rel, od = (np.ascontiguousarray(a[:8]) for a in full)
+        e.replay(cnt, rel, od, ids=ids, actions=act)
+        for f in range(F):
+            e.posterior(f)
+        g = _to_gpu(tuple(np.ascontiguousarray(a[8:]) for a in full))
+        e.replay_device(g[0], g[3], g[4], g[1], g[2])
+        res.append(([e.state(f) for f in range(F)], [e.map_odom(f) for f in range(F)],
+                    [e.status(f) for f in range(F)]))
+        e.close()
+    (sa, ta, fa), (sb, tb, fb) = res
+    assert fa == fb == [0] * F
+    for (xa, Sa, ca), (xb, Sb, cb) in zip(sa, sb):
+        assert ca == cb
+        np.testing.assert_array_equal(xa, xb)
+        np.testing.assert_array_equal(Sa, Sb)
+    np.testing.assert_array_equal(np.stack(ta), np.stack(tb))
 
 
 def test_device_replay_fp32_n1024():

@@ -26,7 +26,7 @@ SWARM_TOL = 3e-8
 
 
 def _env(monkeypatch, resident):
-    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_ROWS"):
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("EKF_RESIDENT", "1" if resident else "0")
 

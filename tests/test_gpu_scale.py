@@ -211,33 +211,6 @@ def test_n1024_fp32_staged_rebuild_bit_identical(n1024, devsync, monkeypatch):
     np.testing.assert_array_equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize("dtype", [pyekf.EKF_F32, pyekf.EKF_F64], ids=["f32", "f64"])
-def test_n1024_builder_bit_identical(n1024, dtype, monkeypatch):
-    """The block builder (EKF_BUILD=1: k_chain's second workgroup per filter, EKF_SCHED_BUILDER)
-    rebuilds each next chunk's block during the corrections from the staged operands and the
-    chain's published Z / Y: 16 circle messages bit-identical to the prologue's own rebuild (the
-    default) and to the events schedule's gather, LDS poisoned."""
-    sc, odom, ws = n1024
-    w = sc.n_warm
-    out = []
-    for env, want in (({"EKF_DEVSYNC": "1", "EKF_BUILD": "1"}, True), ({"EKF_DEVSYNC": "1"}, False),
-                      ({"EKF_DEVSYNC": "0", "EKF_STAGE": "0"}, False)):
-        for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE", "EKF_BUILD", "EKF_ROWS"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        pyekf.poison_lds()
-        e = pyekf.EKF(n_landmarks=1024, dtype=dtype)
-        assert bool(e.schedule & pyekf.EKF_SCHED_BUILDER) == want, env
-        x, S, tmo, cnt = ws
-        e.set_state(x, S, tmo=tmo, counter=cnt)
-        _replay(e, slice(w, w + 16), sc, odom)
-        out.append(e.state())
-        assert e.status() == 0
-        e.close()
-    for o in out[1:]:
-        np.testing.assert_array_equal(o[0], out[0][0])
-        np.testing.assert_array_equal(o[1], out[0][1])
 
 
 @pytest.mark.parametrize("dtype", [pyekf.EKF_F32, pyekf.EKF_F64], ids=["f32", "f64"])

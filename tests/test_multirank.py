@@ -122,6 +122,9 @@ def test_bench_run_gloo_world2():
     res, poses = out[0]
     assert out[1][0] is None  # only rank 0 reports
     assert res["n_gpus"] == 2 and res["config"]["filters_total"] == 6
+    di = res["config"]["distributed"]  # the line records what the process group saw
+    assert di["world_size"] == 2 and di["backend"] == "gloo"
+    assert [r["rank"] for r in di["ranks"]] == [0, 1] and di["ranks"][0]["pid"] != di["ranks"][1]["pid"]
     assert res["config"]["landmarks_initialised_min"] == 24  # the survey sighted every landmark
     assert res["value"] > 0 and res["gathered_poses"]["filters"] == 6
     assert res["parity"]["pose_rmse_m"] == 0.0
