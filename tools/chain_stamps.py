@@ -67,3 +67,14 @@ print(f"N={N} {DT}, chunk {-1 - int(os.environ.get('WHICH', '1'))} of {T} messag
       f"the chunk's stamp 0); chunk starts of the ring, relative: {sorted(ring[:, 0] - ring[:, 0].min())}")
 for k in (1, 21, 3, 7, 5, 6, 2, 12, 16, 40):
     print(f"{names[k]:24s} {s[k] - t0:8d}")
+m = int(sc.count[w + T - 1 - int(os.environ.get("WHICH", "1"))])
+steps = [int(s[64 + 8 * c] - t0) for c in range(m)]
+print("step starts:", steps)
+print("mean step:", (steps[-1] - steps[0]) / max(m - 1, 1))
+for c in (0, 1, m // 2, m - 2):
+    b = 64 + 8 * c
+    d = [s[b + k + 1] - s[b + k] for k in range(6)]
+    print(f"step {c}: start {d[0]}  S,inv,nu {d[1]}  pdone wait+Bx reads {d[2]}  K,M,x,publish {d[3]}"
+          f"  geometry(c+1)+cross update {s[b + 6] - s[b + 4]}  -> next {s[b + 8] - s[b + 6]}")
+    print(f"   wave3: pub seen at {s[192 + 2 * c] - s[b]}, pdone at {s[193 + 2 * c] - s[b]} "
+          f"(wave0 publish at {s[b + 4] - s[b]}, next-step pdone wait at {s[b + 8 + 2] - s[b]})")
