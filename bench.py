@@ -56,12 +56,21 @@ WORKLOADS = {
                                               "N=1024 slots, 960 mapped landmarks, fp32"),
     "n1024_fp64_assoc": (1024, "f64", 1, 16, "configs[2] with unknown association (sensor_cb): "
                                               "N=1024 slots, 960 mapped landmarks, fp64"),
+    # the Joseph-form covariance update (BASELINE.json north_star, ekf_set_joseph): chunks of ≤ 8
+    # markers, two Σ passes per 16-marker message, each of rank 2 + 4m
+    "n1024_fp32_joseph": (1024, "f32", 1, 16, "configs[2] with the Joseph-form Sigma update "
+                                               "(north_star): N=1024, 1 filter, fp32"),
 }
+JOSEPH_CHUNK = 8  # markers per Joseph-form chunk (kMaxJoseph, ekf_device.hpp)
 ASSOC_FREE_SLOTS = 64  # association workloads map N − 64 landmarks (room for new ones)
 
 
 def is_assoc(workload):
     return workload.endswith("_assoc")
+
+
+def is_joseph(workload):
+    return workload.endswith("_joseph")
 
 
 def parse(argv=None):
@@ -455,6 +464,9 @@ def run(args, rank, world, local, backend=None):
     n_warm, counts, ids, act, rel = sw.n_warm, sw.count, sw.ids, sw.actions, sw.rel
     t_gen = time.perf_counter() - t_gen
     ekf = be.EKF(n_landmarks=N, n_filters=F, dtype=dtype, device=local)
+    joseph = is_joseph(args.workload)
+    if joseph and ekf.set_joseph(True) != 0:
+        raise SystemExit("ekf_set_joseph failed")
     sim = None
     if inputs == "device":
         import pyekf
@@ -604,8 +616,11 @@ def run(args, rank, world, local, backend=None):
         value = total_corr / elapsed
         wsz = 4 if dt == "f32" else 8
         n = 3 + 2 * N
-        # the rank-(2+2m) update's useful flops (fp64: the upper triangle, the symmetric pass)
-        mfma_flops = 2.0 * (2 + 2 * m) * (n * n if wsz == 4 else n * (n + 1) / 2) * F
+        # the rank-(2+2m) update's useful flops (fp64: the upper triangle, the symmetric pass);
+        # Joseph: rank 2 + 4·8 per pass, ⌈m/8⌉ passes per message
+        rank_k = 2 + 4 * min(m, JOSEPH_CHUNK) if joseph else 2 + 2 * m
+        passes = -(-m // JOSEPH_CHUNK) if joseph else 1
+        mfma_flops = 2.0 * rank_k * (n * n if wsz == 4 else n * (n + 1) / 2) * F
         result = {
             "metric": "EKF correction steps/sec at N landmarks; pose RMSE vs reference",
             "value": value,
@@ -652,18 +667,21 @@ def run(args, rank, world, local, backend=None):
                          "achieved_tflops": mfma_flops / avg_sig_s / 1e12 if n_sig else 0.0,
                          "peak_tflops": MFMA_PEAK_TF[dt],
                          "frac": mfma_flops / avg_sig_s / 1e12 / MFMA_PEAK_TF[dt] if n_sig else 0.0,
-                         "formula": (f"2*(2+2m)*n^2*F = 2*{2 + 2 * m}*{n}^2*{F}" if wsz == 4 else
-                                     f"2*(2+2m)*n(n+1)/2*F = 2*{2 + 2 * m}*{n}*{n + 1}/2*{F}"),
+                         "formula": (f"2*k*n^2*F = 2*{rank_k}*{n}^2*{F}" if wsz == 4 else
+                                     f"2*k*n(n+1)/2*F = 2*{rank_k}*{n}*{n + 1}/2*{F}") +
+                                    f", k = {'2+4*8 (Joseph chunk)' if joseph else '2+2m'}",
                          "pmc": traffic.get("mfma_busy") if traffic else traffic_err},
                 "chain_kernel_avg_us": ms_gain / max(n_gain, 1) * 1e3,
                 "factor_kernel_avg_us": ms_fac / max(n_fac, 1) * 1e3,
                 # the whole step against the rank-2m ceiling: one Σ pass per
-                # message is the algorithmic minimum, sigma_pass_bytes per step
+                # message is the algorithmic minimum, sigma_pass_bytes per step (Joseph: one
+                # pass per chunk of 8, two per message)
                 "end_to_end": {
-                    "bytes_per_step": bytes_per_launch,
-                    "achieved": bytes_per_launch / (elapsed / K) / 1e9,
-                    "frac": bytes_per_launch / (elapsed / K) / 1e9 / HBM_PEAK_GBS,
-                    "ceiling_corrections_per_s": (HBM_PEAK_GBS * 1e9 / bytes_per_launch * (
+                    "bytes_per_step": passes * bytes_per_launch,
+                    "passes_per_step": passes,
+                    "achieved": passes * bytes_per_launch / (elapsed / K) / 1e9,
+                    "frac": passes * bytes_per_launch / (elapsed / K) / 1e9 / HBM_PEAK_GBS,
+                    "ceiling_corrections_per_s": (HBM_PEAK_GBS * 1e9 / (passes * bytes_per_launch) * (
                         total_corr / world / K)) if bytes_per_launch else None,
                 },
             },
@@ -744,6 +762,8 @@ def ekf_first_poses(args, be, N, dtype, ws, counts, ids, act, rel, odom, t0s, de
     x, S, tmo, cnt = ws
     e = be.EKF(n_landmarks=N, dtype=dtype, device=device)
     e.set_state(x, S, tmo=tmo, counter=cnt)
+    if is_joseph(args.workload):
+        e.set_joseph(True)
     sl = slice(t0s, t0s + k)
     un = is_assoc(args.workload)
     if gpu_in is not None:
@@ -802,7 +822,8 @@ def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
         return ncorr, nmsg, time.perf_counter() - t0
 
     # numpy / OpenBLAS literal (the DenseEKF members of slam.cpp:657-676 set to the warm state)
-    d = ekf_numpy.DenseEKF(n_landmarks=N)
+    jos = is_joseph(args.workload)
+    d = ekf_numpy.DenseEKF(n_landmarks=N, joseph=jos)
     d.state, d.sigma, d.counter = x.copy(), S.copy(), int(cnt)
     d.t_map_odom, d.prev = tuple(tmo), tuple(x[:3])
 
@@ -817,7 +838,7 @@ def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
     nb, kb, tb = timed(np_step, 1, 10.0)
     out = {}
     for literal, k_min, budget in ((True, 1, 10.0), (False, args.steps, 0.0)):
-        ref = orc.OracleEKF(n_landmarks=N, literal=literal)
+        ref = orc.OracleEKF(n_landmarks=N, literal=literal, joseph=jos)
         ref.set(x, S, tmo, x[:3], cnt)
 
         def c_step(t, c, ref=ref):
@@ -831,7 +852,8 @@ def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
     sc_, sk, st = out[False]
     return {"value": nb / tb, "unit": "corrections/s", "cores": _blas_threads() or cores,
             "kind": "port",
-            "sample": f"literal dense restatement of slam.cpp{' sensor_cb' if un else ''} "
+            "sample": f"literal dense restatement of slam.cpp{' sensor_cb' if un else ''}"
+                      f"{' in Joseph form' if jos else ''} "
                       f"(numpy + OpenBLAS dgemm, fp64, "
                       f"oracle/ekf_numpy.py): {kb} message(s) = {nb} corrections in {tb:.2f} s",
             "c_literal": {"value": lc / lt, "cores": cores,
@@ -845,7 +867,7 @@ def cpu_baseline(args, N, ws, counts, ids, act, rel, odom, t0s):
 def parity(args, N, gpu_poses, ws, counts, ids, act, rel, odom, t0s):
     orc = _oracle()
     x, S, tmo, cnt = ws
-    ref = orc.OracleEKF(n_landmarks=N)
+    ref = orc.OracleEKF(n_landmarks=N, joseph=is_joseph(args.workload))
     ref.set(x, S, tmo, x[:3], cnt)
     k = len(gpu_poses)
     ref_p = np.zeros((k, 3))
@@ -861,7 +883,8 @@ def parity(args, N, gpu_poses, ws, counts, ids, act, rel, odom, t0s):
     dth = np.arctan2(np.sin(d[:, 0]), np.cos(d[:, 0]))
     return {"pose_rmse_m": float(np.sqrt(np.mean(d[:, 1] ** 2 + d[:, 2] ** 2))),
             "heading_rmse_rad": float(np.sqrt(np.mean(dth ** 2))),
-            "messages": k, "vs": "oracle structured fp64 (CPU), filter 0, same warm state"}
+            "messages": k, "vs": "oracle structured fp64 (CPU), filter 0, same warm state" + (
+                ", Joseph mode" if is_joseph(args.workload) else "")}
 
 
 if __name__ == "__main__":

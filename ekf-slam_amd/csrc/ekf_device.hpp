@@ -17,6 +17,8 @@ constexpr int kMaxU = 3 + 2 * kMaxChunk;         // touched rows/cols of one chu
 constexpr int kMaxKW = ((2 + 2 * kMaxChunk + 3) / 4) * 4;  // rank of the fused update, padded to 4
 constexpr int kMaxAssoc = 64;                    // association slots per filter per upload
 constexpr int kZC = 2 * kMaxChunk;               // correction columns of Z / rows of Y
+constexpr int kMaxJoseph = kMaxChunk / 2;        // markers of a Joseph-form chunk: its row map Z
+                                                 // holds K's and V's columns (4 per marker)
 
 // Device epochs (unsigned words of the handle's sync buffer, each polled word on its own line):
 constexpr int kSyncSigma = 0;    // epoch (seq + 1) of the last complete Σ pass (k_sigma_epoch)
@@ -32,8 +34,8 @@ constexpr int kNoInit = 4;   // association path: no first-sighting init in the 
 constexpr int kActive = 8;   // filter takes part in this launch
 constexpr int kLook = 16;    // Σ_in not materialised yet: rebuild the chain's block from the
                              // previous chunk's Σ_in (other buffer) and ChunkRec
-constexpr int kJoseph = 128; // Joseph-form Σ update (ekf_set_joseph): one marker per chunk, the
-                             // factor rank 2 + 4 (K·M and (ΣHᵀ − K·S)·Kᵀ, see k_chain)
+constexpr int kJoseph = 128; // Joseph-form Σ update (ekf_set_joseph): ≤ kMaxJoseph markers per
+                             // chunk, the factor rank 2 + 4m (K·M and (ΣHᵀ − K·S)·Kᵀ, see k_chain)
 constexpr int kStageOut = 256;  // behind this chunk's Σ pass (k_patch_stage): gather the rebuild
                                 // operands of the filter's chunk after next (stg_*) into StageRec
 constexpr int kStageIn = 512;   // kLook chain: read its rebuild operands from StageRec (contiguous)
@@ -71,6 +73,8 @@ struct alignas(16) FilterCtl {
 // What the chain kernel (the sequential part of a chunk) hands to the factor kernel: with
 // r(i) = Σ_pred[i][U] and c(j) = Σ_pred[U][j], K_c[i] = r(i)·Z[:, 2c..2c+1] and
 // M_c[:, j] = Y[2c..2c+1, :]·c(j); x_i += r(i)·Zx for rows outside U, xU for rows in U.
+// A Joseph chunk (kJoseph, m ≤ kMaxJoseph) adds V_c[i] = (Σ_c·Hᵀ − K_c·S_c)[i] = r(i)·Z[:, 2m+2c..]
+// (the row factor of the V_c·K_cᵀ term; its column factor is K_c itself).
 struct alignas(16) ChunkRec {
   int m, nu, flags, pad;
   int u[kMaxU + 1];

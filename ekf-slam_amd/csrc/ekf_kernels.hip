@@ -147,8 +147,12 @@ struct ChainShared {
   double nu[kMaxChunk][2];
   double Hs[kMaxChunk][2][5];    // H_c over pA (published for waves 1–2)
   double Sis[kMaxChunk][4];      // S_c⁻¹
-  double GU[kMaxU][2];           // Joseph (one marker per chunk): (Σ·Hᵀ)[U] of the step
-  double Ss[4];                  // Joseph: S of the step
+  // Joseph chunks (m ≤ kMaxJoseph): V_c = (Σ_c·Hᵀ − K_c·S_c)[U] and S_c per step (wave 0), wave 1's
+  // C'_k = K_k[pA_c]ᵀ·Hᵀ and wave 2's D'_k = H·V_k[pA_c]
+  double VU[kMaxJoseph][kMaxU][2];
+  double Ss[kMaxJoseph][4];
+  double Cv[kMaxJoseph][4];
+  double Dv[kMaxJoseph][4];
   // kLook: the previous chunk's record and the blocks rebuilt from it
   struct {
     int u[kMaxU];
@@ -176,6 +180,7 @@ struct ChainShared {
   int pub;    // steps whose K, M, H, S⁻¹ wave 0 has published
   int pdone;  // steps wave 3 has applied outside the cross
   int any_init;  // a correction of this chunk initialised its landmark (slam.cpp:213-216)
+  int zdone;     // Joseph: steps whose Z_c, Zv_c wave 1 has stored (wave 2 reads them)
 };
 
 
@@ -220,8 +225,12 @@ __device__ __forceinline__ void lds_wait_ge3(const __attribute__((address_space(
     __builtin_amdgcn_s_sleep(1);
 }
 
+// J: a Joseph chunk (m ≤ kMaxJoseph). Every step then also subtracts V_c·K_cᵀ, V_c = Σ_c·Hᵀ − K_c·S_c
+// (slam.cpp:264-265's update as (I − KH)Σ(I − KH)ᵀ + K·R·Kᵀ expanded), always after the K_c·M_c term
+// — the order wave 3 uses, so an entry both waves compute has the same bits.
+template <bool J>
 __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int m, int nu,
-                                         bool joseph, double r_noise, unsigned seq) {
+                                         double r_noise, unsigned seq) {
   LdsChain& sh = *shp;
   LdsDesc& d = *dp;
   const int lane = threadIdx.x & 63;
@@ -244,7 +253,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
   }
   // Look-ahead operands of the next marker's cross (see the step): rn = Σ[ℓ, nx..nx+1] and
   // qn = Σ[nx..nx+1, ℓ] one step old, and the previous step's K (kp) and M (mp) of this lane.
-  double rn[2], qn[2], kp0 = 0.0, kp1 = 0.0, mp0 = 0.0, mp1 = 0.0;
+  double rn[2], qn[2], kp0 = 0.0, kp1 = 0.0, mp0 = 0.0, mp1 = 0.0, vp0 = 0.0, vp1 = 0.0;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = min(5 + j, kMaxU - 1);
@@ -362,6 +371,15 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       xr[4] = rank2_sub(rn[1], kp0, kp1, mq2x, mq2y);
       xq[3] = rank2_sub(qn[0], kqx, kqy, mp0, mp1);
       xq[4] = rank2_sub(qn[1], kq2x, kq2y, mp0, mp1);
+      if (J) {  // − V_{c−1}·K_{c−1}ᵀ (step 0: vp = kp = 0)
+        const int cj = min(cp, kMaxJoseph - 1);
+        const double vqx = sh.VU[cj][l0][0], vqy = sh.VU[cj][l0][1];
+        const double vq2x = sh.VU[cj][l0 + 1][0], vq2y = sh.VU[cj][l0 + 1][1];
+        xr[3] = rank2_sub(xr[3], vp0, vp1, kqx, kqy);
+        xr[4] = rank2_sub(xr[4], vp0, vp1, kq2x, kq2y);
+        xq[3] = rank2_sub(xq[3], vqx, vqy, kp0, kp1);
+        xq[4] = rank2_sub(xq[4], vq2x, vq2y, kp0, kp1);
+      }
     }
     EKF_STAMP(66 + 8 * c);
     // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's
@@ -383,6 +401,9 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
     EKF_STAMP(67 + 8 * c);
     const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
     const double K1 = ka * Si[1] + kb * Si[3];
+    // Joseph: V = Σ·Hᵀ − K·S of this lane's row (zero in exact arithmetic; the form's rounding)
+    const double V0 = J ? ka - (K0 * Sm_keep[0] + K1 * Sm_keep[2]) : 0.0;
+    const double V1 = J ? kb - (K0 * Sm_keep[1] + K1 * Sm_keep[3]) : 0.0;
     {
       double xt = xl;
       if (init) {
@@ -404,12 +425,13 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       kd[1] = in ? K1 : 0.0;
       md[0] = in ? mm0 : 0.0;
       md[1] = in ? mm1 : 0.0;
-      if (joseph) {  // G = Σ·Hᵀ and S for the (ΣHᵀ − K·S)·Kᵀ term (chunks of one marker)
-        ldsd* gd = st ? &sh.GU[lane][0] : &sh.junk2[lane][0];
-        gd[0] = in ? ka : 0.0;
-        gd[1] = in ? kb : 0.0;
+      if (J) {  // V and S of the step, for waves 1–3 and the fp32 block patch
+        const int cj = min(c, kMaxJoseph - 1);
+        ldsd* vd = st ? &sh.VU[cj][lane][0] : &sh.junk2[lane][0];
+        vd[0] = in ? V0 : 0.0;
+        vd[1] = in ? V1 : 0.0;
         if (lane == 0)
-          for (int k = 0; k < 4; ++k) sh.Ss[k] = sk ? 0.0 : Sm_keep[k];
+          for (int k = 0; k < 4; ++k) sh.Ss[cj][k] = sk ? 0.0 : Sm_keep[k];
       }
     }
     if (lane == 0) {
@@ -428,7 +450,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
     if (more) {
       // K and M of the five Bx rows / columns: broadcast LDS reads of what this step stored
       // above (issued before geometry(c + 1), so its latency hides; ds_read_b128 each)
-      double kx0[5], kx1[5], mx0[5], mx1[5];
+      double kx0[5], kx1[5], mx0[5], mx1[5], vx0[5], vx1[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         const int l = k < 3 ? k : nx + k - 3;
@@ -438,6 +460,11 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
         kx1[k] = kky;
         mx0[k] = mkx;
         mx1[k] = mky;
+        if (J) {
+          const int cj = min(c, kMaxJoseph - 1);
+          vx0[k] = sh.VU[cj][l][0];
+          vx1[k] = sh.VU[cj][l][1];
+        }
       }
       geometry(c + 1);
       // wave 3's step c−1 writes outside this step's cross must land before this cross update
@@ -449,6 +476,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       for (int k = 0; k < 5; ++k) {
         const int col = k < 3 ? k : nx + k - 3;
         pk[k] = rank2_sub(xr[k], K0, K1, mx0[k], mx1[k]);
+        if (J) pk[k] = rank2_sub(pk[k], V0, V1, kx0[k], kx1[k]);
         *(lane < nu ? &sh.P[pb][lane][col] : &sh.junk[0][lane]) = pk[k];
       }
       // Bx rows × every other column (the block is kept whole so that the chunk's final Σ[U,U]
@@ -457,7 +485,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
 #pragma unroll
       for (int k = 0; k < 5; ++k) {
         const int row = k < 3 ? k : nx + k - 3;
-        const double v = rank2_sub(xq[k], kx0[k], kx1[k], mm0, mm1);
+        double v = rank2_sub(xq[k], kx0[k], kx1[k], mm0, mm1);
+        if (J) v = rank2_sub(v, vx0[k], vx1[k], K0, K1);
         pm[k] = v;
         *(later ? &sh.P[pb][row][lane] : &sh.junk[0][lane]) = v;
       }
@@ -466,6 +495,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       kp1 = K1;
       mp0 = mm0;
       mp1 = mm1;
+      vp0 = V0;
+      vp1 = V1;
     }
     EKF_STAMP(70 + 8 * c);
   }
@@ -597,6 +628,9 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
   T* mc = A.mcat + f * A.km_stride;
   const bool first = (d.flags & kFirst) != 0;
   const bool joseph = (d.flags & kJoseph) != 0;
+  // Joseph: Mcat rows 2 + 2m .. 2 + 4m − 1 hold K_c (the V_c·K_cᵀ term's column factor), written
+  // by the row waves; the column waves leave them alone
+  const int jk0 = joseph ? 2 * d.m : kZC, jk1 = joseph ? 4 * d.m : kZC;
   const int nu = sh.nu;
   const double* xfin = sh.xU;
   // ---- phase B: Kcat = R_pred·Z, Mcat = Y·C_pred on f64 MFMA, 16 rows (or columns) per wave ----
@@ -638,9 +672,8 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kr = ks + 4 * r;
-        if (!(joseph && (kr == 2 || kr == 3)))  // (Joseph: the row waves write K there)
-          mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
-        mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
+        if (kr < jk0 || kr >= jk1) mc[(2 + kr) * ldk + j] = static_cast<T>(acc0[r]);
+        if (16 + kr < jk0 || 16 + kr >= jk1) mc[(18 + kr) * ldk + j] = static_cast<T>(acc1[r]);
       }
     }
   };
@@ -713,7 +746,8 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
         kc[(2 + c) * ldk + i] = static_cast<T>(acc0[r]);
         kc[(18 + c) * ldk + i] = static_cast<T>(acc1[r]);
         // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
-        if (joseph && c < 2) mc[(4 + c) * ldk + i] = static_cast<T>(acc0[r]);
+        // (2m ≤ 16: acc0 holds every K_c)
+        if (joseph && c < jk0) mc[(2 + jk0 + c) * ldk + i] = static_cast<T>(acc0[r]);
       }
     }
     if (merged) columns(i, raw, r0t);
@@ -815,9 +849,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   const double* xin = A.x[d.parity] + f * A.x_stride;
   const int m = d.m;
   const bool first = (d.flags & kFirst) != 0;
-  // Joseph (one marker per chunk): Σ ← Σ − K·M − (ΣHᵀ − K·S)·Kᵀ, i.e. (I−KH)Σ(I−KH)ᵀ + K·R·Kᵀ
-  // expanded (slam.cpp:264-265's update in Joseph form). Row factor V = G − K·S beside K, column
-  // factor Kᵀ beside M: the record's Z carries V in columns 2..3, the chain's block gets the term.
+  // Joseph (≤ kMaxJoseph markers per chunk): Σ ← Σ − K_c·M_c − (Σ_cHᵀ − K_c·S_c)·K_cᵀ per step,
+  // i.e. (I−KH)Σ(I−KH)ᵀ + K·R·Kᵀ expanded (slam.cpp:264-265's update in Joseph form). Row factor
+  // V_c = G_c − K_c·S_c beside K_c, column factor K_cᵀ beside M_c: the record's Z carries V_c's
+  // row map in columns 2m + 2c.., the chain's block gets the term step by step.
   const bool joseph = (d.flags & kJoseph) != 0;
 
   // kLook: this chunk's Σ_in is still being written by the previous chunk's Σ pass. Rebuild what
@@ -1015,19 +1050,20 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     EKF_STAMP(7);
     __syncthreads();
     EKF_STAMP(5);
-    // a Joseph chunk before: its V'·K'ᵀ term as rank 2..3 (K' columns 2..3 are V' = R·Z'[:, 2..3];
-    // M' rows 2..3 become K'ᵀ, the column factor)
+    // a Joseph chunk before: its V'·K'ᵀ terms as rank 2m'..4m'−1 (K' columns 2m'.. are
+    // V' = R·Z'[:, 2m'..]; M' rows 2m'.. become K'ᵀ, the column factor)
     const bool pj = sh.pv.joseph != 0;
+    const int pm2 = 2 * min(sh.pv.m, kMaxJoseph);
     if (pj) {
-      for (int e = tid; e < 2 * kW; e += blockDim.x) {
+      for (int e = tid; e < pm2 * kW; e += blockDim.x) {
         const int k = e / kW, b = e - k * kW;
-        sh.pv.M[2 + k][b] = b < kMaxU ? sh.pv.K[b][k] : 0.0;
+        sh.pv.M[pm2 + k][b] = b < kMaxU ? sh.pv.K[b][k] : 0.0;
       }
       __syncthreads();
     }
     // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
-    // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4)
-    const int zc = pj ? 4 : 2 * sh.pv.m;
+    // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4m')
+    const int zc = pj ? 2 * pm2 : 2 * sh.pv.m;
     for (int tt = wv; tt < 9; tt += 4) {
       const int ti = tt / 3, tj = tt % 3;
       const int col = 16 * tj + i16, ar = min(16 * ti + i16, kMaxU - 1), cc = min(col, kMaxU - 1);
@@ -1166,6 +1202,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   if (tid == 0) {
     sh.pub = 0;
     sh.pdone = 0;
+    sh.zdone = 0;
     sh.any_init = 0;
   }
   if (pending) drain_stores();
@@ -1175,36 +1212,53 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     pending = 0;
   }
   if (wave == 0) {
-    chain_wave0((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, joseph, A.r, seq);
+    if (joseph)
+      chain_wave0<true>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq);
+    else
+      chain_wave0<false>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq);
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
     // lane → column 3+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
     const int hb = lane & 31, hr = lane >> 5;
     const int b = min(3 + hb, kMaxU - 1);
-    for (int c = 0; c + 1 < m; ++c) {
-      lds_wait_ge(&sh.pub, c + 1);
-      EKF_STAMPT(192 + 2 * c, 192);
-      const int nx = 5 + 2 * c;
-      const bool colok = 3 + hb < nu && b != nx && b != nx + 1;
-      const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
-      double pv[16], k0[16], k1[16];
+    auto rest = [&](auto jc) {  // (Joseph: V_c[a]·K_c[b] after the K·M term, as wave 0 does)
+      constexpr bool J = decltype(jc)::value;
+      for (int c = 0; c + 1 < m; ++c) {
+        lds_wait_ge(&sh.pub, c + 1);
+        EKF_STAMPT(192 + 2 * c, 192);
+        const int nx = 5 + 2 * c, cj = min(c, kMaxJoseph - 1);
+        const bool colok = 3 + hb < nu && b != nx && b != nx + 1;
+        const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
+        const double kb0 = J ? sh.KU[c][b][0] : 0.0, kb1 = J ? sh.KU[c][b][1] : 0.0;
+        double pv[16], k0[16], k1[16], w0[16], w1[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
-        const int a = min(3 + hr + 2 * i, kMaxU - 1);
-        pv[i] = P[a][b];
-        k0[i] = sh.KU[c][a][0];
-        k1[i] = sh.KU[c][a][1];
-      }
-      // every lane stores every row (masked-off entries to its junk slot): no divergent branches,
-      // so the reads above are waited for once, not once per predicated store
+        for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
+          const int a = min(3 + hr + 2 * i, kMaxU - 1);
+          pv[i] = P[a][b];
+          k0[i] = sh.KU[c][a][0];
+          k1[i] = sh.KU[c][a][1];
+          if (J) {
+            w0[i] = sh.VU[cj][a][0];
+            w1[i] = sh.VU[cj][a][1];
+          }
+        }
+        // every lane stores every row (masked-off entries to its junk slot): no divergent
+        // branches, so the reads above are waited for once, not once per predicated store
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int a = 3 + hr + 2 * i;
-        const bool ok = colok && a < nu && a != nx && a != nx + 1;
-        *(ok ? &P[a][b] : &sh.junk[3][lane]) = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
+        for (int i = 0; i < 16; ++i) {
+          const int a = 3 + hr + 2 * i;
+          const bool ok = colok && a < nu && a != nx && a != nx + 1;
+          double v = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
+          if (J) v = rank2_sub(v, w0[i], w1[i], kb0, kb1);
+          *(ok ? &P[a][b] : &sh.junk[3][lane]) = v;
+        }
+        lds_publish(&sh.pdone, c + 1);
+        EKF_STAMPT(193 + 2 * c, 192);
       }
-      lds_publish(&sh.pdone, c + 1);
-      EKF_STAMPT(193 + 2 * c, 192);
-    }
+    };
+    if (joseph)
+      rest(std::true_type{});
+    else
+      rest(std::false_type{});
   } else if (wave == 1) {  // Z_c: K_c[i] = r_0(i)·Z_c for every row i
     // Σ_c[i, pA_c] = r_0(i)·(E_c − Σ_{k<c} Z_k·M_k[:, pA_c]) (E_c selects the positions pA_c), so
     // Z_c = E_c·G − Σ_{k<c} Z_k·C_k with G = Hᵀ·S⁻¹ (5×2) and C_k = M_k[:, pA_c]·G (2×2): lane k
@@ -1217,8 +1271,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
     constexpr int oZ = static_cast<int>(offsetof(ChunkRec, Z));
     {  // columns ≥ 2m of the record's Z are zero (the factor kernel and a rebuilding chain read
-       // them); Joseph keeps columns 2..3 for V
-      const int z0c = joseph ? 2 * m + 2 : 2 * m;
+       // them); Joseph keeps columns 2m..4m for V
+      const int z0c = joseph ? 4 * m : 2 * m;
       const int zw = kZC - z0c;
       for (int e = lane; e < kMaxU * zw; e += 64) {
         const int b = e / zw, k = z0c + (e - b * zw);
@@ -1227,6 +1281,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
     const int li = lane < kMaxU ? lane : kMaxU - 1;
     double zxa = 0.0;  // Σ_c Z_c ν_c of row `lane`, accumulated as the Z_c come (the record's Zx)
+    if (!joseph) {
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1269,13 +1324,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: LDS keeps its order)
       {  // row li of Z_c
         const int pos = li < 3 ? li : (li == pj ? 3 : (li == pj + 1 ? 4 : -1));
-        double z0 = 0.0, z1 = 0.0, W0 = 0.0, W1 = 0.0;
+        double z0 = 0.0, z1 = 0.0;
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
           z0 = pos == a ? G0[a] : z0;
           z1 = pos == a ? G1[a] : z1;
-          W0 = pos == a ? H0[a] : W0;
-          W1 = pos == a ? H1[a] : W1;
         }
         for (int k = 0; k < c; ++k) {
           const double zk0 = sh.Z[li][2 * k], zk1 = sh.Z[li][2 * k + 1];
@@ -1291,16 +1344,102 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           sh.Z[lane][2 * c] = Z0;
           sh.Z[lane][2 * c + 1] = Z1;
           st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
-          if (joseph) {  // V = W − Z·S with W = E·Hᵀ (c = 0): r₀(i)·V = (ΣHᵀ − K·S)[i]
-            const double V0 = in ? W0 - (Z0 * sh.Ss[0] + Z1 * sh.Ss[2]) : 0.0;
-            const double V1 = in ? W1 - (Z0 * sh.Ss[1] + Z1 * sh.Ss[3]) : 0.0;
-            sh.Z[lane][2] = V0;
-            sh.Z[lane][3] = V1;
-            st_wt2(rr, oZ + 8 * (kZC * lane + 2), V0, V1);
-          }
         }
       }
       EKF_STAMPT(320 + c, 64);
+    }
+    } else {
+    // Joseph: Σ_c[i, U] = r_0(i)·Φ_c with Φ_{c+1} = Φ_c − Z_c·M_c[:, U] − Zv_c·K_c[U]ᵀ, so
+    // W_c = Φ_c[:, pA]·Hᵀ = E_c·Hᵀ − Σ_{k<c} (Z_k·C_k + Zv_k·C'_k), C_k = M_k[:, pA_c]·Hᵀ and
+    // C'_k = K_k[pA_c]ᵀ·Hᵀ (2×2 each); then Z_c = W_c·S_c⁻¹ (K_c = G_c·S⁻¹, G_c[i] = r_0(i)·W_c) and
+    // Zv_c = W_c − Z_c·S_c (V_c = G_c − K_c·S_c). One marker: Z_0 = E·Hᵀ·S⁻¹, as the simple form.
+    const int cols = 2 * min(m, kMaxJoseph);
+    for (int c = 0; c < m && c < kMaxJoseph; ++c) {
+      lds_wait_ge(&sh.pub, c + 1);
+      const int pj = 3 + 2 * c;
+      double H0[5], H1[5], Si[4], Sc[4];
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        H0[a] = sh.Hs[c][0][a];
+        H1[a] = sh.Hs[c][1][a];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        Si[k] = sh.Sis[c][k];
+        Sc[k] = sh.Ss[c][k];
+      }
+      {  // lane k < c: C_k and C'_k
+        const int k = lane < c ? lane : 0;
+        double m0[5], m1[5], q0[5], q1[5];
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          const int pa = a < 3 ? a : pj + a - 3;
+          m0[a] = sh.MU[k][pa][0];
+          m1[a] = sh.MU[k][pa][1];
+          q0[a] = sh.KU[k][pa][0];
+          q1[a] = sh.KU[k][pa][1];
+        }
+        double c00 = 0.0, c01 = 0.0, c10 = 0.0, c11 = 0.0;
+        double e00 = 0.0, e01 = 0.0, e10 = 0.0, e11 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          c00 = fma(m0[a], H0[a], c00);
+          c01 = fma(m0[a], H1[a], c01);
+          c10 = fma(m1[a], H0[a], c10);
+          c11 = fma(m1[a], H1[a], c11);
+          e00 = fma(q0[a], H0[a], e00);
+          e01 = fma(q0[a], H1[a], e01);
+          e10 = fma(q1[a], H0[a], e10);
+          e11 = fma(q1[a], H1[a], e11);
+        }
+        double* cd = lane < c ? &sh.Cz[lane][0] : &sh.junk[1][0];
+        double* ed = lane < c ? &sh.Cv[lane][0] : &sh.junk[1][4];
+        cd[0] = c00;
+        cd[1] = c01;
+        cd[2] = c10;
+        cd[3] = c11;
+        ed[0] = e00;
+        ed[1] = e01;
+        ed[2] = e10;
+        ed[3] = e11;
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: LDS keeps its order)
+      {  // row li of W_c, then of Z_c and Zv_c
+        const int pos = li < 3 ? li : (li == pj ? 3 : (li == pj + 1 ? 4 : -1));
+        double w0 = 0.0, w1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          w0 = pos == a ? H0[a] : w0;
+          w1 = pos == a ? H1[a] : w1;
+        }
+        for (int k = 0; k < c; ++k) {
+          const double zk0 = sh.Z[li][2 * k], zk1 = sh.Z[li][2 * k + 1];
+          const double vk0 = sh.Z[li][cols + 2 * k], vk1 = sh.Z[li][cols + 2 * k + 1];
+          const double c00 = sh.Cz[k][0], c01 = sh.Cz[k][1], c10 = sh.Cz[k][2], c11 = sh.Cz[k][3];
+          const double e00 = sh.Cv[k][0], e01 = sh.Cv[k][1], e10 = sh.Cv[k][2], e11 = sh.Cv[k][3];
+          w0 = fma(-zk1, c10, fma(-zk0, c00, w0));
+          w1 = fma(-zk1, c11, fma(-zk0, c01, w1));
+          w0 = fma(-vk1, e10, fma(-vk0, e00, w0));
+          w1 = fma(-vk1, e11, fma(-vk0, e01, w1));
+        }
+        const bool in = lane < nu;
+        const double Z0 = in ? w0 * Si[0] + w1 * Si[2] : 0.0;
+        const double Z1 = in ? w0 * Si[1] + w1 * Si[3] : 0.0;
+        const double V0 = in ? w0 - (Z0 * Sc[0] + Z1 * Sc[2]) : 0.0;
+        const double V1 = in ? w1 - (Z0 * Sc[1] + Z1 * Sc[3]) : 0.0;
+        zxa += Z0 * sh.nu[c][0] + Z1 * sh.nu[c][1];
+        if (lane < kMaxU) {
+          sh.Z[lane][2 * c] = Z0;
+          sh.Z[lane][2 * c + 1] = Z1;
+          sh.Z[lane][cols + 2 * c] = V0;
+          sh.Z[lane][cols + 2 * c + 1] = V1;
+          st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
+          st_wt2(rr, oZ + 8 * (kZC * lane + cols + 2 * c), V0, V1);
+        }
+      }
+      lds_publish(&sh.zdone, c + 1);  // (wave 2 reads Z_c, Zv_c)
+      EKF_STAMPT(320 + c, 64);
+    }
     }
     if (lane < kMaxU) sh.Zx[lane] = zxa;
   } else {  // wave 2: Y_c: M_c[:, j] = Y_c·c_0(j) for every column j; Y_c to the record at once
@@ -1310,8 +1449,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     for (int e = lane; e < (kZC - 2 * m) * kMaxU; e += 64)  // rows ≥ 2m of the record's Y are zero
       st_wt(&(&rec->Y[2 * m][0])[e], 0.0);
     const int lj = lane < kMaxU ? lane : kMaxU - 1;
+    // Joseph: Σ_{c+1}[·, j] also loses V_c·K_c[j]ᵀ, and K_c[j] = r_0(j)·Z_c = Z_cᵀ·c_0(j) (Σ_pred is
+    // symmetric in exact arithmetic; fp64 Σ exactly): Y_c = H·E_cᵀ − Σ_{k<c} (D_k·Y_k + D'_k·Z_kᵀ),
+    // D'_k = H·V_k[pA_c], with wave 1's Z_k (flag zdone)
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
+      if (joseph && c > 0) lds_wait_ge(&sh.zdone, min(c, kMaxJoseph));
       const int pj = 3 + 2 * c;
       double H0[5], H1[5];
 #pragma unroll
@@ -1319,7 +1462,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         H0[a] = sh.Hs[c][0][a];
         H1[a] = sh.Hs[c][1][a];
       }
-      {  // lane k < c: D_k
+      {  // lane k < c: D_k (Joseph: and D'_k)
         const int k = lane < c ? lane : 0;
         double k0[5], k1[5];
 #pragma unroll
@@ -1341,6 +1484,29 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         dd[1] = d01;
         dd[2] = d10;
         dd[3] = d11;
+        if (joseph) {
+          const int kj = min(k, kMaxJoseph - 1);
+          double v0[5], v1[5];
+#pragma unroll
+          for (int a = 0; a < 5; ++a) {
+            const int pa = a < 3 ? a : pj + a - 3;
+            v0[a] = sh.VU[kj][pa][0];
+            v1[a] = sh.VU[kj][pa][1];
+          }
+          double e00 = 0.0, e01 = 0.0, e10 = 0.0, e11 = 0.0;
+#pragma unroll
+          for (int a = 0; a < 5; ++a) {
+            e00 = fma(H0[a], v0[a], e00);
+            e01 = fma(H0[a], v1[a], e01);
+            e10 = fma(H1[a], v0[a], e10);
+            e11 = fma(H1[a], v1[a], e11);
+          }
+          double* ed = lane < c ? &sh.Dv[kj][0] : &sh.junk[2][4];
+          ed[0] = e00;
+          ed[1] = e01;
+          ed[2] = e10;
+          ed[3] = e11;
+        }
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       {  // column lj of Y_c
@@ -1356,6 +1522,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           const double d00 = sh.Dy[k][0], d01 = sh.Dy[k][1], d10 = sh.Dy[k][2], d11 = sh.Dy[k][3];
           y0 = fma(-d01, yk1, fma(-d00, yk0, y0));
           y1 = fma(-d11, yk1, fma(-d10, yk0, y1));
+          if (joseph) {
+            const int kj = min(k, kMaxJoseph - 1);
+            const double zk0 = sh.Z[lj][2 * k], zk1 = sh.Z[lj][2 * k + 1];
+            const double e00 = sh.Dv[kj][0], e01 = sh.Dv[kj][1], e10 = sh.Dv[kj][2], e11 = sh.Dv[kj][3];
+            y0 = fma(-e01, zk1, fma(-e00, zk0, y0));
+            y1 = fma(-e11, zk1, fma(-e10, zk0, y1));
+          }
         }
         if (lane < kMaxU) {
           const bool in = lane < nu;
@@ -1384,11 +1557,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       double v = P[a][b];
       if (m > 0)
         v = rank2_sub(v, sh.KU[c][a][0], sh.KU[c][a][1], sh.MU[c][b][0], sh.MU[c][b][1]);
-      if (m > 0 && joseph) {  // − (G − K·S)[a]·K[b]ᵀ
-        const double k0 = sh.KU[c][a][0], k1 = sh.KU[c][a][1];
-        const double v0 = sh.GU[a][0] - (k0 * sh.Ss[0] + k1 * sh.Ss[2]);
-        const double v1 = sh.GU[a][1] - (k0 * sh.Ss[1] + k1 * sh.Ss[3]);
-        v = rank2_sub(v, v0, v1, sh.KU[c][b][0], sh.KU[c][b][1]);
+      if (m > 0 && joseph) {  // − V_c[a]·K_c[b]ᵀ
+        const int cj = min(c, kMaxJoseph - 1);
+        v = rank2_sub(v, sh.VU[cj][a][0], sh.VU[cj][a][1], sh.KU[c][b][0], sh.KU[c][b][1]);
       }
       if (a < nu && b < nu) st_wt(&rec->Pend[a][b], v);
     }

@@ -300,13 +300,15 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
         return EKF_E_ARG;
     }
   if (int rc = handle_info(s->h, &s->info)) return rc;  // host-planned work first, bulk joined
-  // Joseph form on the HBM pipeline takes one marker per chunk (ekf_api.cpp plan_known); the
-  // device planner writes one chunk per message, so it cannot honour it: refuse rather than run
-  // the simple form silently (the resident path carries the form in its own kernel)
-  if (s->info.joseph && !s->info.resident) return EKF_E_ARG;
+  // Joseph form on the HBM pipeline takes ≤ kMaxJoseph markers per chunk: the parallel form's
+  // ekf_replay_device plans two chunks per message; the sequential form writes one chunk per
+  // message, so it refuses the form rather than run the simple one silently (the resident path
+  // carries the form in its own kernel)
+  const bool par = parallel_ok(s, T, sense);
+  if (s->info.joseph && !s->info.resident && !par) return EKF_E_ARG;
   hipSetDevice(s->info.device);
   if (int rc = reserve(s, T)) return rc;
-  if (parallel_ok(s, T, sense)) return run_parallel(s, T, wheel_cmd, sense);
+  if (par) return run_parallel(s, T, wheel_cmd, sense);
   const int b = s->buf;
   s->buf ^= 1;
   const hipStream_t st = s->sst;

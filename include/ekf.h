@@ -143,7 +143,8 @@ int ekf_replay(ekf_t h, int assoc, int T, int m_max, const int* counts, const in
 
 /* ekf_replay with known ids (assoc = 0) whose inputs already live in device memory of the
  * handle's GPU (same layouts; d_actions nullable): the descriptors are planned on the GPU (one
- * chunk per message, so m_max <= EKF_MAX_CHUNK; no Joseph form, no resident handle: EKF_E_ARG)
+ * chunk per message, so m_max <= EKF_MAX_CHUNK; with the Joseph form two chunks of <= 8 markers
+ * per message; no resident handle: EKF_E_ARG)
  * and no input crosses PCIe. The measurement (range, bearing) of slam.cpp:208-210 is computed on
  * the GPU (correctly rounded sqrt; the bearing's atan2 may differ from glibc's in the last bit).
  * Inputs are not validated on the host: an id outside [0, N) is skipped by the correction and
@@ -167,8 +168,10 @@ int ekf_posterior(ekf_t h, int filter);
 /* Joseph-form covariance update, opt-in (off by default, like the reference, which applies
  * Σ ← (I − KH)Σ at slam.cpp:264-265): Σ ← (I − KH)Σ(I − KH)ᵀ + KRKᵀ for every later correction.
  * Equal in exact arithmetic with the optimal gain; it differs only in rounding. Resident path: its
- * own kernel instantiation. HBM pipeline (fp32 and fp64): one marker per chunk, the factor pair of
- * rank 2 + 4 (K·M and (ΣHᵀ − K·S)·Kᵀ), so one Σ pass per correction instead of per message. */
+ * own kernel instantiation. HBM pipeline (fp32 and fp64): chunks of <= 8 markers, each folded into
+ * one Σ pass of rank 2 + 4m (K_c·M_c and (Σ_cHᵀ − K_c·S_c)·K_cᵀ per correction), so two Σ passes
+ * per 16-marker message instead of one; ekf_replay_device and the simulator's parallel form plan
+ * two chunks per message on the GPU. */
 int ekf_set_joseph(ekf_t h, int on);
 
 /* Deferred submission. While on, the callbacks above only plan their work on the host; the plan

@@ -79,8 +79,11 @@ class DenseEKF:
     """Filter members of slam.cpp:657-676; constructor init slam.cpp:127-139."""
 
     def __init__(self, n_landmarks=50, q_noise=1.0e-2, r_noise=1.0e-2, init_var=10e6,
-                 mah_threshold=2.0):
+                 mah_threshold=2.0, joseph=False):
         self.N = n_landmarks
+        # opt-in Joseph form (BASELINE.json north_star; the reference uses (I − KH)Σ):
+        # Σ ← (I − KH)Σ(I − KH)ᵀ + K·R·Kᵀ, dense, as the C oracle's literal Joseph mode
+        self.joseph = joseph
         self.n = n = 2 * n_landmarks + 3
         self.sigma = np.zeros((n, n))
         self.sigma[3:, 3:] = np.eye(n - 3) * init_var
@@ -134,7 +137,11 @@ class DenseEKF:
         z_diff = z - z_hat
         z_diff[1] = normalize_angle(z_diff[1])
         self.state = self.state + K @ z_diff
-        self.sigma = (np.eye(self.n) - K @ H) @ self.sigma
+        if self.joseph:
+            ikh = np.eye(self.n) - K @ H
+            self.sigma = (ikh @ self.sigma) @ ikh.T + (K @ self.R) @ K.T
+        else:
+            self.sigma = (np.eye(self.n) - K @ H) @ self.sigma
         self.state[0] = normalize_angle(self.state[0])
 
     @staticmethod

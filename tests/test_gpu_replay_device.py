@@ -48,9 +48,11 @@ def _to_gpu(arrs):
             torch.from_numpy(act).cuda(), torch.from_numpy(rel).cuda(), torch.from_numpy(od).cuda())
 
 
-def _run(scs, N, F, spans, kinds, dtype=pyekf.EKF_F64, warm=None, holes=False):
+def _run(scs, N, F, spans, kinds, dtype=pyekf.EKF_F64, warm=None, holes=False, joseph=False):
     """Replay the spans [(T0, T1), ...] in order, span i through kinds[i] ('host' / 'device')."""
     e = pyekf.EKF(n_landmarks=N, n_filters=F, dtype=dtype)
+    if joseph:
+        assert e.set_joseph(True) == pyekf.EKF_OK
     if warm is not None:
         for f in range(F):
             x, S, tmo, c = warm
@@ -189,7 +191,7 @@ def test_device_replay_fp32_n1024():
 
 
 def test_device_replay_rejects():
-    """No resident handles, no Joseph form, at most EKF_MAX_CHUNK markers per message (one chunk)."""
+    """No resident handles, at most EKF_MAX_CHUNK markers per message (one chunk)."""
     import torch
     sc = synth.synthetic(96, 4)
     g = _to_gpu(_inputs([sc], 1, 0, 4))
@@ -198,10 +200,6 @@ def test_device_replay_rejects():
         e.replay_device(g[0], g[3], g[4], g[1], g[2])
     e.close()
     e = pyekf.EKF(n_landmarks=96)
-    e.set_joseph(True)
-    with pytest.raises(pyekf.EkfError):
-        e.replay_device(g[0], g[3], g[4], g[1], g[2])
-    e.set_joseph(False)
     wide = torch.zeros((4, 1, 17, 2), dtype=torch.float64, device="cuda")
     with pytest.raises(pyekf.EkfError):
         e.replay_device(g[0], wide, g[4], torch.zeros((4, 1, 17), dtype=torch.int32, device="cuda"))
@@ -211,3 +209,72 @@ def test_device_replay_rejects():
     e.sync()
     assert e.status() == 0
     e.close()
+
+
+@pytest.mark.parametrize("F,env", [(1, {}), (4, {}), (3, {"EKF_DEVSYNC": "0"}),
+                                   (2, {"EKF_SERIAL": "1"})],
+                         ids=["1filter", "4filters", "3filters_events", "2filters_serial"])
+def test_device_replay_joseph_equals_host(monkeypatch, F, env):
+    """Joseph form (ekf_set_joseph) through the device planner: every message becomes two chunks of
+    ≤ 8 markers (plan_kernels.hip, the second one empty for a short message), the host plans chunks
+    of ≤ 8 (plan_known). fp64 N = 96, up to 12 markers per message, holes (empty and all-DELETE
+    messages): the two end alike, and filter 0 equals the C oracle's Joseph mode."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pyekf.poison_lds()
+    scs = []
+    for k in range(3):  # messages of 12, 5, 8, 9 and 1 markers: one or two chunks of ≤ 8
+        s0 = synth.synthetic(96, 30, seed=7 + k, max_markers=12)
+        cnt = np.minimum(s0.count, np.roll([12, 5, 8, 9, 1], k)[np.arange(30) % 5]).astype(s0.count.dtype)
+        scs.append(synth.Scenario(s0.n_landmarks, s0.landmarks, s0.wheel, s0.ids, s0.actions,
+                                  s0.rel, cnt, s0.truth, s0.track, s0.radius))
+    assert scs[0].count.max() == 12 and scs[0].count.min() == 1
+    host, sh, ph = _run(scs, 96, F, [(0, 30)], ["host"], holes=True, joseph=True)
+    dev, sd, pd = _run(scs, 96, F, [(0, 30)], ["device"], holes=True, joseph=True)
+    assert sh == sd == [0] * F
+    _close(host, dev, STATE_TOL)
+    assert np.abs(ph - pd).max() <= STATE_TOL
+    o = orc.run_scenario(scs[0], False, joseph=True)
+    assert np.abs(dev[0][0] - o["state"]).max() < 1e-7
+    assert np.abs(dev[0][1] - o["sigma"]).max() < 1e-7
+
+
+@pytest.mark.parametrize("dtype", [pyekf.EKF_F32, pyekf.EKF_F64], ids=["f32", "f64"])
+def test_device_replay_joseph_n1024(dtype):
+    """The Joseph form at the headline shape (bench.py --workload n1024_fp32_joseph): N = 1024 from
+    an fp64 survey, 12 messages of 16 markers through the device planner — two chunks of 8 per
+    message, each chunk's V_c·K_cᵀ terms folded into its one Σ pass — against the fp64 oracle's
+    Joseph mode from the same state, at the fp32 tolerances of tests/test_gpu_scale.py (pose 1e-6,
+    state 1e-5, Σ 5e-5) or the fp64 populated-map ones (state 5e-8, Σ 1e-7)."""
+    N, warm, T = 1024, 40, 12
+    sc = synth.synthetic(N, warm + T)
+    assert sc.count[warm:].max() == 16
+    e64 = pyekf.EKF(n_landmarks=N)
+    odom = pyekf.odometry(sc)
+    e64.replay(sc.count[:warm, None], sc.rel[:warm, None], odom[:warm, None],
+               ids=sc.ids[:warm, None], actions=sc.actions[:warm, None])
+    x0, S0, c0 = e64.state()
+    ws = (x0, S0, e64.map_odom(), c0)
+    e64.close()
+    dev, sd, _ = _run([sc], N, 1, [(warm, warm + T)], ["device"], dtype=dtype, warm=ws,
+                      joseph=True)
+    assert sd == [0]
+    xd, Sd, cd = dev[0]
+    assert np.all(np.isfinite(Sd))
+    ref = orc.OracleEKF(n_landmarks=N, joseph=True)
+    ref.set(x0, S0, ws[2], x0[:3], c0)
+    for t in range(warm, warm + T):
+        ref.set_odom(odom[t])
+        c = int(sc.count[t])
+        ref.fake_sensor_cb(sc.ids[t, :c], sc.actions[t, :c], sc.rel[t, :c])
+    xr, Sr, _, cr = ref.get()
+    assert cd == cr
+    if dtype == pyekf.EKF_F32:
+        assert np.abs(xd[:3] - xr[:3]).max() < 1e-6
+        assert np.abs(xd - xr).max() < 1e-5
+        assert np.abs(Sd - Sr).max() < 5e-5
+    else:
+        assert np.abs(xd - xr).max() < 5e-8
+        assert np.abs(Sd - Sr).max() < 1e-7

@@ -216,7 +216,8 @@ def test_n1024_fp32_staged_rebuild_bit_identical(n1024, devsync, monkeypatch):
 @pytest.mark.parametrize("dtype", [pyekf.EKF_F32, pyekf.EKF_F64], ids=["f32", "f64"])
 def test_n1024_joseph_populated_against_oracle(n1024, dtype):
     """configs[2]'s populated map with the Joseph form (BASELINE.json north_star; ekf_set_joseph)
-    on the HBM pipeline: 6 circle messages (96 corrections, one Σ pass each) from the fp64 survey's
+    on the HBM pipeline: 6 circle messages (96 corrections in chunks of ≤ 8, one Σ pass per chunk
+    with the V_c·K_cᵀ terms folded in; host-planned, pose per message) from the fp64 survey's
     state against the oracle's Joseph mode. fp32 within the fp32 tolerances above (poses 1e-6,
     state 1e-5, Σ 5e-5), fp64 state 5e-8 and Σ 1e-7 (the populated-map tolerances above)."""
     sc, odom, ws = n1024

@@ -51,8 +51,8 @@ def _check_inputs(sim, sw, t0=0):
     return cnt, ids, act, rel, odom
 
 
-def _oracle(N, cnt, ids, act, rel, odom, f):
-    ref = orc.OracleEKF(n_landmarks=N)
+def _oracle(N, cnt, ids, act, rel, odom, f, joseph=False):
+    ref = orc.OracleEKF(n_landmarks=N, joseph=joseph)
     for t in range(cnt.shape[0]):
         ref.set_odom(odom[t])
         c = int(cnt[t, f])
@@ -244,18 +244,34 @@ def test_sim_parallel_form_sense_all_on_the_pipeline(monkeypatch):
     e.close()
 
 
-def test_sim_refuses_joseph_on_the_pipeline():
-    """ekf_set_joseph on an HBM-pipeline handle (fp32): the device planner cannot write the
-    one-marker chunks the form needs there, so ekf_sim_run returns EKF_E_ARG instead of running
-    the simple form; with the form off again the same run goes through."""
-    N, F = 64, 2
-    sw = synth.swarm(N, F, 4)
-    e = pyekf.EKF(n_landmarks=N, n_filters=F, dtype=pyekf.EKF_F32)
-    sim = _sim_for(e, sw)
+def test_sim_joseph_on_the_pipeline(monkeypatch):
+    """ekf_set_joseph on an HBM-pipeline handle: the parallel form (ekf_replay_device's planner, two
+    chunks of ≤ 8 markers per message) runs the Joseph form — basic_world forced onto the pipeline
+    over two runs, against the oracle's Joseph mode fed the device's markers (1e-8). The sequential
+    form writes one chunk per message, so it returns EKF_E_ARG instead of running the simple form."""
+    monkeypatch.setenv("EKF_RESIDENT", "0")
+    monkeypatch.delenv("EKF_SIM_PARALLEL", raising=False)
+    F, T1, T2 = 4, 12, 10
+    drive = synth.circle_drive(T1 + T2 + 1, 0.3, sense=synth.SENSE_ALL)
+    seeds = np.uint64(5151) + np.arange(F, dtype=np.uint64)
+    sw = synth._generate(50, drive, seeds, synth.BASIC_WORLD_LANDMARKS,
+                         start_pose=(synth.BASIC_WORLD_THETA0, 0.0, 0.0), max_range=0.8)
+    e = pyekf.EKF(n_landmarks=50, n_filters=F)
+    assert e.path == pyekf.EKF_PATH_PIPELINE
     assert e.set_joseph(True) == pyekf.EKF_OK
+    sim = _sim_for(e, sw, max_range=0.8)
+    cnt, ids, act, rel, odom = _runs(sim, sw, ((0, T1), (T1, T1 + T2)))
+    for f in (0, 3):
+        assert e.status(f) == 0
+        x, S, _ = e.state(f)
+        xr, Sr, _, _ = _oracle(50, cnt, ids, act, rel, odom, f, joseph=True)
+        assert np.abs(x - xr).max() < POSE_TOL, f
+        assert np.abs(S - Sr).max() < POSE_TOL, f
+    monkeypatch.setenv("EKF_SIM_PARALLEL", "0")
+    tpm = sw.wheel.shape[1]
+    T = T1 + T2
     with pytest.raises(pyekf.EkfError) as ei:
-        sim.run(sw.cmd[:sw.wheel.shape[1]], sw.sense[:1])
+        sim.run(sw.cmd[T * tpm:(T + 1) * tpm], sw.sense[T:T + 1])
     assert ei.value.rc == pyekf.EKF_E_ARG
-    assert e.set_joseph(False) == pyekf.EKF_OK
     sim.close()
     e.close()

@@ -66,3 +66,26 @@ def test_oracle_joseph_modes_agree(assoc):
     assert np.abs(js["poses"] - jl["poses"]).max() < 1e-9
     assert np.abs(js["sigma"] - simple["sigma"]).max() < 3e-8
     assert np.abs(js["poses"] - simple["poses"]).max() < 1e-9
+
+
+def test_numpy_oracle_joseph_matches_c():
+    """bench.py's CPU leg of the Joseph workload (n1024_fp32_joseph): oracle/ekf_numpy.py's dense
+    (I−KH)Σ(I−KH)ᵀ + KRKᵀ equals the C oracle's Joseph mode message by message (fake_sensor_cb,
+    slam.cpp:180-316, with the update of :264-265 in Joseph form)."""
+    import ekf_numpy
+    import pyekf
+    from pyekf import synth
+    sc = synth.synthetic(20, 14, seed=5, max_markers=6)
+    odom = pyekf.odometry(sc)
+    d = ekf_numpy.DenseEKF(n_landmarks=20, joseph=True)
+    ref = orc.OracleEKF(n_landmarks=20, joseph=True)
+    for t in range(sc.n_messages):
+        c = int(sc.count[t])
+        d.t_odom_robot = tuple(odom[t])
+        d.fake_sensor_cb(sc.ids[t, :c], sc.actions[t, :c], sc.rel[t, :c])
+        ref.set_odom(odom[t])
+        ref.fake_sensor_cb(sc.ids[t, :c], sc.actions[t, :c], sc.rel[t, :c])
+        x = ref.get(sigma=False)[0]
+        assert np.abs(d.state - x).max() < 1e-8, t
+    x, S, _, _ = ref.get()
+    assert np.abs(d.sigma - S).max() < 1e-7
