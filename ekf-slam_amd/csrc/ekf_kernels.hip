@@ -903,6 +903,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     tq = ctl->tmo[tid < 3 ? tid : 0];
   }
 
+  EKF_STAMP(14);
   // ---- A0: index sets U (this chunk) and U' (kLook: the previous chunk, from the descriptor) ----
   if (tid < kMaxU) {  // u[3+2c], u[4+2c] = the columns of marker c's landmark (bad id → slot 0's)
     int u = tid < 3 ? tid : 0;  // padding 0: loads stay in bounds
@@ -1088,6 +1089,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         if (row < nu && col < nu) P[row][col] = acc[r];
       }
     }
+    EKF_STAMPT(10, 64);
+    EKF_STAMPT(11, 128);
+    EKF_STAMPT(13, 192);
     // waves 2 and 3 (two P tiles against wave 0's three): the predicted pose and x_in[U]
     if (wv == 2 && ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
       double a1, a2;
@@ -1095,6 +1099,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
       sh.a1 = a1;
       sh.a2 = a2;
+      EKF_STAMPT(8, 128);
     }
     if (wv == 3) {
       if (ln < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
@@ -1112,6 +1117,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         sh.xU[0][ln] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[ln] + r;
       }
       if (ln < 3) sh.xpose[ln] = sh.pv.xU[ln];  // pose ∈ U' always
+      EKF_STAMPT(9, 192);
     }
   } else {
     double vd[kPer];
