@@ -281,7 +281,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
     lx = readlane_f64(xl, pj);
     ly = readlane_f64(xl, pj + 1);
     init = false;
-    if (!skn && !noinit && lx == 0.0 && ly == 0.0) {  // slam.cpp:213-216 (zn, skn: marker c)
+    // slam.cpp:213-216 (zn, skn: marker c); a wave-uniform test, so a scalar branch
+    if (__builtin_amdgcn_readfirstlane(!skn && !noinit && lx == 0.0 && ly == 0.0)) {
       init = true;
       sh.any_init = 1;
       lx = pose[1] + zn0 * cos(zn1 + pose[0]);
@@ -301,8 +302,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       zn1 = d.z[c + 1][1];
       skn = sh.skip[c + 1];
     }
-    double Si[4] = {0.0, 0.0, 0.0, 0.0}, nv0 = 0.0, nv1 = 0.0, Sm_keep[4];
-    if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
+    double Si[4], nv0, nv1, Sm_keep[4];
     EKF_STAMP(65 + 8 * c);
     // (Σ·Hᵀ)[ℓ] and (H·Σ)[:, ℓ]. H's shape (range_bearing): H0 = [0, h1, h2, −h1, −h2],
     // H1 = [−1, g1, g2, −g1, −g2] — a row times H is two FMAs on (v1 − v3, v2 − v4) (exact negations)
@@ -327,22 +327,33 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
         Sm[3] = fma(H1[2], tb2, fma(H1[1], tb1, -tb[0])) + r_noise;
       }
       for (int k = 0; k < 4; ++k) Sm_keep[k] = Sm[k];
-      if (!sk && inv2(Sm, Si)) {
-        nv0 = z0 - zhat[0];
-        bool nok;
-        const double nn = normalize_angle_near(z1 - zhat[1], &nok);
-        nv1 = nok ? nn : normalize_angle(z1 - zhat[1]);
-      } else {
-        if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every lane
-        sk = true;
-      }
-    }
-    if (sk) {
+      // The common case without a branch (so the step's scalar chain is one basic block): a
+      // finite, nonsingular S and a bearing / innovation within normalize_angle_near's range.
+      // Anything else — a skipped marker, a singular S (arma's inv throws), an angle beyond it —
+      // redoes these scalars on the generic path below, in the reference's order; the common
+      // case's values are that path's bit for bit.
+      const double det = inv2_calc(Sm, Si);
+      nv0 = z0 - zhat[0];
+      bool nok;
+      nv1 = normalize_angle_near(z1 - zhat[1], &nok);
+      const bool good = !sk && bok && nok && inv2_ok(det, Si);
+      if (!__builtin_amdgcn_readfirstlane(good)) {  // (uniform: every lane has the same scalars)
+        if (!bok) zhat[1] = normalize_angle(braw);  // |θ| > π: the generic fmod path
+        if (!sk && inv2(Sm, Si)) {
+          nv0 = z0 - zhat[0];
+          bool nok2;
+          const double nn = normalize_angle_near(z1 - zhat[1], &nok2);
+          nv1 = nok2 ? nn : normalize_angle(z1 - zhat[1]);
+        } else {
+          if (!sk) sh.status |= EKF_FLAG_NUMERIC_D;  // same value from every lane
+          sk = true;
 #pragma unroll
-      for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
-      Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
-      nv0 = nv1 = 0.0;
-      ka = kb = mm0 = mm1 = 0.0;
+          for (int a = 0; a < 5; ++a) H0[a] = H1[a] = 0.0;
+          Si[0] = Si[1] = Si[2] = Si[3] = 0.0;
+          nv0 = nv1 = 0.0;
+          ka = kb = mm0 = mm1 = 0.0;
+        }
+      }
     }
     // The next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}) after step c−1. Pose columns /
     // rows: pk / pm (pA ⊃ pose). The nx columns / rows were read one step back (rn / qn, after
@@ -406,14 +417,16 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
     const double V1 = J ? kb - (K0 * Sm_keep[1] + K1 * Sm_keep[3]) : 0.0;
     {
       double xt = xl;
-      if (init) {
-        if (ul == jx) xt = lx;
-        else if (ul == jx + 1) xt = ly;
-      }
+      xt = (init && ul == jx) ? lx : ((init && ul == jx + 1) ? ly : xt);
       xt = xt + (K0 * nv0 + K1 * nv1);              // slam.cpp:261
       bool tok;                                     // slam.cpp:267 on lane 0, branch-free
       const double tn = normalize_angle_near(xt, &tok);
-      if (lane == 0) xt = tok ? tn : normalize_angle(xt);
+      const double xraw = xt;
+      xt = lane == 0 ? tn : xt;
+      // lane 0's θ beyond normalize_angle_near's range: the generic path (a scalar branch)
+      if (__builtin_amdgcn_ballot_w64(!tok) & 1ull) {
+        if (lane == 0) xt = normalize_angle(xraw);
+      }
       xl = xt;
       *(lane < nu ? &sh.xU[0][lane] : &sh.junk[0][lane]) = xt;
     }
@@ -512,58 +525,72 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
 constexpr int kChainThreads = 256;
 constexpr int kRebW = kMaxU + 1;                                      // 36: entry e = a·36 + b
 constexpr int kRebPer = (kRebW * kRebW + kChainThreads - 1) / kChainThreads;  // 6
+// The predict (slam.cpp:198) changes an entry of a block over U × U' only in rows / columns 1 and 2
+// (α_i = 0 unless u_i ∈ {1, 2}, and u_i = i for the pose positions of U and U') and on the pose
+// diagonal (Q̄): 4·36 − 3 entries of the 36 × 36 block. Special entry s → (a, b): s < 72 rows 1, 2
+// (b = 0..35); s < 140 columns 1, 2 (a = 0, 3..35); s = 140 the (0, 0) entry.
+constexpr int kSpec = 141;
+__device__ __forceinline__ void special_entry(int s, int& a, int& b) {
+  if (s < 72) {
+    a = 1 + (s >= 36);
+    b = s - (s >= 36 ? 36 : 0);
+  } else if (s < 140) {
+    const int r = s - 72, h = r >= 34;
+    b = 1 + h;
+    const int a2 = r - (h ? 34 : 0);
+    a = a2 == 0 ? 0 : a2 + 2;
+  } else {
+    a = 0;
+    b = 0;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void rebuild_rcd(ChainShared& sh, double (&P)[kMaxU][kMaxU + 1],
                                             const T (&vd)[kRebPer], const T (&vr)[kRebPer],
                                             const T (&vc)[kRebPer], int tid, int nu, int np,
                                             double q) {
   constexpr int kW = kRebW, kPer = kRebPer;
-  const bool pf = sh.pv.first != 0;
-  const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
-  // every LDS read of the six entries first (clamped indices, no branch around a read): one
-  // LDS round instead of a wait per predicated read
-  double r0Ub[kPer], r0Ua[kPer], c0Ua[kPer], r0Pb[kPer], c0Pb[kPer];
-  int ua[kPer], ub[kPer], pu[kPer];
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const int e = tid + i * kChainThreads;
-    const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
-    ua[i] = sh.u[a];
-    ub[i] = sh.u[b];
-    pu[i] = sh.pv.u[b];
-    r0Ub[i] = sh.pv.r0U[b];
-    r0Ua[i] = sh.pv.r0U[a];
-    c0Ua[i] = sh.pv.c0U[a];
-    r0Pb[i] = sh.pv.r0P[b];
-    c0Pb[i] = sh.pv.c0P[b];
-  }
+  // the raw blocks: no LDS read
 #pragma unroll
   for (int i = 0; i < kPer; ++i) {
     const int e = tid + i * kChainThreads;
     const int a = e / kW, b = e % kW;
-    double v = static_cast<double>(vd[i]), vR = 0.0, wC = 0.0;
-    if (b < np) {
-      vR = static_cast<double>(vr[i]);
-      wC = static_cast<double>(vc[i]);
-    }
-    if (pf) {
-      const double ai = alpha_of(ua[i], qa1, qa2), aj = alpha_of(ub[i], qa1, qa2);
-      const double ak = alpha_of(pu[i], qa1, qa2);
-      v = v + ai * r0Ub[i];
-      v = v + (c0Ua[i] + ai * s00) * aj;
-      v = (ua[i] == ub[i] && ua[i] < 3) ? v + q : v;
-      double v2 = vR + ai * r0Pb[i];
-      v2 = v2 + (c0Ua[i] + ai * s00) * ak;
-      double w2 = wC + ak * r0Ua[i];
-      w2 = w2 + (c0Pb[i] + ak * s00) * ai;
-      const bool qd = ua[i] == pu[i] && ua[i] < 3;
-      vR = b < np ? (qd ? v2 + q : v2) : 0.0;
-      wC = b < np ? (qd ? w2 + q : w2) : 0.0;
-    }
-    if (a < nu && b < nu) P[a][b] = v;
+    if (a < nu && b < nu) P[a][b] = static_cast<double>(vd[i]);
     if (a < nu) {  // b = k over U' (36: the MFMA k padding, zero)
-      sh.pv.R[a][b] = vR;
-      sh.pv.C[b][a] = wC;
+      sh.pv.R[a][b] = b < np ? static_cast<double>(vr[i]) : 0.0;
+      sh.pv.C[b][a] = b < np ? static_cast<double>(vc[i]) : 0.0;
+    }
+  }
+  if (sh.pv.first == 0) return;  // (uniform)
+  // the previous chunk's predict on its special entries only (the others it leaves as they are)
+  lds_barrier();
+  const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
+  for (int s = tid; s < 3 * kSpec; s += kChainThreads) {
+    const int blk = s >= 2 * kSpec ? 2 : (s >= kSpec ? 1 : 0);
+    int a, b;
+    special_entry(s - blk * kSpec, a, b);
+    if (a >= nu) continue;
+    const double ai = alpha_of(a, qa1, qa2);
+    if (blk == 0) {  // D = Σ_in'[U, U] → P
+      if (b >= nu) continue;
+      const double aj = alpha_of(b, qa1, qa2);
+      double v = P[a][b];
+      v = v + ai * sh.pv.r0U[b];
+      v = v + (sh.pv.c0U[a] + ai * s00) * aj;
+      P[a][b] = (a == b && a < 3) ? v + q : v;
+    } else if (b < np) {  // b = k over U'
+      const double ak = alpha_of(b, qa1, qa2);
+      const bool qd = a == b && a < 3;
+      if (blk == 1) {  // R = Σ_in'[U, U']
+        double v2 = sh.pv.R[a][b] + ai * sh.pv.r0P[b];
+        v2 = v2 + (sh.pv.c0U[a] + ai * s00) * ak;
+        sh.pv.R[a][b] = qd ? v2 + q : v2;
+      } else {  // C = Σ_in'[U', U]
+        double w2 = sh.pv.C[b][a] + ak * sh.pv.r0U[a];
+        w2 = w2 + (sh.pv.c0P[b] + ak * s00) * ai;
+        sh.pv.C[b][a] = qd ? w2 + q : w2;
+      }
     }
   }
 }
@@ -1153,21 +1180,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // ---- A3: x[U] pose, α, this chunk's predict folded in: P ← A P Aᵀ + Q̄ (slam.cpp:198) --------
   __syncthreads();
   {
-    // every thread reads its raw entries, row 0 and column 0 straight from the block (one LDS
-    // round, no α / row / column exchange); α, row 0, column 0 also go to LDS for the record
+    // α, row 0, column 0 to LDS for the record; the predict (slam.cpp:198) changes only the
+    // special entries (rows / columns 1, 2 and the pose diagonal, special_entry): one per thread,
+    // its raw value, row 0 and column 0 read before any is written
     const double a1 = sh.a1, a2 = sh.a2, s00 = P[0][0];
-    double pr[kPer], r0[kPer], c0[kPer];
-    int ua[kPer], ub[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = tid + i * kChainThreads;
-      const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);
-      pr[i] = P[a][b];
-      r0[i] = P[0][b];
-      c0[i] = P[a][0];
-      ua[i] = sh.u[a];
-      ub[i] = sh.u[b];
-    }
     if (tid < nu) {
       if (tid < 3) sh.xU[0][tid] = sh.pose[tid];
       sh.alphaU[tid] = first ? alpha_of(sh.u[tid], a1, a2) : 0.0;
@@ -1175,19 +1191,19 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       sh.col0raw[tid] = P[tid][0];
     }
     if (tid == 0) sh.s00 = s00;
-    // predict folded in: P ← A P Aᵀ + Q̄ on the block (slam.cpp:198)
     if (first) {
-      __syncthreads();  // every raw read done before the first write
-#pragma unroll
-      for (int i = 0; i < kPer; ++i) {
-        const int e = tid + i * kChainThreads;
-        const int a = e / kW, b = e % kW;
-        const double ai = alpha_of(ua[i], a1, a2), aj = alpha_of(ub[i], a1, a2);
-        double v = pr[i] + ai * r0[i];
-        v = v + (c0[i] + ai * s00) * aj;
-        v = (ua[i] == ub[i] && ua[i] < 3) ? v + A.q : v;
-        if (a < nu && b < nu) P[a][b] = v;
-      }
+      int a, b;
+      special_entry(min(tid, kSpec - 1), a, b);
+      const bool ok = tid < kSpec && a < nu && b < nu;
+      a = min(a, kMaxU - 1);
+      b = min(b, kMaxU - 1);
+      const double pr = P[a][b], r0 = P[0][b], c0 = P[a][0];
+      lds_barrier();  // every raw read done before the first write
+      const double ai = alpha_of(a, a1, a2), aj = alpha_of(b, a1, a2);
+      double v = pr + ai * r0;
+      v = v + (c0 + ai * s00) * aj;
+      v = (a == b && a < 3) ? v + A.q : v;
+      if (ok) P[a][b] = v;
     }
   }
   __syncthreads();

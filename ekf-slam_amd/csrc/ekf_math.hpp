@@ -81,15 +81,24 @@ __device__ __forceinline__ void range_bearing(const double* pose, double lx, dou
 }
 
 // arma::inv on a 2×2 (closed form: adjugate / det, one reciprocal). false if singular / non-finite.
-__device__ __forceinline__ bool inv2(const double* A, double* o) {
+// inv2_calc: the adjugate / det without a test (returns det); inv2_ok: whether it was a valid inverse.
+__device__ __forceinline__ double inv2_calc(const double* A, double* o) {
   const double det = A[0] * A[3] - A[1] * A[2];
-  if (!(fabs(det) > 0.0)) return false;
   const double idet = rcp_refined(det);
   o[0] = A[3] * idet;
   o[1] = -A[1] * idet;
   o[2] = -A[2] * idet;
   o[3] = A[0] * idet;
-  return isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
+  return det;
+}
+__device__ __forceinline__ bool inv2_ok(double det, const double* o) {
+  return fabs(det) > 0.0 && isfinite(o[0]) && isfinite(o[1]) && isfinite(o[2]) && isfinite(o[3]);
+}
+__device__ __forceinline__ bool inv2(const double* A, double* o) {
+  const double det = A[0] * A[3] - A[1] * A[2];
+  if (!(fabs(det) > 0.0)) return false;
+  inv2_calc(A, o);
+  return inv2_ok(det, o);
 }
 
 // slam.cpp:364-401: d_k = νᵀ ψ⁻¹ ν for a landmark at (lx, ly) with P the 5×5 block of Σ over

@@ -79,3 +79,4 @@ for c in (0, 1, m // 2, m - 2):
           f"  geometry(c+1)+cross update {s[b + 6] - s[b + 4]}  -> next {s[b + 8] - s[b + 6]}")
     print(f"   wave3: pub seen at {s[192 + 2 * c] - s[b]}, pdone at {s[193 + 2 * c] - s[b]} "
           f"(wave0 publish at {s[b + 4] - s[b]}, next-step pdone wait at {s[b + 8 + 2] - s[b]})")
+    print(f"   wave1 Z_c done at {s[320 + c] - s[b]}, wave2 Y_c done at {s[360 + c] - s[b]} (from wave 0's step start)")
