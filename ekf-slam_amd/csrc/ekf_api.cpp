@@ -238,7 +238,7 @@ int join_bulk(ekf_ctx* h) {
 // hd: the host copy of the group's descriptors (nullptr: written on the device, no kStageOut).
 template <typename T>
 int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
-                 bool pipelined, bool nolook, bool publish_end, bool stage_hint) {
+                 bool pipelined, bool nolook, bool publish_end, int stage_hint) {
   PassArgs<T> a = args<T>(h, dptr, f0);
   a.desc_stride = nf;
   const unsigned s0 = static_cast<unsigned>(h->seq);
@@ -287,8 +287,9 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
     });
     if (rc) return rc;
     // some filter stages the rebuild operands of its chunk after next (device-written descriptors:
-    // the caller's hint, the staging kernel reads every descriptor's own flags)
-    bool stage = !hd && stage_hint;
+    // the caller's hint — the group's first stage_hint chunks may, the last two of a device replay
+    // have no chunk after next in it — the staging kernel reads every descriptor's own flags)
+    bool stage = !hd && i < stage_hint;
     for (int k = 0; hd && k < nf; ++k) {
       const int fl = hd[static_cast<size_t>(i) * nf + k].flags;
       stage = stage || ((fl & kActive) && (fl & kStageOut));
@@ -308,8 +309,10 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
 // nolook: some active filter's first chunk gathers its own Σ_in (no kLook rebuild)
 // publish_end: the group's last Σ pass publishes its device epoch (false only for a flush's last
 // launch, whose successor the next flush orders on the host: one kernel less on the stream's tail)
+// stage_hint (device-written descriptors): the group's first stage_hint chunks may stage rebuild
+// operands (kStageOut), so only they are followed by the staging kernel
 int group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int nf, int nchunks,
-          bool pipelined, bool nolook = true, bool publish_end = true, bool stage_hint = false) {
+          bool pipelined, bool nolook = true, bool publish_end = true, int stage_hint = 0) {
   return h->cfg.dtype == EKF_F32
              ? launch_group<float>(h, dptr, hd, f0, nf, nchunks, pipelined, nolook, publish_end,
                                    stage_hint)
@@ -1394,7 +1397,8 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   const bool stg = h->stage != nullptr;
   int rc = EKF_OK;
   if (h->devsync && !h->serial) {
-    rc = group(h, h->ddesc, nullptr, 0, h->F, Tc, true, true, false, stg);
+    // (the device planner stages only for chunks two on inside this replay: kStageOut needs next2)
+    rc = group(h, h->ddesc, nullptr, 0, h->F, Tc, true, true, false, stg ? Tc - 2 : 0);
   } else {
     // Events: a chunk t ≥ 1 needs the Σ pass two back (kLook), or — no message of its filter
     // earlier in this replay — the passes before the replay, which the first chunk's join covers:
@@ -1402,7 +1406,7 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
     // Σ pass of t − 1 where the CUs allow (not a join of the whole bulk stream per message)
     for (int t = 0; t < Tc && !rc; ++t)
       rc = group(h, h->ddesc + static_cast<size_t>(t) * F, nullptr, 0, h->F, 1, true, t == 0, true,
-                 stg);
+                 stg && t + 2 < Tc ? 1 : 0);
   }
   h->main_dirty = true;
   return rc;

@@ -1239,11 +1239,18 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     else
       chain_wave0<false>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq);
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
-    // lane → column 3+(lane&31), rows 3.. of parity lane>>5; all loads issued before the stores
+    // lane → column 3+(lane&31), rows 3.. of parity lane>>5. The lane's 16 entries stay in
+    // registers for the whole chunk: every step's rank-2 term is applied to all of them — also to
+    // those in the next marker's cross, which wave 0 updates (and stores) itself with the same
+    // operands in the same order, so the register copy keeps the block's bits — and only the
+    // entries outside that cross are stored (what wave 0 reads ahead, and the block's final state).
     const int hb = lane & 31, hr = lane >> 5;
     const int b = min(3 + hb, kMaxU - 1);
     auto rest = [&](auto jc) {  // (Joseph: V_c[a]·K_c[b] after the K·M term, as wave 0 does)
       constexpr bool J = decltype(jc)::value;
+      double pv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) pv[i] = P[min(3 + hr + 2 * i, kMaxU - 1)][b];  // clamped rows
       for (int c = 0; c + 1 < m; ++c) {
         lds_wait_ge(&sh.pub, c + 1);
         EKF_STAMPT(192 + 2 * c, 192);
@@ -1251,11 +1258,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         const bool colok = 3 + hb < nu && b != nx && b != nx + 1;
         const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
         const double kb0 = J ? sh.KU[c][b][0] : 0.0, kb1 = J ? sh.KU[c][b][1] : 0.0;
-        double pv[16], k0[16], k1[16], w0[16], w1[16];
+        double k0[16], k1[16], w0[16], w1[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
           const int a = min(3 + hr + 2 * i, kMaxU - 1);
-          pv[i] = P[a][b];
           k0[i] = sh.KU[c][a][0];
           k1[i] = sh.KU[c][a][1];
           if (J) {
@@ -1271,6 +1277,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           const bool ok = colok && a < nu && a != nx && a != nx + 1;
           double v = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
           if (J) v = rank2_sub(v, w0[i], w1[i], kb0, kb1);
+          pv[i] = v;
           *(ok ? &P[a][b] : &sh.junk[3][lane]) = v;
         }
         lds_publish(&sh.pdone, c + 1);
