@@ -1288,6 +1288,21 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       rest(std::true_type{});
     else
       rest(std::false_type{});
+    // The posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277) as soon as wave 0 has
+    // published the last step (its x is stored before that), beside waves 1–2's last Z / Y and off
+    // the epilogue (a pose composition's sin / cos on one lane)
+    if (lane == 0 && (d.flags & kLast)) {
+      lds_wait_ge(&sh.pub, m);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      const Pose2 tmo = compose(Pose2{sh.xU[0][0], sh.xU[0][1], sh.xU[0][2]},
+                                inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
+      ctl->tmo[0] = tmo.theta;
+      ctl->tmo[1] = tmo.x;
+      ctl->tmo[2] = tmo.y;
+      sh.tmo[0] = tmo.theta;
+      sh.tmo[1] = tmo.x;
+      sh.tmo[2] = tmo.y;
+    }
   } else if (wave == 1) {  // Z_c: K_c[i] = r_0(i)·Z_c for every row i
     // Σ_c[i, pA_c] = r_0(i)·(E_c − Σ_{k<c} Z_k·M_k[:, pA_c]) (E_c selects the positions pA_c), so
     // Z_c = E_c·G − Σ_{k<c} Z_k·C_k with G = Hᵀ·S⁻¹ (5×2) and C_k = M_k[:, pA_c]·G (2×2): lane k
@@ -1359,6 +1374,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           z0 = pos == a ? G0[a] : z0;
           z1 = pos == a ? G1[a] : z1;
         }
+#pragma unroll 4
         for (int k = 0; k < c; ++k) {
           const double zk0 = sh.Z[li][2 * k], zk1 = sh.Z[li][2 * k + 1];
           const double c00 = sh.Cz[k][0], c01 = sh.Cz[k][1], c10 = sh.Cz[k][2], c11 = sh.Cz[k][3];
@@ -1441,6 +1457,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           w0 = pos == a ? H0[a] : w0;
           w1 = pos == a ? H1[a] : w1;
         }
+#pragma unroll 4
         for (int k = 0; k < c; ++k) {
           const double zk0 = sh.Z[li][2 * k], zk1 = sh.Z[li][2 * k + 1];
           const double vk0 = sh.Z[li][cols + 2 * k], vk1 = sh.Z[li][cols + 2 * k + 1];
@@ -1546,6 +1563,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           y0 = pos == a ? H0[a] : y0;
           y1 = pos == a ? H1[a] : y1;
         }
+#pragma unroll 4
         for (int k = 0; k < c; ++k) {
           const double yk0 = sh.Y[2 * k][lj], yk1 = sh.Y[2 * k + 1][lj];
           const double d00 = sh.Dy[k][0], d01 = sh.Dy[k][1], d10 = sh.Dy[k][2], d11 = sh.Dy[k][3];
@@ -1596,26 +1614,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   __syncthreads();
   EKF_STAMP(12);
   // ---- epilogue -----------------------------------------------------------------------------
-  // Wave 3 (one lane): the posterior t_map_odom. Waves 0–2 meanwhile prefetch the next chunk's
-  // descriptor and store the record write-through. The record's epoch is published at the next
+  // Waves 0–2 prefetch the next chunk's descriptor and store the record write-through. The record's epoch is published at the next
   // chunk's start (or the kernel's end): the stores drain behind the next prologue instead of
   // stalling this one. The record parity's release (the bulk stream done with it) was awaited by
   // the prologue's poll.
   const double* xfin = sh.xU[0];
   const bool pre_next = ci + 1 < nchunks;
   if (wave == 3) {
-    if (lane == 0) {
-      if (d.flags & kLast) {  // posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277)
-        const Pose2 tmo = compose(Pose2{xfin[0], xfin[1], xfin[2]},
-                                  inverse(Pose2{d.odom[0], d.odom[1], d.odom[2]}));
-        ctl->tmo[0] = tmo.theta;
-        ctl->tmo[1] = tmo.x;
-        ctl->tmo[2] = tmo.y;
-        sh.tmo[0] = tmo.theta;
-        sh.tmo[1] = tmo.x;
-        sh.tmo[2] = tmo.y;
-      }
-    }
+    // (the posterior t_map_odom: wave 3 after the last step, above)
   } else {
     if (pre_next && tid >= 128 && tid < 128 + static_cast<int>(sizeof(MsgDesc) / 16))
       reinterpret_cast<uint4*>(&sdesc[(ci + 1) & 1])[tid - 128] = reinterpret_cast<const uint4*>(
