@@ -1038,41 +1038,52 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     __syncthreads();
     EKF_STAMP(3);
     EKF_STAMP(4);
-    // K' (48×32: 6 tiles of R·Z') and M' (32×48: 6 tiles of Y'·C) on f64 MFMA, 12 tiles over the 4
-    // waves. Operand reads are unconditional (clamped rows / columns feed only discarded outputs,
-    // k ≥ |U'| is zero-padded), all issued before the tile's first MFMA.
-    for (int tt = wv; tt < 12; tt += 4) {
-      double av[9], bv[9];
-      const bool kt = tt < 6;
-      const int ti = kt ? tt >> 1 : (tt - 6) / 3, tj = kt ? tt & 1 : (tt - 6) % 3;
-      const int ar = min(16 * ti + i16, kMaxU - 1), bc = min(16 * tj + i16, kMaxU - 1);
-      if (kt) {
+    // K' (48×32: 6 tiles of R·Z') and M' (32×48: 6 tiles of Y'·C) on f64 MFMA, 12 tiles, three per
+    // wave. Operand reads are unconditional (clamped rows / columns feed only discarded outputs,
+    // k ≥ |U'| is zero-padded in both operands, so every k-step runs: its MFMA adds exact zeros).
+    // The wave's three tiles are one basic block — every operand read issued first (a row / column
+    // pointer and stride per tile instead of a branch), then three interleaved accumulation chains:
+    // the MFMA pipe, not each tile's read latency and dependent chain in turn, sets the time.
+    {
+      double av[3][9], bv[3][9];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int tt = wv + 4 * q;
+        const bool kt = tt < 6;
+        const int ti = kt ? tt >> 1 : (tt - 6) / 3, tj = kt ? tt & 1 : (tt - 6) % 3;
+        const int ar = min(16 * ti + i16, kMaxU - 1), bc = min(16 * tj + i16, kMaxU - 1);
+        // A: K' tile R[ar][k], M' tile Y'[row][k] (k contiguous); B: Z'[k][col] (stride kZC + 1) or
+        // C[k][bc] (stride kMaxU + 1)
+        const double* pa = kt ? &sh.pv.R[ar][0] : &sh.pv.Y[16 * ti + i16][0];
+        const double* pb = kt ? &sh.pv.Z[0][16 * tj + i16] : &sh.pv.C[0][bc];
+        const int sb = kt ? kZC + 1 : kMaxU + 1;
 #pragma unroll
         for (int s0 = 0; s0 < 9; ++s0) {
-          av[s0] = sh.pv.R[ar][4 * s0 + k4];
-          bv[s0] = sh.pv.Z[4 * s0 + k4][16 * tj + i16];
-        }
-      } else {
-#pragma unroll
-        for (int s0 = 0; s0 < 9; ++s0) {
-          av[s0] = sh.pv.Y[16 * ti + i16][4 * s0 + k4];
-          bv[s0] = sh.pv.C[4 * s0 + k4][bc];
+          av[q][s0] = pa[4 * s0 + k4];
+          bv[q][s0] = pb[(4 * s0 + k4) * sb];
         }
       }
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      d4 acc[3] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
       for (int s0 = 0; s0 < 9; ++s0)
-        if (4 * s0 < np) acc = mfma_f64(av[s0], bv[s0], acc);
-      if (kt) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * ti + k4 + 4 * r;
-          if (row < kMaxU) sh.pv.K[row][16 * tj + i16] = acc[r];
+        for (int q = 0; q < 3; ++q) acc[q] = mfma_f64(av[q][s0], bv[q][s0], acc[q]);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int tt = wv + 4 * q;
+        const bool kt = tt < 6;
+        const int ti = kt ? tt >> 1 : (tt - 6) / 3, tj = kt ? tt & 1 : (tt - 6) % 3;
+        if (kt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * ti + k4 + 4 * r;
+            if (row < kMaxU) sh.pv.K[row][16 * tj + i16] = acc[q][r];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (16 * tj + i16 < kMaxU) sh.pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[q][r];
         }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (16 * tj + i16 < kMaxU) sh.pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[r];
       }
     }
     EKF_STAMP(7);
@@ -1091,35 +1102,53 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
     // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
     // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4m')
-    const int zc = pj ? 2 * pm2 : 2 * sh.pv.m;
-    for (int tt = wv; tt < 9; tt += 4) {
-      const int ti = tt / 3, tj = tt % 3;
-      const int col = 16 * tj + i16, ar = min(16 * ti + i16, kMaxU - 1), cc = min(col, kMaxU - 1);
-      double av[8], bv[8];
+    // (every k-step runs: K' columns and M' rows beyond the chunk's rank are zero, so their MFMAs
+    // add exact zeros.) Waves 0, 2 and 3 take two tiles, wave 1 — which has no pose or x[U] to do
+    // below — three (tiles 1, 5, 8); a wave's tiles interleaved as in the K' / M' phase.
+    auto ptiles = [&](auto ntc) {
+      constexpr int NT = decltype(ntc)::value;
+      double av[NT][8], bv[NT][8];
+      d4 acc[NT];
 #pragma unroll
-      for (int s0 = 0; s0 < 8; ++s0) {
-        av[s0] = -sh.pv.K[ar][4 * s0 + k4];
-        bv[s0] = sh.pv.M[4 * s0 + k4][cc];
-      }
-      d4 acc;
+      for (int q = 0; q < NT; ++q) {
+        const int tt = q < 2 ? wv + 4 * q : 8;
+        const int ti = tt / 3, tj = tt % 3;
+        const int col = 16 * tj + i16, ar = min(16 * ti + i16, kMaxU - 1), cc = min(col, kMaxU - 1);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = min(16 * ti + k4 + 4 * r, kMaxU - 1);
-        acc[r] = P[row][cc];
+        for (int s0 = 0; s0 < 8; ++s0) {
+          av[q][s0] = -sh.pv.K[ar][4 * s0 + k4];
+          bv[q][s0] = sh.pv.M[4 * s0 + k4][cc];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = min(16 * ti + k4 + 4 * r, kMaxU - 1);
+          acc[q][r] = P[row][cc];
+        }
       }
 #pragma unroll
       for (int s0 = 0; s0 < 8; ++s0)
-        if (4 * s0 < zc) acc = mfma_f64(av[s0], bv[s0], acc);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * ti + k4 + 4 * r;
-        if (row < nu && col < nu) P[row][col] = acc[r];
+        for (int q = 0; q < NT; ++q) acc[q] = mfma_f64(av[q][s0], bv[q][s0], acc[q]);
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int tt = q < 2 ? wv + 4 * q : 8;
+        const int ti = tt / 3, tj = tt % 3;
+        const int col = 16 * tj + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * ti + k4 + 4 * r;
+          if (row < nu && col < nu) P[row][col] = acc[q][r];
+        }
       }
-    }
+    };
+    if (wv == 1)
+      ptiles(std::integral_constant<int, 3>{});
+    else
+      ptiles(std::integral_constant<int, 2>{});
     EKF_STAMPT(10, 64);
     EKF_STAMPT(11, 128);
     EKF_STAMPT(13, 192);
-    // waves 2 and 3 (two P tiles against wave 0's three): the predicted pose and x_in[U]
+    // waves 2 and 3 (two P tiles against wave 1's three): the predicted pose and x_in[U]
     if (wv == 2 && ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
       double a1, a2;
       const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
