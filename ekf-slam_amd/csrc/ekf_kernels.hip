@@ -173,6 +173,8 @@ struct ChainShared {
   double junk2[64][2];
   double pose[3];
   double xpose[3];  // x_in pose (posterior of the previous chunk)
+  double npose[3], na1, na2;  // the next chunk's predicted pose and At entries (wave 3, ahead)
+  int npose_ci;               // the chunk index they belong to (−1: none)
   double tmo[3];    // t_map_odom
   double a1, a2, s00;
   int nu_cnt;
@@ -821,6 +823,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // so padding rows / columns that feed MFMA or dot products as zeros really are zeros
   for (int e = tid; e < static_cast<int>(sizeof(ChainShared) / 8); e += blockDim.x)
     reinterpret_cast<double*>(&sh)[e] = 0.0;
+  if (tid == 0) sh.npose_ci = -1;  // (ordered before its first reader by the chunk loop's barriers)
   bool pre = false;        // sdesc[ci & 1] was prefetched by the previous chunk's epilogue
   unsigned pending = 0;    // chain epoch of the previous chunk, not yet published (its record
                            // stores are still in flight; see the epilogue)
@@ -1103,15 +1106,16 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
     // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4m')
     // (every k-step runs: K' columns and M' rows beyond the chunk's rank are zero, so their MFMAs
-    // add exact zeros.) Waves 0, 2 and 3 take two tiles, wave 1 — which has no pose or x[U] to do
-    // below — three (tiles 1, 5, 8); a wave's tiles interleaved as in the K' / M' phase.
+    // add exact zeros.) Waves 0 and 1 take three tiles (0, 4, 7 and 1, 5, 8), wave 2 — which sets
+    // the predicted pose below — two (2, 6), wave 3 — x[U] below — one (3); a wave's tiles
+    // interleaved as in the K' / M' phase.
     auto ptiles = [&](auto ntc) {
       constexpr int NT = decltype(ntc)::value;
       double av[NT][8], bv[NT][8];
       d4 acc[NT];
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
-        const int tt = q < 2 ? wv + 4 * q : 8;
+        const int tt = q < 2 ? wv + 4 * q : 7 + wv;
         const int ti = tt / 3, tj = tt % 3;
         const int col = 16 * tj + i16, ar = min(16 * ti + i16, kMaxU - 1), cc = min(col, kMaxU - 1);
 #pragma unroll
@@ -1131,7 +1135,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         for (int q = 0; q < NT; ++q) acc[q] = mfma_f64(av[q][s0], bv[q][s0], acc[q]);
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
-        const int tt = q < 2 ? wv + 4 * q : 8;
+        const int tt = q < 2 ? wv + 4 * q : 7 + wv;
         const int ti = tt / 3, tj = tt % 3;
         const int col = 16 * tj + i16;
 #pragma unroll
@@ -1141,20 +1145,30 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
       }
     };
-    if (wv == 1)
+    if (wv < 2)
       ptiles(std::integral_constant<int, 3>{});
-    else
+    else if (wv == 2)
       ptiles(std::integral_constant<int, 2>{});
+    else
+      ptiles(std::integral_constant<int, 1>{});
     EKF_STAMPT(10, 64);
     EKF_STAMPT(11, 128);
     EKF_STAMPT(13, 192);
-    // waves 2 and 3 (two P tiles against wave 1's three): the predicted pose and x_in[U]
+    // waves 2 and 3 (fewer P tiles): the predicted pose and x_in[U]
     if (wv == 2 && ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
-      double a1, a2;
-      const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
-      predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
-      sh.a1 = a1;
-      sh.a2 = a2;
+      if (sh.npose_ci == ci) {  // computed ahead by the chunk before (wave 3)
+        sh.pose[0] = sh.npose[0];
+        sh.pose[1] = sh.npose[1];
+        sh.pose[2] = sh.npose[2];
+        sh.a1 = sh.na1;
+        sh.a2 = sh.na2;
+      } else {
+        double a1, a2;
+        const double xp[3] = {sh.pv.xU[0], sh.pv.xU[1], sh.pv.xU[2]};
+        predicted_pose(sh.tmo, d, xp, sh.pose, &a1, &a2);
+        sh.a1 = a1;
+        sh.a2 = a2;
+      }
       EKF_STAMPT(8, 128);
     }
     if (wv == 3) {
@@ -1331,6 +1345,29 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       sh.tmo[0] = tmo.theta;
       sh.tmo[1] = tmo.x;
       sh.tmo[2] = tmo.y;
+    }
+    // ... and the next chunk's predicted pose (slam.cpp:184-196), beside waves 1–2's last Z / Y
+    // instead of in its prologue: its inputs are this chunk's final pose (the record's x[U] there,
+    // which the next chunk would read), the t_map_odom after this chunk (the word it would load)
+    // and its descriptor's odometry — the same values, so the same bits
+    if (lane == 0 && ci + 1 < nchunks) {
+      const MsgDesc& nd = A.desc[static_cast<size_t>(ci + 1) * A.desc_stride + fy];
+      const int nfl = nd.flags;
+      const double od[3] = {nd.odom[0], nd.odom[1], nd.odom[2]};
+      if ((nfl & kActive) && (nfl & kLook) && !A.gather) {
+        lds_wait_ge(&sh.pub, m);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const double xp[3] = {sh.xU[0][0], sh.xU[0][1], sh.xU[0][2]};
+        const double tm[3] = {sh.tmo[0], sh.tmo[1], sh.tmo[2]};
+        double np_[3], a1, a2;
+        predicted_pose(tm, nfl, od, xp, np_, &a1, &a2);
+        sh.npose[0] = np_[0];
+        sh.npose[1] = np_[1];
+        sh.npose[2] = np_[2];
+        sh.na1 = a1;
+        sh.na2 = a2;
+        sh.npose_ci = ci + 1;
+      }
     }
   } else if (wave == 1) {  // Z_c: K_c[i] = r_0(i)·Z_c for every row i
     // Σ_c[i, pA_c] = r_0(i)·(E_c − Σ_{k<c} Z_k·M_k[:, pA_c]) (E_c selects the positions pA_c), so

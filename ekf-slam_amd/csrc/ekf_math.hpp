@@ -17,12 +17,12 @@ __device__ __forceinline__ double alpha_of(int idx, double a1, double a2) {
 
 // Predicted pose and the two nonzeros of At (slam.cpp:184-196). xin = posterior of the last
 // message = filter_previous_configuration (slam.cpp:291).
-__device__ __forceinline__ void predicted_pose(const double* tmo, const MsgDesc& d,
+__device__ __forceinline__ void predicted_pose(const double* tmo, int flags, const double* odom,
                                                const double* xin, double* pose, double* a1,
                                                double* a2) {
-  if (d.flags & kFirst) {
+  if (flags & kFirst) {
     const Pose2 cur = compose(Pose2{tmo[0], tmo[1], tmo[2]},
-                              Pose2{d.odom[0], d.odom[1], d.odom[2]});
+                              Pose2{odom[0], odom[1], odom[2]});
     *a1 = -(cur.y - xin[2]);
     *a2 = cur.x - xin[1];
     pose[0] = normalize_angle(cur.theta);
@@ -35,6 +35,11 @@ __device__ __forceinline__ void predicted_pose(const double* tmo, const MsgDesc&
     pose[1] = xin[1];
     pose[2] = xin[2];
   }
+}
+__device__ __forceinline__ void predicted_pose(const double* tmo, const MsgDesc& d,
+                                               const double* xin, double* pose, double* a1,
+                                               double* a2) {
+  predicted_pose(tmo, d.flags, d.odom, xin, pose, a1, a2);
 }
 
 // 1/x and 1/√x from the hardware estimate plus two Newton steps (≤ 1 ulp; the f64 division
