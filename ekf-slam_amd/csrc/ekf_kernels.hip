@@ -1041,24 +1041,25 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     __syncthreads();
     EKF_STAMP(3);
     EKF_STAMP(4);
-    // K' (48×32: 6 tiles of R·Z') and M' (32×48: 6 tiles of Y'·C) on f64 MFMA, 12 tiles, three per
-    // wave. Operand reads are unconditional (clamped rows / columns feed only discarded outputs,
-    // k ≥ |U'| is zero-padded in both operands, so every k-step runs: its MFMA adds exact zeros).
-    // The wave's three tiles are one basic block — every operand read issued first (a row / column
-    // pointer and stride per tile instead of a branch), then three interleaved accumulation chains:
-    // the MFMA pipe, not each tile's read latency and dependent chain in turn, sets the time.
-    {
-      double av[3][9], bv[3][9];
+    // K' = R·Z' (35 × 32) and M' = Y'·C (32 × 35) on f64 MFMA. Their 32 × 32 cores are 8 tiles,
+    // two per wave; the 3-wide bands K'[32..34][·] and M'[·][32..34] (16 × 16 tiles there would be
+    // 13/16 padding) are VALU dot products, one output per thread of waves 0–2, and wave 3 forms
+    // x_in[U] instead. Operand reads are unconditional (clamped rows / columns feed only discarded
+    // outputs, k ≥ |U'| is zero-padded in both operands, so every k-step runs: its MFMA adds exact
+    // zeros). A wave's tiles and its VALU work are one basic block (operand reads first, then two
+    // interleaved accumulation chains beside the dot product): the MFMA and VALU pipes overlap.
+    auto kmphase = [&](auto w3c) {
+      constexpr bool W3 = decltype(w3c)::value;
+      double av[2][9], bv[2][9];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int tt = wv + 4 * q;
-        const bool kt = tt < 6;
-        const int ti = kt ? tt >> 1 : (tt - 6) / 3, tj = kt ? tt & 1 : (tt - 6) % 3;
-        const int ar = min(16 * ti + i16, kMaxU - 1), bc = min(16 * tj + i16, kMaxU - 1);
-        // A: K' tile R[ar][k], M' tile Y'[row][k] (k contiguous); B: Z'[k][col] (stride kZC + 1) or
-        // C[k][bc] (stride kMaxU + 1)
-        const double* pa = kt ? &sh.pv.R[ar][0] : &sh.pv.Y[16 * ti + i16][0];
-        const double* pb = kt ? &sh.pv.Z[0][16 * tj + i16] : &sh.pv.C[0][bc];
+      for (int q = 0; q < 2; ++q) {
+        const int tt = wv + 4 * q;  // 0..3 K' tiles, 4..7 M' tiles
+        const bool kt = tt < 4;
+        const int ti = (kt ? tt : tt - 4) >> 1, tj = (kt ? tt : tt - 4) & 1;
+        // A: R[row][k] (K') or Y'[row][k] (M'), k contiguous; B: Z'[k][col] (stride kZC + 1) or
+        // C[k][col] (stride kMaxU + 1)
+        const double* pa = kt ? &sh.pv.R[16 * ti + i16][0] : &sh.pv.Y[16 * ti + i16][0];
+        const double* pb = kt ? &sh.pv.Z[0][16 * tj + i16] : &sh.pv.C[0][16 * tj + i16];
         const int sb = kt ? kZC + 1 : kMaxU + 1;
 #pragma unroll
         for (int s0 = 0; s0 < 9; ++s0) {
@@ -1066,29 +1067,68 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           bv[q][s0] = pb[(4 * s0 + k4) * sb];
         }
       }
-      d4 acc[3] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+      // the VALU share: a band output (waves 0–2) or x_in[U] (wave 3)
+      double bacc[4] = {0.0, 0.0, 0.0, 0.0};
+      int brow = 0, bcol = 0;
+      bool bk = false;
+      double xres = 0.0;
+      if (!W3) {
+        if (tid < 96) {  // K'[32 + t/32][t%32] = R[row]·Z'[:, col]
+          bk = true;
+          brow = 32 + (tid >> 5);
+          bcol = tid & 31;
+        } else {  // M'[u/3][32 + u%3] = Y'[row]·C[:, col]
+          const int u = tid - 96;
+          brow = u / 3;
+          bcol = 32 + (u - 3 * (u / 3));
+        }
+        const double* ra = bk ? &sh.pv.R[min(brow, kMaxU - 1)][0] : &sh.pv.Y[brow][0];
+        const double* cb = bk ? &sh.pv.Z[0][bcol] : &sh.pv.C[0][min(bcol, kMaxU)];
+        const int sc = bk ? kZC + 1 : kMaxU + 1;
+#pragma unroll
+        for (int k = 0; k < kMaxU + 1; ++k) bacc[k & 3] = fma(ra[k], cb[k * sc], bacc[k & 3]);
+      } else {
+        // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
+        const int l = ln < kMaxU ? ln : kMaxU - 1;
+        const int u = sh.u[l];
+        int pos = -1;
+#pragma unroll
+        for (int k = kMaxU - 1; k >= 0; --k) pos = (k < np && sh.pv.u[k] == u) ? k : pos;
+#pragma unroll
+        for (int k = 0; k < kMaxU; ++k) bacc[k & 3] = fma(sh.pv.R[l][k], sh.pv.Zx[k], bacc[k & 3]);
+        const double r = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);  // R[·][k ≥ |U'|] = 0
+        xres = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[l] + r;
+      }
+      d4 acc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
 #pragma unroll
       for (int s0 = 0; s0 < 9; ++s0)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) acc[q] = mfma_f64(av[q][s0], bv[q][s0], acc[q]);
+        for (int q = 0; q < 2; ++q) acc[q] = mfma_f64(av[q][s0], bv[q][s0], acc[q]);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < 2; ++q) {
         const int tt = wv + 4 * q;
-        const bool kt = tt < 6;
-        const int ti = kt ? tt >> 1 : (tt - 6) / 3, tj = kt ? tt & 1 : (tt - 6) % 3;
-        if (kt) {
+        const bool kt = tt < 4;
+        const int ti = (kt ? tt : tt - 4) >> 1, tj = (kt ? tt : tt - 4) & 1;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = 16 * ti + k4 + 4 * r;
-            if (row < kMaxU) sh.pv.K[row][16 * tj + i16] = acc[q][r];
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (16 * tj + i16 < kMaxU) sh.pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[q][r];
+        for (int r = 0; r < 4; ++r) {
+          const double v = acc[q][r];
+          if (kt) sh.pv.K[16 * ti + k4 + 4 * r][16 * tj + i16] = v;
+          else sh.pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = v;
         }
       }
-    }
+      if (!W3) {
+        const double v = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
+        if (bk) sh.pv.K[brow][bcol] = v;
+        else if (bcol < kMaxU) sh.pv.M[brow][bcol] = v;
+      } else {
+        if (ln < nu) sh.xU[0][ln] = xres;
+        if (ln < 3) sh.xpose[ln] = sh.pv.xU[ln];  // pose ∈ U' always
+      }
+    };
+    if (wv == 3)
+      kmphase(std::true_type{});
+    else
+      kmphase(std::false_type{});
     EKF_STAMP(7);
     __syncthreads();
     EKF_STAMP(5);
@@ -1106,55 +1146,43 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
     // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4m')
     // (every k-step runs: K' columns and M' rows beyond the chunk's rank are zero, so their MFMAs
-    // add exact zeros.) Waves 0 and 1 take three tiles (0, 4, 7 and 1, 5, 8), wave 2 — which sets
-    // the predicted pose below — two (2, 6), wave 3 — x[U] below — one (3); a wave's tiles
-    // interleaved as in the K' / M' phase.
-    auto ptiles = [&](auto ntc) {
-      constexpr int NT = decltype(ntc)::value;
-      double av[NT][8], bv[NT][8];
-      d4 acc[NT];
+    // add exact zeros.) The 32 × 32 core of P on MFMA, one 16 × 16 tile per wave; the 3-wide bands
+    // (rows 32..34 and columns 32..34, 201 entries) as VALU dot products, one per thread, in the same
+    // basic block.
+    {
+      const int ti = wv >> 1, tj = wv & 1;
+      const int col = 16 * tj + i16, ar = 16 * ti + i16;
+      double av[8], bv[8];
 #pragma unroll
-      for (int q = 0; q < NT; ++q) {
-        const int tt = q < 2 ? wv + 4 * q : 7 + wv;
-        const int ti = tt / 3, tj = tt % 3;
-        const int col = 16 * tj + i16, ar = min(16 * ti + i16, kMaxU - 1), cc = min(col, kMaxU - 1);
-#pragma unroll
-        for (int s0 = 0; s0 < 8; ++s0) {
-          av[q][s0] = -sh.pv.K[ar][4 * s0 + k4];
-          bv[q][s0] = sh.pv.M[4 * s0 + k4][cc];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = min(16 * ti + k4 + 4 * r, kMaxU - 1);
-          acc[q][r] = P[row][cc];
-        }
+      for (int s0 = 0; s0 < 8; ++s0) {
+        av[s0] = -sh.pv.K[ar][4 * s0 + k4];
+        bv[s0] = sh.pv.M[4 * s0 + k4][col];
       }
+      d4 acc;
 #pragma unroll
-      for (int s0 = 0; s0 < 8; ++s0)
+      for (int r = 0; r < 4; ++r) acc[r] = P[16 * ti + k4 + 4 * r][col];
+      // band entry: t < 105 → rows 32..34 × columns 0..34, then rows 0..31 × columns 32..34
+      const int t = tid < 201 ? tid : 200;
+      const int brow = t < 105 ? 32 + t / 35 : (t - 105) / 3;
+      const int bcol = t < 105 ? t - 35 * (t / 35) : 32 + (t - 105) - 3 * ((t - 105) / 3);
+      const int br = min(brow, kMaxU - 1), bc = min(bcol, kMaxU - 1);
+      double bs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < NT; ++q) acc[q] = mfma_f64(av[q][s0], bv[q][s0], acc[q]);
+      for (int k = 0; k < kZC; ++k) bs[k & 3] = fma(sh.pv.K[br][k], sh.pv.M[k][bc], bs[k & 3]);
+      const double bv0 = P[br][bc];
 #pragma unroll
-      for (int q = 0; q < NT; ++q) {
-        const int tt = q < 2 ? wv + 4 * q : 7 + wv;
-        const int ti = tt / 3, tj = tt % 3;
-        const int col = 16 * tj + i16;
+      for (int s0 = 0; s0 < 8; ++s0) acc = mfma_f64(av[s0], bv[s0], acc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * ti + k4 + 4 * r;
-          if (row < nu && col < nu) P[row][col] = acc[q][r];
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * ti + k4 + 4 * r;
+        if (row < nu && col < nu) P[row][col] = acc[r];
       }
-    };
-    if (wv < 2)
-      ptiles(std::integral_constant<int, 3>{});
-    else if (wv == 2)
-      ptiles(std::integral_constant<int, 2>{});
-    else
-      ptiles(std::integral_constant<int, 1>{});
+      if (tid < 201 && brow < nu && bcol < nu) P[brow][bcol] = bv0 - ((bs[0] + bs[1]) + (bs[2] + bs[3]));
+    }
     EKF_STAMPT(10, 64);
     EKF_STAMPT(11, 128);
     EKF_STAMPT(13, 192);
-    // waves 2 and 3 (fewer P tiles): the predicted pose and x_in[U]
+    // wave 2: the predicted pose
     if (wv == 2 && ln == 0) {  // the predicted pose (slam.cpp:184-196) from x' of the pose
       if (sh.npose_ci == ci) {  // computed ahead by the chunk before (wave 3)
         sh.pose[0] = sh.npose[0];
@@ -1171,24 +1199,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       }
       EKF_STAMPT(8, 128);
     }
-    if (wv == 3) {
-      if (ln < nu) {  // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
-        const int u = sh.u[ln];
-        int pos = -1;
-#pragma unroll
-        for (int k = kMaxU - 1; k >= 0; --k) {
-          const bool hit = k < np && sh.pv.u[k] == u;
-          pos = hit ? k : pos;
-        }
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};  // four partial sums (k mod 4): a 9-deep chain
-#pragma unroll
-        for (int k = 0; k < kMaxU; ++k) acc[k & 3] = fma(sh.pv.R[ln][k], sh.pv.Zx[k], acc[k & 3]);
-        const double r = (acc[0] + acc[1]) + (acc[2] + acc[3]);  // R[·][k ≥ |U'|] = 0
-        sh.xU[0][ln] = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[ln] + r;
-      }
-      if (ln < 3) sh.xpose[ln] = sh.pv.xU[ln];  // pose ∈ U' always
-      EKF_STAMPT(9, 192);
-    }
+    EKF_STAMPT(9, 192);  // (x_in[U]: wave 3 in the K' / M' phase)
   } else {
     double vd[kPer];
 #pragma unroll
