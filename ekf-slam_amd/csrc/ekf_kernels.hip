@@ -521,9 +521,8 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
 // The previous chunk's predict on the gathered rebuild operands: v + α_i·Σ[0][j] +
 // (Σ[i][0] + α_i·Σ00)·α_j + Q̄, for D = Σ_in'[U, U] → P, R = Σ_in'[U, U'] → pv.R and
 // C = Σ_in'[U', U] → pv.C (R / C columns k ≥ |U'| up to 36 zeroed: MFMA k padding). Thread tid's
-// entries e = tid + i·256 of the 36 × 36 block. k_chain's prologue and the builder both run it, so
-// their blocks agree bit for bit. Reads sh.u (U), sh.pv.u (U'), the staged row 0 / column 0
-// (pv.r0U, c0U, r0P, c0P) and the previous predict (pv.first, a1, a2).
+// entries e = tid + i·256 of the 36 × 36 block. Reads sh.u (U), sh.pv.u (U'), the staged row 0 /
+// column 0 (pv.r0U, c0U, r0P, c0P) and the previous predict (pv.first, a1, a2).
 constexpr int kChainThreads = 256;
 constexpr int kRebW = kMaxU + 1;                                      // 36: entry e = a·36 + b
 constexpr int kRebPer = (kRebW * kRebW + kChainThreads - 1) / kChainThreads;  // 6
@@ -565,35 +564,62 @@ __device__ __forceinline__ void rebuild_rcd(ChainShared& sh, double (&P)[kMaxU][
     }
   }
   if (sh.pv.first == 0) return;  // (uniform)
-  // the previous chunk's predict on its special entries only (the others it leaves as they are)
-  lds_barrier();
+  // The previous predict on the special entries, by the thread that gathered them (its raw values
+  // are in registers, so no barrier): a thread's entries e = tid + 256·i have b = (tid % 36 + 4·i)
+  // mod 36, so besides position 0 (rows 1, 2 are e ∈ [36, 108); (0, 0) is e = 0) at most one
+  // position ic ≥ 1 falls in column 1 or 2. Both are rewritten over the raw stores above (same
+  // thread, same address: LDS order), with one wait for all operand reads and no branch.
+  const int r = tid % kW;
+  int ic = 0;
+#pragma unroll
+  for (int i = 1; i < kPer; ++i) {
+    const int bb = (r + 4 * i) % kW;
+    ic = (bb == 1 || bb == 2) && tid + i * kChainThreads < kW * kW ? i : ic;
+  }
+  double sv[2][3];
+  sv[0][0] = static_cast<double>(vd[0]);
+  sv[0][1] = static_cast<double>(vr[0]);
+  sv[0][2] = static_cast<double>(vc[0]);
+  sv[1][0] = sv[1][1] = sv[1][2] = 0.0;
+#pragma unroll
+  for (int i = 1; i < kPer; ++i) {
+    sv[1][0] = ic == i ? static_cast<double>(vd[i]) : sv[1][0];
+    sv[1][1] = ic == i ? static_cast<double>(vr[i]) : sv[1][1];
+    sv[1][2] = ic == i ? static_cast<double>(vc[i]) : sv[1][2];
+  }
   const double s00 = sh.pv.r0U[0], qa1 = sh.pv.a1, qa2 = sh.pv.a2;
-  for (int s = tid; s < 3 * kSpec; s += kChainThreads) {
-    const int blk = s >= 2 * kSpec ? 2 : (s >= kSpec ? 1 : 0);
-    int a, b;
-    special_entry(s - blk * kSpec, a, b);
-    if (a >= nu) continue;
-    const double ai = alpha_of(a, qa1, qa2);
-    if (blk == 0) {  // D = Σ_in'[U, U] → P
-      if (b >= nu) continue;
-      const double aj = alpha_of(b, qa1, qa2);
-      double v = P[a][b];
-      v = v + ai * sh.pv.r0U[b];
-      v = v + (sh.pv.c0U[a] + ai * s00) * aj;
-      P[a][b] = (a == b && a < 3) ? v + q : v;
-    } else if (b < np) {  // b = k over U'
-      const double ak = alpha_of(b, qa1, qa2);
-      const bool qd = a == b && a < 3;
-      if (blk == 1) {  // R = Σ_in'[U, U']
-        double v2 = sh.pv.R[a][b] + ai * sh.pv.r0P[b];
-        v2 = v2 + (sh.pv.c0U[a] + ai * s00) * ak;
-        sh.pv.R[a][b] = qd ? v2 + q : v2;
-      } else {  // C = Σ_in'[U', U]
-        double w2 = sh.pv.C[b][a] + ak * sh.pv.r0U[a];
-        w2 = w2 + (sh.pv.c0P[b] + ak * s00) * ai;
-        sh.pv.C[b][a] = qd ? w2 + q : w2;
-      }
-    }
+  int pa[2], pb[2];
+  bool sp[2];
+  double r0u_b[2], c0u_a[2], r0p_b[2], r0u_a[2], c0p_b[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int e = tid + (j ? ic : 0) * kChainThreads;
+    const int a = e / kW, b = e % kW;
+    pa[j] = a;
+    pb[j] = b;
+    sp[j] = j ? ic > 0 : (a == 1 || a == 2 || b == 1 || b == 2 || e == 0);
+    const int ac = min(a, kMaxU - 1), bc = min(b, kMaxU - 1);
+    r0u_b[j] = sh.pv.r0U[bc];
+    c0u_a[j] = sh.pv.c0U[ac];
+    r0p_b[j] = sh.pv.r0P[bc];
+    r0u_a[j] = sh.pv.r0U[ac];
+    c0p_b[j] = sh.pv.c0P[bc];
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int a = pa[j], b = pb[j];
+    const double ai = alpha_of(a, qa1, qa2), aj = alpha_of(b, qa1, qa2);
+    const bool qd = a == b && a < 3;
+    double v = sv[j][0] + ai * r0u_b[j];  // D = Σ_in'[U, U] → P
+    v = v + (c0u_a[j] + ai * s00) * aj;
+    double v2 = sv[j][1] + ai * r0p_b[j];  // R = Σ_in'[U, U'] (b = k over U')
+    v2 = v2 + (c0u_a[j] + ai * s00) * aj;
+    double w2 = sv[j][2] + aj * r0u_a[j];  // C = Σ_in'[U', U]
+    w2 = w2 + (c0p_b[j] + aj * s00) * ai;
+    const bool okd = sp[j] && a < nu && b < nu, okr = sp[j] && a < nu && b < np;
+    *(okd ? &P[a][b] : &sh.junk[0][tid & 63]) = qd ? v + q : v;
+    *(okr ? &sh.pv.R[a][b] : &sh.junk[1][tid & 63]) = qd ? v2 + q : v2;
+    *(okr ? &sh.pv.C[b][a] : &sh.junk[2][tid & 63]) = qd ? w2 + q : w2;
   }
 }
 
@@ -1263,6 +1289,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   __syncthreads();
   EKF_STAMP(2);
   EKF_DUMP_BLOCK(seq);
+  EKF_STAMP(18);
 
   // ---- A2: the m corrections -----------------------------------------------------------------
   // The dependent chain (ẑ, H, S⁻¹, ν → K, M, x → next marker) runs on wave 0 alone, with no
@@ -1287,6 +1314,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     if (tid == 0) epoch_store(A.sync + kSyncChain + f, pending);
     pending = 0;
   }
+  EKF_STAMP(19);
   if (wave == 0) {
     if (joseph)
       chain_wave0<true>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq);

@@ -63,10 +63,12 @@ names = {14: "A0: early loads issued", 1: "A0", 21: "kLook: loads landed", 3: "k
          7: "kLook: K', M' tiles", 5: "kLook: x[U]", 6: "A1 done (P tiles)",
          2: "predict (steps start)", 12: "steps+final pass", 16: "epi: rec stores issued",
          40: "chunk end", 10: "  wave1 P tiles done", 11: "  wave2 P tiles done",
-         13: "  wave3 P tiles done", 8: "  wave2 predicted pose", 9: "  wave3 x[U]"}
+         13: "  wave3 P tiles done", 8: "  wave2 predicted pose", 9: "  wave3 x[U]",
+         15: "  raw R, C, D stored", 17: "  (prev predict barrier)", 18: "  (diag block dump)",
+         19: "  drain + barrier, wave 0 enters"}
 print(f"N={N} {DT}, chunk {-1 - int(os.environ.get('WHICH', '1'))} of {T} messages (cycles from "
       f"the chunk's stamp 0); chunk starts of the ring, relative: {sorted(ring[:, 0] - ring[:, 0].min())}")
-for k in (14, 1, 21, 3, 7, 5, 10, 11, 13, 8, 9, 6, 2, 12, 16, 40):
+for k in (14, 1, 21, 15, 17, 3, 7, 5, 10, 11, 13, 8, 9, 6, 2, 18, 19, 12, 16, 40):
     print(f"{names[k]:24s} {s[k] - t0:8d}")
 m = int(sc.count[w + T - 1 - int(os.environ.get("WHICH", "1"))])
 steps = [int(s[64 + 8 * c] - t0) for c in range(m)]
