@@ -1479,8 +1479,26 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           z0 = pos == a ? G0[a] : z0;
           z1 = pos == a ? G1[a] : z1;
         }
-#pragma unroll 4
-        for (int k = 0; k < c; ++k) {
+        // the history in groups of 4 terms: a group's 12 LDS reads are issued together and
+        // waited for once (one term per read-wait-FMA round trip was ≈ 135 cycles)
+        int k = 0;
+        for (; k + 4 <= c; k += 4) {
+          double zz[4][2], cz[4][4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            zz[q][0] = sh.Z[li][2 * (k + q)];
+            zz[q][1] = sh.Z[li][2 * (k + q) + 1];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cz[q][e] = sh.Cz[k + q][e];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            z0 = fma(-zz[q][1], cz[q][2], fma(-zz[q][0], cz[q][0], z0));
+            z1 = fma(-zz[q][1], cz[q][3], fma(-zz[q][0], cz[q][1], z1));
+          }
+        }
+        for (; k < c; ++k) {
           const double zk0 = sh.Z[li][2 * k], zk1 = sh.Z[li][2 * k + 1];
           const double c00 = sh.Cz[k][0], c01 = sh.Cz[k][1], c10 = sh.Cz[k][2], c11 = sh.Cz[k][3];
           z0 = fma(-zk1, c10, fma(-zk0, c00, z0));
@@ -1668,8 +1686,27 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           y0 = pos == a ? H0[a] : y0;
           y1 = pos == a ? H1[a] : y1;
         }
+        int k0 = 0;
+        if (!joseph) {  // (uniform) groups of 4 terms, reads issued together (as wave 1's Z)
+          for (; k0 + 4 <= c; k0 += 4) {
+            double yy[4][2], dy[4][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              yy[q][0] = sh.Y[2 * (k0 + q)][lj];
+              yy[q][1] = sh.Y[2 * (k0 + q) + 1][lj];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) dy[q][e] = sh.Dy[k0 + q][e];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              y0 = fma(-dy[q][1], yy[q][1], fma(-dy[q][0], yy[q][0], y0));
+              y1 = fma(-dy[q][3], yy[q][1], fma(-dy[q][2], yy[q][0], y1));
+            }
+          }
+        }
 #pragma unroll 4
-        for (int k = 0; k < c; ++k) {
+        for (int k = k0; k < c; ++k) {
           const double yk0 = sh.Y[2 * k][lj], yk1 = sh.Y[2 * k + 1][lj];
           const double d00 = sh.Dy[k][0], d01 = sh.Dy[k][1], d10 = sh.Dy[k][2], d11 = sh.Dy[k][3];
           y0 = fma(-d01, yk1, fma(-d00, yk0, y0));
