@@ -563,6 +563,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
           rjk[t] = rjk[t] - (ea[4 + t] + eb[4 + t]);
         }
       }
+      AM_STAMP(c, 5);
 
       // ---- the step (slam.cpp:443-488), every lane the same: ẑ, H, S, S⁻¹, ν, K / M at the pose ----
       double zhat[2], H0[5], H1[5], braw;

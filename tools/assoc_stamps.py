@@ -36,9 +36,10 @@ for wg in range(2):
     t0 = int(st[wg, 16, 0])
     print(f"workgroup {'0' if wg == 0 else 'last'}: total {(int(st[wg, 16, 1]) - t0) / 100:.2f} us")
     for c in range(16):
-        s0, s1, s2, s3, s4 = (int(v) for v in st[wg, c, :5])
+        s0, s1, s2, s3, s4, s5 = (int(v) for v in st[wg, c, :6])
         if s0 == 0:
             continue
+        hist = f" (history sums {(s5 - s3) / 100:5.2f})" if s5 else ""
         print(f"  step {c:2d} at {(s0 - t0) / 100:7.2f}: score+argmin {(s1 - s0) / 100:6.2f} "
               f"exchange {(s2 - s1) / 100:6.2f} loads {(s3 - s2) / 100:6.2f} "
-              f"math {(s4 - s3) / 100:6.2f} us")
+              f"math {(s4 - s3) / 100:6.2f} us{hist}")
