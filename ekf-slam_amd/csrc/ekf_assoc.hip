@@ -62,9 +62,16 @@ __device__ unsigned long long g_am_stamps[2][kMaxChunk + 1][8];
 namespace {
 
 
+// Two waves per workgroup: wave 0 does everything below; wave 1 (history_helper) only sums each
+// step's history terms of the lanes' crosses with the step's landmark (Σ_c[k, j], Σ_c[j, k]) — the
+// even and odd steps in two fma chains, as wave 0 summed them alone before, so the same bits —
+// while wave 0 forms the step's pose-level quantities, which do not need them.
+constexpr int kAmThreads = 2 * kAmSlots;
+
 struct AmShared {
-  alignas(16) double hkm[kMaxChunk][kAmSlots][8];  // this wave's K_c[k] (0..3) and M_c[:, k] (4..7), by lane:
+  alignas(16) double hkm[kMaxChunk][kAmSlots][8];  // wave 0's K_c[k] (0..3) and M_c[:, k] (4..7), by lane:
                                        // a lane's step in 64 contiguous bytes (ds_read_b128 × 4)
+  double es[8][kAmSlots];             // wave 1's history sums of the current step, by lane
   double jh[kMaxChunk][8];            // the step's landmark: K (0..3) and M (4..7) of every step
   double jc[18];                      // its block and state (AmCur, x included)
   double pb[kMaxChunk][18];           // fp32 patch: every marker's landmark's final block
@@ -305,10 +312,60 @@ __device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, b
   return all;
 }
 
+// One history term of a lane's crosses with the step's landmark j: acc[0..3] += K_cc[k]·M_cc[:, j],
+// acc[4..7] += K_cc[j]·M_cc[:, k] (slam.cpp:264-265's rank-2 terms at (k, j) and (j, k)).
+__device__ __forceinline__ void hist_term(const AmShared& sh, int cc, int lane, double (&acc)[8]) {
+  const double* jk = sh.jh[cc];
+  const double* jm = sh.jh[cc] + 4;
+  const double2* hl = reinterpret_cast<const double2*>(sh.hkm[cc][lane]);
+  const double2 q0 = hl[0], q1 = hl[1], q2 = hl[2], q3 = hl[3];  // ds_read_b128 × 4
+  const double ok0 = q0.x, ok1 = q0.y, ok2 = q1.x, ok3 = q1.y;
+  const double om0 = q2.x, om1 = q2.y, om2 = q3.x, om3 = q3.y;
+  acc[0] = fma(ok1, jm[2], fma(ok0, jm[0], acc[0]));
+  acc[1] = fma(ok1, jm[3], fma(ok0, jm[1], acc[1]));
+  acc[2] = fma(ok3, jm[2], fma(ok2, jm[0], acc[2]));
+  acc[3] = fma(ok3, jm[3], fma(ok2, jm[1], acc[3]));
+  acc[4] = fma(jk[1], om2, fma(jk[0], om0, acc[4]));
+  acc[5] = fma(jk[1], om3, fma(jk[0], om1, acc[5]));
+  acc[6] = fma(jk[3], om2, fma(jk[2], om0, acc[6]));
+  acc[7] = fma(jk[3], om3, fma(jk[2], om1, acc[7]));
+}
+
+// Workgroup barrier ordering LDS only: the waves' global stores (tables, Kcat / Mcat rows) are not
+// waited for here (__syncthreads' workgroup fence would drain them at every step).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Wave 1: per step, after wave 0 has published j (sh.jl) and j's history (sh.jh) — barrier A — this
+// lane's sums Σ_cc<c K_cc[k]·M_cc[:, j] and K_cc[j]·M_cc[:, k] into sh.es, read by wave 0 after
+// barrier B. Both waves pass both barriers at every step, whatever the step decides. Two steps'
+// twelve LDS reads go out together (this wave holds few live registers, unlike wave 0).
+__device__ __forceinline__ void history_helper(AmShared& sh, int m, int k, int lane) {
+  for (int c = 0; c < m; ++c) {
+    lds_barrier();  // A
+    const int j = sh.jl[c];
+    double ea[8] = {0, 0, 0, 0, 0, 0, 0, 0}, eb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (j >= 0 && k != j) {
+      int cc = 0;
+      for (; cc + 1 < c; cc += 2) {
+        hist_term(sh, cc, lane, ea);
+        hist_term(sh, cc + 1, lane, eb);
+      }
+      if (cc < c) hist_term(sh, cc, lane, ea);
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) sh.es[t][lane] = ea[t] + eb[t];
+    lds_barrier();  // B
+  }
+}
+
 }  // namespace
 
 template <typename T>
-__global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B) {
+__global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs B) {
   __shared__ AmShared sh;
   const int G = B.G, fy = blockIdx.y;
   // XCD-local placement (B.xcd): the grid has 8 blocks per workgroup; filter fy's workgroups are
@@ -322,10 +379,14 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
   const int flags = d.flags;
   if (!(flags & kActive)) return;  // (every workgroup of the filter)
   const int f = A.f0 + fy;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (kAmSlots - 1);
   const int N = A.N, ld = A.ld, ldk = A.ldk;
   const int Np = G * kAmSlots;
   const int k = g * kAmSlots + lane;  // this lane's landmark slot
+  if (threadIdx.x >= kAmSlots) {  // wave 1: the odd history terms only (uniform per wave)
+    history_helper(sh, d.m, k, lane);
+    return;
+  }
   const bool valid = k < N;
   const int ix = 3 + 2 * (valid ? k : N - 1);  // its state index (clamped for the loads)
   const T* S = A.sig[d.parity] + f * A.sig_stride;
@@ -445,10 +506,11 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
     double Kk[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, Mk[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
     double Kp[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}}, Mp[2][3] = {{0.0, 0.0, 0.0},
                                                                          {0.0, 0.0, 0.0}};
+    // the new landmark's state (slam.cpp:351-354, the pose before this marker's correction)
+    double nx = 0.0, ny = 0.0;
+    double rkj[4] = {0.0, 0.0, 0.0, 0.0}, rjk[4] = {0.0, 0.0, 0.0, 0.0};
     if (j >= 0) {
       const int jx = 3 + 2 * j;
-      // the new landmark's state (slam.cpp:351-354, the pose before this marker's correction)
-      double nx = 0.0, ny = 0.0;
       if (isnew) {  // (uniform)
         nx = pose[1] + z0 * cos(z1 + pose[0]);
         ny = pose[2] + z0 * sin(z1 + pose[0]);
@@ -474,7 +536,6 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       // Σ_in crosses of this lane's slot with j (no predict term between landmarks)
       const T* q0 = S + static_cast<size_t>(ix) * ld;
       const T* p0 = S + static_cast<size_t>(jx) * ld;
-      double rkj[4], rjk[4];
       rkj[0] = static_cast<double>(q0[jx]);
       rkj[1] = static_cast<double>(q0[jx + 1]);
       rkj[2] = static_cast<double>(q0[ld + jx]);
@@ -510,11 +571,16 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
           sh.jh[cc][t] = sh.hkm[cc][lj][t];
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+    // ---- the step (slam.cpp:443-488): wave 0 forms what every lane shares (ẑ, H, S, S⁻¹, ν,
+    // K / M at the pose) while wave 1 (history_helper) sums this step's history terms of every
+    // lane's crosses with j, between barriers A and B (both waves pass both at every step) ----
+    lds_barrier();  // A: sh.jl[c], sh.jc and j's history sh.jh published to wave 1
+    AM_STAMP(c, 3);
+    double H0[5], H1[5], Si[4], nu0 = 0.0, nu1 = 0.0;
+    bool sok = false;
+    if (j >= 0) {
       double jkk[4], jkp[6], jpk[6], xj[2];
-      AM_STAMP(c, 3);
 #pragma unroll
       for (int t = 0; t < 4; ++t) jkk[t] = sh.jc[t];
 #pragma unroll
@@ -523,50 +589,7 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       for (int t = 0; t < 6; ++t) jpk[t] = sh.jc[10 + t];
       xj[0] = isnew ? nx : sh.jc[16];
       xj[1] = isnew ? ny : sh.jc[17];
-      // ---- this lane's slot: its crosses with j at step c (before the step's math, while few
-      // registers are live: the history sums then keep their LDS reads in flight) ----
-      if (k == j) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          rkj[t] = kk[t];
-          rjk[t] = kk[t];
-        }
-      } else {
-        // Σ_c[k, j] = Σ_p[k, j] − Σ_cc K_cc[k]·M_cc[:, j] and Σ_c[j, k] likewise, each sum in
-        // two interleaved fma chains (even / odd steps): half the dependent chain length
-        double ea[8] = {0, 0, 0, 0, 0, 0, 0, 0}, eb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        auto term = [&](int cc, double (&acc)[8]) __attribute__((always_inline)) {
-          const double* jk = sh.jh[cc];
-          const double* jm = sh.jh[cc] + 4;
-          const double2* hl = reinterpret_cast<const double2*>(sh.hkm[cc][lane]);
-          const double2 q0 = hl[0], q1 = hl[1], q2 = hl[2], q3 = hl[3];  // ds_read_b128 × 4
-          const double ok0 = q0.x, ok1 = q0.y, ok2 = q1.x, ok3 = q1.y;
-          const double om0 = q2.x, om1 = q2.y, om2 = q3.x, om3 = q3.y;
-          acc[0] = fma(ok1, jm[2], fma(ok0, jm[0], acc[0]));
-          acc[1] = fma(ok1, jm[3], fma(ok0, jm[1], acc[1]));
-          acc[2] = fma(ok3, jm[2], fma(ok2, jm[0], acc[2]));
-          acc[3] = fma(ok3, jm[3], fma(ok2, jm[1], acc[3]));
-          acc[4] = fma(jk[1], om2, fma(jk[0], om0, acc[4]));
-          acc[5] = fma(jk[1], om3, fma(jk[0], om1, acc[5]));
-          acc[6] = fma(jk[3], om2, fma(jk[2], om0, acc[6]));
-          acc[7] = fma(jk[3], om3, fma(jk[2], om1, acc[7]));
-        };
-        int cc = 0;
-        for (; cc + 1 < c; cc += 2) {
-          term(cc, ea);
-          term(cc + 1, eb);
-        }
-        if (cc < c) term(cc, ea);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          rkj[t] = rkj[t] - (ea[t] + eb[t]);
-          rjk[t] = rjk[t] - (ea[4 + t] + eb[4 + t]);
-        }
-      }
-      AM_STAMP(c, 5);
-
-      // ---- the step (slam.cpp:443-488), every lane the same: ẑ, H, S, S⁻¹, ν, K / M at the pose ----
-      double zhat[2], H0[5], H1[5], braw;
+      double zhat[2], braw;
       bool bok;
       range_bearing(pose, xj[0], xj[1], zhat, H0, H1, &braw, &bok);
       if (!bok) zhat[1] = normalize_angle(braw);
@@ -606,12 +629,12 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
       }
       Sm[0] += r_noise;
       Sm[3] += r_noise;
-      double Si[4];
-      if (!inv2(Sm, Si)) {
+      sok = inv2(Sm, Si);
+      if (!sok) {
         status |= EKF_FLAG_NUMERIC_D;  // Armadillo's inv throws; this marker is skipped
       } else {
-        const double nu0 = z0 - zhat[0];
-        const double nu1 = normalize_angle(z1 - zhat[1]);
+        nu0 = z0 - zhat[0];
+        nu1 = normalize_angle(z1 - zhat[1]);
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
           Kp[a][0] = Gt[a][0] * Si[0] + Gt[a][1] * Si[2];
@@ -628,6 +651,27 @@ __global__ __launch_bounds__(kAmSlots) void k_assoc_msg(PassArgs<T> A, AmArgs B)
           Mp[0][b] = m0;
           Mp[1][b] = m1;
         }
+      }
+    }
+    lds_barrier();  // B: wave 1's sums in sh.es
+    AM_STAMP(c, 5);
+    if (sok) {
+      // this lane's crosses with j at step c: Σ_c[k, j] = Σ_p[k, j] − Σ_cc K_cc[k]·M_cc[:, j] and
+      // Σ_c[j, k] likewise (the sums from wave 1)
+      if (k == j) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          rkj[t] = kk[t];
+          rjk[t] = kk[t];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          rkj[t] = rkj[t] - sh.es[t][lane];
+          rjk[t] = rjk[t] - sh.es[4 + t][lane];
+        }
+      }
+      {
         // ---- this lane's slot: K[k], M[:, k] from its crosses with j ----
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
@@ -915,17 +959,17 @@ hipError_t launch_assoc_msg(const PassArgs<T>& a, const AmArgs& b, int nf, hipSt
                             hipEvent_t e0, hipEvent_t e1) {
   const dim3 grid(b.xcd ? 8 * b.G : b.G, nf);
   if (e0 && e1)
-    hipExtLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmSlots), 0, s, e0, e1, 0, a, b);
+    hipExtLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmThreads), 0, s, e0, e1, 0, a, b);
   else
-    hipLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmSlots), 0, s, a, b);
+    hipLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmThreads), 0, s, a, b);
   return hipGetLastError();
 }
 
 int assoc_msg_blocks_per_cu(bool f32) {
   int nb = 0;
   const hipError_t e =
-      f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<float>, kAmSlots, 0)
-          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<double>, kAmSlots, 0);
+      f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<float>, kAmThreads, 0)
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<double>, kAmThreads, 0);
   return e == hipSuccess ? nb : 0;
 }
 
