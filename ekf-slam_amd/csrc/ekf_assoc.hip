@@ -62,16 +62,17 @@ __device__ unsigned long long g_am_stamps[2][kMaxChunk + 1][8];
 namespace {
 
 
-// Two waves per workgroup: wave 0 does everything below; wave 1 (history_helper) only sums each
-// step's history terms of the lanes' crosses with the step's landmark (Σ_c[k, j], Σ_c[j, k]) — the
-// even and odd steps in two fma chains, as wave 0 summed them alone before, so the same bits —
-// while wave 0 forms the step's pose-level quantities, which do not need them.
-constexpr int kAmThreads = 2 * kAmSlots;
+// Three waves per workgroup: wave 0 does everything below; waves 1 and 2 (history_helper) only sum
+// each step's history terms of the lanes' crosses with the step's landmark (Σ_c[k, j], Σ_c[j, k]),
+// the even steps' on wave 1 and the odd steps' on wave 2 — the two fma chains wave 0 interleaved
+// alone before, so the same bits — while wave 0 forms the step's pose-level quantities, which do
+// not need them.
+constexpr int kAmThreads = 3 * kAmSlots;
 
 struct AmShared {
   alignas(16) double hkm[kMaxChunk][kAmSlots][8];  // wave 0's K_c[k] (0..3) and M_c[:, k] (4..7), by lane:
                                        // a lane's step in 64 contiguous bytes (ds_read_b128 × 4)
-  double es[8][kAmSlots];             // wave 1's history sums of the current step, by lane
+  double es[2][8][kAmSlots];          // waves 1 / 2: the even / odd steps' history sums, by lane
   double jh[kMaxChunk][8];            // the step's landmark: K (0..3) and M (4..7) of every step
   double jc[18];                      // its block and state (AmCur, x included)
   double pb[kMaxChunk][18];           // fp32 patch: every marker's landmark's final block
@@ -313,14 +314,26 @@ __device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, b
 }
 
 // One history term of a lane's crosses with the step's landmark j: acc[0..3] += K_cc[k]·M_cc[:, j],
-// acc[4..7] += K_cc[j]·M_cc[:, k] (slam.cpp:264-265's rank-2 terms at (k, j) and (j, k)).
-__device__ __forceinline__ void hist_term(const AmShared& sh, int cc, int lane, double (&acc)[8]) {
-  const double* jk = sh.jh[cc];
-  const double* jm = sh.jh[cc] + 4;
+// acc[4..7] += K_cc[j]·M_cc[:, k] (slam.cpp:264-265's rank-2 terms at (k, j) and (j, k)). The
+// operands (this lane's history, 4 × ds_read_b128, and j's, broadcast) are loaded apart from the
+// fmas so that several terms' reads can be in flight together.
+struct HistOps {
+  double2 o[4], jv[4];
+};
+__device__ __forceinline__ void hist_load(const AmShared& sh, int cc, int lane, HistOps& p) {
   const double2* hl = reinterpret_cast<const double2*>(sh.hkm[cc][lane]);
-  const double2 q0 = hl[0], q1 = hl[1], q2 = hl[2], q3 = hl[3];  // ds_read_b128 × 4
-  const double ok0 = q0.x, ok1 = q0.y, ok2 = q1.x, ok3 = q1.y;
-  const double om0 = q2.x, om1 = q2.y, om2 = q3.x, om3 = q3.y;
+  const double2* jl = reinterpret_cast<const double2*>(sh.jh[cc]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p.o[i] = hl[i];
+    p.jv[i] = jl[i];
+  }
+}
+__device__ __forceinline__ void hist_fma(const HistOps& p, double (&acc)[8]) {
+  const double ok0 = p.o[0].x, ok1 = p.o[0].y, ok2 = p.o[1].x, ok3 = p.o[1].y;
+  const double om0 = p.o[2].x, om1 = p.o[2].y, om2 = p.o[3].x, om3 = p.o[3].y;
+  const double jk[4] = {p.jv[0].x, p.jv[0].y, p.jv[1].x, p.jv[1].y};
+  const double jm[4] = {p.jv[2].x, p.jv[2].y, p.jv[3].x, p.jv[3].y};
   acc[0] = fma(ok1, jm[2], fma(ok0, jm[0], acc[0]));
   acc[1] = fma(ok1, jm[3], fma(ok0, jm[1], acc[1]));
   acc[2] = fma(ok3, jm[2], fma(ok2, jm[0], acc[2]));
@@ -339,25 +352,36 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Wave 1: per step, after wave 0 has published j (sh.jl) and j's history (sh.jh) — barrier A — this
-// lane's sums Σ_cc<c K_cc[k]·M_cc[:, j] and K_cc[j]·M_cc[:, k] into sh.es, read by wave 0 after
-// barrier B. Both waves pass both barriers at every step, whatever the step decides. Two steps'
-// twelve LDS reads go out together (this wave holds few live registers, unlike wave 0).
-__device__ __forceinline__ void history_helper(AmShared& sh, int m, int k, int lane) {
+// Waves 1 (par 0) and 2 (par 1): per step, after wave 0 has published j (sh.jl) and j's history
+// (sh.jh) — barrier A — this lane's sums over the steps cc < c with cc ≡ par (mod 2) of
+// K_cc[k]·M_cc[:, j] and K_cc[j]·M_cc[:, k] into sh.es[par], read by wave 0 after barrier B. Every
+// wave passes both barriers at every step, whatever the step decides.
+__device__ __forceinline__ void history_helper(AmShared& sh, int m, int k, int lane, int par) {
   for (int c = 0; c < m; ++c) {
     lds_barrier();  // A
     const int j = sh.jl[c];
-    double ea[8] = {0, 0, 0, 0, 0, 0, 0, 0}, eb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (j >= 0 && k != j) {
-      int cc = 0;
-      for (; cc + 1 < c; cc += 2) {
-        hist_term(sh, cc, lane, ea);
-        hist_term(sh, cc + 1, lane, eb);
+    double e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (j >= 0) {  // (uniform; the lane k = j ignores its sums)
+      int cc = par;
+      for (; cc + 6 < c; cc += 8) {  // four terms' reads in flight, then their fmas in order
+        HistOps p0, p1, p2, p3;
+        hist_load(sh, cc, lane, p0);
+        hist_load(sh, cc + 2, lane, p1);
+        hist_load(sh, cc + 4, lane, p2);
+        hist_load(sh, cc + 6, lane, p3);
+        hist_fma(p0, e);
+        hist_fma(p1, e);
+        hist_fma(p2, e);
+        hist_fma(p3, e);
       }
-      if (cc < c) hist_term(sh, cc, lane, ea);
+      for (; cc < c; cc += 2) {
+        HistOps p0;
+        hist_load(sh, cc, lane, p0);
+        hist_fma(p0, e);
+      }
     }
 #pragma unroll
-    for (int t = 0; t < 8; ++t) sh.es[t][lane] = ea[t] + eb[t];
+    for (int t = 0; t < 8; ++t) sh.es[par][t][lane] = e[t];
     lds_barrier();  // B
   }
 }
@@ -383,8 +407,8 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
   const int N = A.N, ld = A.ld, ldk = A.ldk;
   const int Np = G * kAmSlots;
   const int k = g * kAmSlots + lane;  // this lane's landmark slot
-  if (threadIdx.x >= kAmSlots) {  // wave 1: the odd history terms only (uniform per wave)
-    history_helper(sh, d.m, k, lane);
+  if (threadIdx.x >= kAmSlots) {  // waves 1, 2: the history sums only (uniform per wave)
+    history_helper(sh, d.m, k, lane, (threadIdx.x >> 6) - 1);
     return;
   }
   const bool valid = k < N;
@@ -573,9 +597,9 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
       }
     }
     // ---- the step (slam.cpp:443-488): wave 0 forms what every lane shares (ẑ, H, S, S⁻¹, ν,
-    // K / M at the pose) while wave 1 (history_helper) sums this step's history terms of every
+    // K / M at the pose) while waves 1-2 (history_helper) sum this step's history terms of every
     // lane's crosses with j, between barriers A and B (both waves pass both at every step) ----
-    lds_barrier();  // A: sh.jl[c], sh.jc and j's history sh.jh published to wave 1
+    lds_barrier();  // A: sh.jl[c], sh.jc and j's history sh.jh published to waves 1-2
     AM_STAMP(c, 3);
     double H0[5], H1[5], Si[4], nu0 = 0.0, nu1 = 0.0;
     bool sok = false;
@@ -653,11 +677,11 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
         }
       }
     }
-    lds_barrier();  // B: wave 1's sums in sh.es
+    lds_barrier();  // B: waves 1 / 2's sums in sh.es
     AM_STAMP(c, 5);
     if (sok) {
       // this lane's crosses with j at step c: Σ_c[k, j] = Σ_p[k, j] − Σ_cc K_cc[k]·M_cc[:, j] and
-      // Σ_c[j, k] likewise (the sums from wave 1)
+      // Σ_c[j, k] likewise (the sums from waves 1-2)
       if (k == j) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
@@ -667,8 +691,8 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
       } else {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          rkj[t] = rkj[t] - sh.es[t][lane];
-          rjk[t] = rjk[t] - sh.es[4 + t][lane];
+          rkj[t] = rkj[t] - (sh.es[0][t][lane] + sh.es[1][t][lane]);
+          rjk[t] = rjk[t] - (sh.es[0][4 + t][lane] + sh.es[1][4 + t][lane]);
         }
       }
       {
