@@ -118,6 +118,33 @@ def test_device_replay_chains_with_host_calls():
     assert np.abs(mixed[0][1] - o["sigma"]).max() < 1e-7
 
 
+@pytest.mark.parametrize("env", [{}, {"EKF_SERIAL": "0"}, {"EKF_CU_SPLIT": "8"}],
+                         ids=["36filters_serial", "36filters_events", "36filters_device_epochs"])
+def test_device_device_host_handover_36_filters(monkeypatch, env):
+    """36 filters (more than 32: one stream by default; EKF_SERIAL=0 keeps the chain and bulk
+    streams with HIP events; a CU split of 8 per XCD holds all 36 chains, so device epochs), fp64
+    N = 96 (the HBM pipeline), spans device → device → host of one drive with holes. The second device call's first chunks need the Σ passes two back, which belong to the
+    first device call; the host call adopts the device's planning state. Round 4 saw exactly this
+    hand-over off by 3.29 on the state under a since-removed schedule; the wait that fixed it
+    (a device replay's chain waits for the pass two back) is what this test pins, against the whole
+    drive planned on the host, without any pairing of filters."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pyekf.poison_lds()
+    F = 36
+    scs = [synth.synthetic(96, 30, seed=51 + k) for k in range(4)]
+    spans = [(0, 11), (11, 20), (20, 30)]
+    mixed, sm, pm = _run(scs, 96, F, spans, ["device", "device", "host"], holes=True)
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
+        monkeypatch.delenv(k, raising=False)
+    host, sh, ph = _run(scs, 96, F, [(0, 30)], ["host"], holes=True)
+    assert sm == sh == [0] * F
+    _close(host, mixed, STATE_TOL)
+    assert np.abs(ph - pm).max() <= STATE_TOL
+
+
 def test_posterior_then_device_replay(monkeypatch):
     """ekf_posterior enqueues k_posterior on the main stream, reading its descriptor in the upload
     buffer; with device epochs the next ekf_replay_device plans on the bulk stream and rewrites that
