@@ -11,7 +11,8 @@
 // entries of Σ_c outside the blocks that a step needs are the crosses with its landmark j:
 //   Σ_c[k, j] = Σ_p[k, j] − Σ_{c'<c} K_{c'}[k]·M_{c'}[:, j],   Σ_c[j, k] likewise,
 // i.e. Σ_in (no predict term between landmarks) and the factor histories of k and of j. So:
-//   * one lane per landmark slot, 64 slots per workgroup (one wave), G = ⌈N / 64⌉ workgroups per
+//   * one lane per landmark slot, 64 slots per workgroup (wave 0; waves 1-2 only sum the history
+//     terms, history_helper), G = ⌈N / 64⌉ workgroups per
 //     filter; a lane keeps its slot's block and state in registers and its K / M history in LDS;
 //   * per marker: every lane scores its landmark (k_assoc's expression, ekf_math.hpp assoc_dist),
 //     a wave argmin (first index on ties, arma::index_min), then the G workgroups exchange their
