@@ -632,28 +632,25 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
       P5[3][4] = jkk[1];
       P5[4][3] = jkk[2];
       P5[4][4] = jkk[3];
+      // H's shape (range_bearing): H0 = [0, h1, h2, −h1, −h2], H1 = [−1, g1, g2, −g1, −g2] (exact
+      // negations), so a row times H is two fmas on (v1 − v3, v2 − v4), as in the chain's step
+      const double h1 = H0[1], h2 = H0[2], g1 = H1[1], g2 = H1[2];
       double Gt[5][2];  // (Σ·Hᵀ)[pA]
 #pragma unroll
       for (int a = 0; a < 5; ++a) {
-        double g0 = 0.0, g1 = 0.0;
-#pragma unroll
-        for (int b = 0; b < 5; ++b) {
-          g0 += P5[a][b] * H0[b];
-          g1 += P5[a][b] * H1[b];
-        }
-        Gt[a][0] = g0;
-        Gt[a][1] = g1;
+        const double d1 = P5[a][1] - P5[a][3], d2 = P5[a][2] - P5[a][4];
+        Gt[a][0] = fma(h2, d2, h1 * d1);
+        Gt[a][1] = fma(g2, d2, fma(g1, d1, -P5[a][0]));
       }
-      double Sm[4] = {0.0, 0.0, 0.0, 0.0};  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:476)
-#pragma unroll
-      for (int a = 0; a < 5; ++a) {
-        Sm[0] += H0[a] * Gt[a][0];
-        Sm[1] += H0[a] * Gt[a][1];
-        Sm[2] += H1[a] * Gt[a][0];
-        Sm[3] += H1[a] * Gt[a][1];
+      double Sm[4];  // S = H·(Σ·Hᵀ)[pA] + R (slam.cpp:476)
+      {
+        const double t1 = Gt[1][0] - Gt[3][0], t2 = Gt[2][0] - Gt[4][0];
+        const double u1 = Gt[1][1] - Gt[3][1], u2 = Gt[2][1] - Gt[4][1];
+        Sm[0] = fma(h2, t2, h1 * t1) + r_noise;
+        Sm[1] = fma(h2, u2, h1 * u1);
+        Sm[2] = fma(g2, t2, fma(g1, t1, -Gt[0][0]));
+        Sm[3] = fma(g2, u2, fma(g1, u1, -Gt[0][1])) + r_noise;
       }
-      Sm[0] += r_noise;
-      Sm[3] += r_noise;
       sok = inv2(Sm, Si);
       if (!sok) {
         status |= EKF_FLAG_NUMERIC_D;  // Armadillo's inv throws; this marker is skipped
@@ -666,15 +663,10 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
           Kp[a][1] = Gt[a][0] * Si[1] + Gt[a][1] * Si[3];
         }
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
-          double m0 = 0.0, m1 = 0.0;
-#pragma unroll
-          for (int a = 0; a < 5; ++a) {
-            m0 += H0[a] * P5[a][b];
-            m1 += H1[a] * P5[a][b];
-          }
-          Mp[0][b] = m0;
-          Mp[1][b] = m1;
+        for (int b = 0; b < 3; ++b) {  // (H·Σ)[:, pose b]
+          const double e1 = P5[1][b] - P5[3][b], e2 = P5[2][b] - P5[4][b];
+          Mp[0][b] = fma(h2, e2, h1 * e1);
+          Mp[1][b] = fma(g2, e2, fma(g1, e1, -P5[0][b]));
         }
       }
     }
@@ -698,35 +690,21 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
       }
       {
         // ---- this lane's slot: K[k], M[:, k] from its crosses with j ----
+        // (H's shape as above: two fmas on the differences)
+        const double h1 = H0[1], h2 = H0[2], g1 = H1[1], g2 = H1[2];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          double g0 = 0.0, g1 = 0.0;  // (Σ·Hᵀ)[k_a] over pA
-#pragma unroll
-          for (int b = 0; b < 3; ++b) {
-            g0 += kp[3 * a + b] * H0[b];
-            g1 += kp[3 * a + b] * H1[b];
-          }
-          g0 += rkj[2 * a] * H0[3];
-          g0 += rkj[2 * a + 1] * H0[4];
-          g1 += rkj[2 * a] * H1[3];
-          g1 += rkj[2 * a + 1] * H1[4];
-          Kk[a][0] = g0 * Si[0] + g1 * Si[2];
-          Kk[a][1] = g0 * Si[1] + g1 * Si[3];
+        for (int a = 0; a < 2; ++a) {  // (Σ·Hᵀ)[k_a] over pA
+          const double d1 = kp[3 * a + 1] - rkj[2 * a], d2 = kp[3 * a + 2] - rkj[2 * a + 1];
+          const double q0 = fma(h2, d2, h1 * d1);
+          const double q1 = fma(g2, d2, fma(g1, d1, -kp[3 * a]));
+          Kk[a][0] = q0 * Si[0] + q1 * Si[2];
+          Kk[a][1] = q0 * Si[1] + q1 * Si[3];
         }
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          double m0 = 0.0, m1 = 0.0;  // (H·Σ)[:, k_b]
-#pragma unroll
-          for (int a = 0; a < 3; ++a) {
-            m0 += H0[a] * pk[2 * a + b];
-            m1 += H1[a] * pk[2 * a + b];
-          }
-          m0 += H0[3] * rjk[b];
-          m0 += H0[4] * rjk[2 + b];
-          m1 += H1[3] * rjk[b];
-          m1 += H1[4] * rjk[2 + b];
-          Mk[0][b] = m0;
-          Mk[1][b] = m1;
+        for (int b = 0; b < 2; ++b) {  // (H·Σ)[:, k_b]
+          const double e1 = pk[2 + b] - rjk[b], e2 = pk[4 + b] - rjk[2 + b];
+          Mk[0][b] = fma(h2, e2, h1 * e1);
+          Mk[1][b] = fma(g2, e2, fma(g1, e1, -pk[b]));
         }
         // ---- Σ ← Σ − K·M on the lane's block and the pose block; x += K·ν (slam.cpp:482-488) ----
         double nkk[4], nkp[6], npk[6];
