@@ -119,12 +119,12 @@ def test_device_replay_chains_with_host_calls():
 
 
 # The two-stream HIP-event schedule at > 32 filters (opt-in: EKF_SERIAL=0) failed this test in two
-# of four runs at the end of round 5 (one filter's pose off by 6.1 rad / 0.36 m after the host span;
+# of five runs at the end of round 5 (one filter's pose off by 6.1 rad / 0.36 m after the host span;
 # DESIGN.md §5, the 36-filter hand-over paragraph): a missing ordering edge in that schedule's device-replay
 # hand-over, not yet found. Kept as a non-strict xfail so the default schedules stay gating.
 _EVENTS_36 = pytest.param({"EKF_SERIAL": "0"}, id="36filters_events", marks=pytest.mark.xfail(
     strict=False, reason="intermittent: device -> device -> host hand-over under the opt-in "
-                         "two-stream event schedule at 36 filters (2 failures in 4 runs, round 5)"))
+                         "two-stream event schedule at 36 filters (2 failures in 5 runs, round 5)"))
 
 
 @pytest.mark.parametrize("env", [pytest.param({}, id="36filters_serial"), _EVENTS_36,
