@@ -96,6 +96,8 @@ def parse(argv=None):
     p.add_argument("--parity-messages", type=int, default=10)
     p.add_argument("--traffic", choices=["auto", "off"], default="auto",
                    help="auto: measure the Σ pass's HBM bytes with two rocprofv3 --pmc child runs")
+    p.add_argument("--no-fp64", action="store_true",
+                   help="skip the n1024_fp32 line's fp64 leg (configs[2] at slam.cpp's arithmetic)")
     return p.parse_args(argv)
 
 
@@ -116,7 +118,7 @@ def _pmc_pass(args, counters):
     d = tempfile.mkdtemp(prefix="ekf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
     cmd = [exe, "--pmc", *counters, "-d", d, "-o", "pmc", "--output-format", "csv", "--",
            sys.executable, os.path.abspath(__file__), "--workload", args.workload,
-           "--steps", "8", "--warmup", "2", "--no-cpu", "--traffic", "off"]
+           "--steps", "8", "--warmup", "2", "--no-cpu", "--traffic", "off", "--no-fp64"]
     env = dict(os.environ, EKF_SERIAL="1")
     name = " ".join(counters)
     try:
@@ -726,6 +728,10 @@ def run(args, rank, world, local, backend=None):
                                   ws, counts, ids, act, rel, odom, tp)
         if world == 1:
             result["cpu_baseline"] = cpu_baseline(args, N, ws, counts, ids, act, rel, odom, tp)
+    if (rank == 0 and world == 1 and args.workload == "n1024_fp32" and gpu_in is not None
+            and warm_state and not args.no_fp64):
+        result["fp64"] = fp64_leg(args, be, N, warm_state[0], gpu_rows, ids.shape[2], n_warm, W, K,
+                                  local, counts, ids, act, rel, odom, gpu_in)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if sim is not None:
@@ -735,6 +741,56 @@ def run(args, rank, world, local, backend=None):
         dist.barrier()
         dist.destroy_process_group()
     return result, all_poses
+
+
+def fp64_leg(args, be, N, ws, gpu_rows, M, n_warm, W, K, local, counts, ids, act, rel, odom,
+             gpu_in):
+    """configs[2] at the reference's own arithmetic (slam.cpp is fp64 throughout), after the
+    fp32 line's timed region: a fresh fp64 handle from the same survey state replays the same
+    warm-up and the same K timed messages from the same HBM inputs through the same entry point
+    (ekf_replay_device), timed the same way; then one more span with HIP events per launch (chain,
+    Σ pass) and, unless --no-cpu, pose parity of the first messages against the fp64 oracle."""
+    x, S, tmo, cnt = ws
+    e = be.EKF(n_landmarks=N, dtype=be.F64, device=local)
+    e.set_state(x, S, tmo=tmo, counter=cnt)
+
+    def span(a, b):
+        pc, pi, pa, pr, po = (base + a * rb for base, rb in gpu_rows)
+        e.replay_device_raw(b - a, M, pc, pr, po, pi, pa)
+    t0s = n_warm + W
+    if W > 2:
+        span(n_warm, t0s - 2)
+    e.sync()
+    span(max(t0s - 2, n_warm), t0s)
+    be.sync()
+    t0 = time.perf_counter()
+    span(t0s, t0s + K)
+    e.sync()
+    be.sync()
+    el = time.perf_counter() - t0
+    live = np.arange(act.shape[2]) < counts[t0s:t0s + K][..., None]
+    corr = int(np.count_nonzero(live[:, :1] & (act[t0s:t0s + K, :1] != 2)))
+    e.profile(True)
+    span(t0s + K, t0s + 2 * K)
+    n_sig, ms_sig = e.profile_read(0)
+    n_ch, ms_ch = e.profile_read(1)
+    e.profile(False)
+    st = e.status(0)
+    byt = e.sigma_pass_bytes()
+    e.close()
+    sig_us = ms_sig / max(n_sig, 1) * 1e3
+    out = {"value": corr / el, "unit": "corrections/s", "ms_per_step": el / K * 1e3,
+           "steps": K, "dtype": "f64", "status_flags": st,
+           "chain_kernel_avg_us": ms_ch / max(n_ch, 1) * 1e3,
+           "sigma_pass_avg_us": sig_us,
+           "sigma_pass_frac": byt / (sig_us * 1e-6) / 1e9 / HBM_PEAK_GBS if n_sig else None,
+           "note": "same survey state, warm-up, messages and entry point as the fp32 value, "
+                   "on an fp64 handle (Σ and its pass in fp64), timed after it; not the value"}
+    if not args.no_cpu:
+        out["parity"] = parity(args, N, ekf_first_poses(args, be, N, be.F64, ws, counts, ids, act,
+                                                        rel, odom, t0s, local, gpu_in=gpu_in),
+                               ws, counts, ids, act, rel, odom, t0s)
+    return out
 
 
 def reduce_ranks(elapsed, corrections, poses, device):

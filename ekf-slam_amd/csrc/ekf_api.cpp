@@ -83,6 +83,11 @@ struct ekf_ctx {
   unsigned* sync = nullptr;               // device epochs: Σ pass done, its ticket, chains done
   hipEvent_t ev_sig[2] = {nullptr, nullptr};  // bulk → main: Σ pass of launch s, by s & 1
   long long seq = 0;                      // launch pairs issued
+  // dev only (EKF_DBG_ORDER bit mask, tools/diag_handover.py): conservative hand-off variants
+  // for locating a missing ordering edge of the event schedule
+  unsigned dbg_order = 0;
+  std::vector<hipEvent_t> dbg_ev;         // bit 4: a fresh event per Σ pass (never re-recorded)
+  unsigned long long* dlog = nullptr;     // bit 4096: PassArgs::dlog
   void* sig[2] = {nullptr, nullptr};
   double* x[2] = {nullptr, nullptr};
   void* kcat = nullptr;
@@ -164,6 +169,8 @@ PassArgs<T> args(ekf_ctx* h, const MsgDesc* desc, int f0) {
   a.r = h->cfg.r_noise;
   a.gate = h->cfg.mah_gate;
   a.joseph = h->joseph ? 1 : 0;
+  a.dbg = static_cast<int>(h->dbg_order >> 8);
+  a.dlog = h->dlog;
   return a;
 }
 
@@ -258,11 +265,21 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
   }
   if (pipelined && !nolook) {
     // events: a rebuilding (kLook) chain needs the Σ pass two launches back
-    if (!h->devsync) HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s0 & 1], 0));
+    if (!h->devsync) {
+      if (h->dbg_order & 1u) {
+        if (join_bulk(h)) return EKF_E_HIP;
+      } else if (h->dbg_order & 16u) {
+        if (s0 >= 2 && s0 - 2 < h->dbg_ev.size())
+          HIPCHK(hipStreamWaitEvent(ms, h->dbg_ev[s0 - 2], 0));
+      } else {
+        HIPCHK(hipStreamWaitEvent(ms, h->ev_sig[s0 & 1], 0));
+      }
+    }
   } else if (!a.polls) {
     // a chain that gathers its own Σ_in needs the previous pass: everything on the bulk stream
     if (join_bulk(h)) return EKF_E_HIP;
   }
+  if (h->dbg_order & 8192u) HIPCHK(launch_dbg_sum<T>(a, nf, 3, ms));
   int rc = timed(h, 1, ms, [&](hipEvent_t e0, hipEvent_t e1) {
     return launch_chain<T>(a, nf, nchunks, ms, e0, e1);
   });
@@ -286,6 +303,7 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
       return launch_factors<T>(ai, nf, bs, e0, e1);
     });
     if (rc) return rc;
+    if (h->dbg_order & 8192u) HIPCHK(launch_dbg_sum<T>(ai, nf, 1, bs));
     // some filter stages the rebuild operands of its chunk after next (device-written descriptors:
     // the caller's hint — the group's first stage_hint chunks may, the last two of a device replay
     // have no chunk after next in it — the staging kernel reads every descriptor's own flags)
@@ -299,7 +317,20 @@ int launch_group(ekf_ctx* h, const MsgDesc* dptr, const MsgDesc* hd, int f0, int
       return launch_sigma_pass<T>(ai, nf, last ? publish_end : !in_group, stage, bs, e0, e1);
     });
     if (rc) return rc;
+    if (h->dbg_order & 8192u) HIPCHK(launch_dbg_sum<T>(ai, nf, 2, bs));
     if (!h->devsync) HIPCHK(hipEventRecord(h->ev_sig[(s0 + i) & 1], bs));
+    if (h->dbg_order & 16u) {
+      while (h->dbg_ev.size() <= s0 + i) {
+        hipEvent_t e = nullptr;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        h->dbg_ev.push_back(e);
+      }
+      HIPCHK(hipEventRecord(h->dbg_ev[s0 + i], bs));
+    }
+    if ((h->dbg_order & 8u) && !h->devsync) {  // every launch pair drained before the next
+      HIPCHK(hipStreamSynchronize(bs));
+      HIPCHK(hipStreamSynchronize(ms));
+    }
   }
   h->seq += nchunks;
   h->epoch_owed = a.polls && !publish_end;
@@ -1053,6 +1084,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
   };
   if (hipSetDevice(cfg.device) != hipSuccess) return fail(EKF_E_HIP);
   if (const char* e = std::getenv("EKF_SERIAL")) h->serial = std::atoi(e) != 0;
+  if (const char* e = std::getenv("EKF_DBG_ORDER")) h->dbg_order = static_cast<unsigned>(std::atoi(e));
   if (const char* e = std::getenv("EKF_ASSOC_MSG")) h->assoc_msg = std::atoi(e) != 0;
   {  // EKF_RESIDENT=0: the HBM pipeline at every size (tests compare the two)
     const char* e = std::getenv("EKF_RESIDENT");
@@ -1103,7 +1135,13 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     if (hipMalloc(&h->stage, stage_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
     if (hipMemset(h->stage, 0, stage_bytes) != hipSuccess) return fail(EKF_E_HIP);
   }
-  const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + h->F);
+  // (+ 3F words: PassArgs::dbg & 8's per-kernel launch epochs)
+  if (h->dbg_order & (4096u | 8192u)) {
+    const size_t b = sizeof(unsigned long long) * kDlogKinds * 64 * 64 * 8;
+    if (hipMalloc(&h->dlog, b) != hipSuccess) return fail(EKF_E_NOMEM);
+    if (hipMemset(h->dlog, 0, b) != hipSuccess) return fail(EKF_E_HIP);
+  }
+  const size_t sync_bytes = sizeof(unsigned) * (kSyncChain + 4 * static_cast<size_t>(h->F));
   if (hipMalloc(&h->sync, sync_bytes) != hipSuccess) return fail(EKF_E_NOMEM);
   if (hipMemset(h->sync, 0, sync_bytes) != hipSuccess) return fail(EKF_E_HIP);
   h->ddesc_cap = std::max(kDescInit, static_cast<size_t>(h->F) * 4);
@@ -1170,8 +1208,10 @@ int ekf_destroy(ekf_t h) {
   if (h->ev_chain) hipEventDestroy(h->ev_chain);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->sync) hipFree(h->sync);
+  if (h->dlog) hipFree(h->dlog);
   for (hipEvent_t e : h->ev_sig)
     if (e) hipEventDestroy(e);
+  for (hipEvent_t e : h->dbg_ev) hipEventDestroy(e);
   if (h->bulk) hipStreamDestroy(h->bulk);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
@@ -1338,7 +1378,8 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   // starts beside the planner instead of behind a main → bulk event hop (≈ 6 µs of each replay)
   const bool beside = h->devsync && !h->serial;
   // the bulk stream may still read the last descriptors (an idle one reads nothing: no hop)
-  if (hipStreamQuery(h->bulk) != hipSuccess && join_bulk(h)) return EKF_E_HIP;
+  if (((h->dbg_order & 2u) || hipStreamQuery(h->bulk) != hipSuccess) && join_bulk(h))
+    return EKF_E_HIP;
   // ... and the main stream: work there that the bulk stream is not ordered after (a k_posterior
   // of ekf_posterior reads its descriptor in ddesc) must end before a planner on the bulk stream
   // rewrites ddesc. (Chains are covered: the bulk stream's factor kernels follow every chain
@@ -1409,6 +1450,7 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
                  stg && t + 2 < Tc ? 1 : 0);
   }
   h->main_dirty = true;
+  if (!rc && (h->dbg_order & 32u) && drain(h)) return EKF_E_HIP;
   return rc;
 }
 
@@ -1664,6 +1706,23 @@ extern "C" int ekfslam_diag_read_am_stamps(unsigned long long* out);  // ekf_ass
 // dev only: k_assoc_msg's s_memrealtime stamps, [2 workgroups][kMaxChunk + 1][8]
 int ekf_diag_am_stamps(unsigned long long* out) { return ekfslam_diag_read_am_stamps(out); }
 #endif
+
+// dev only (tools/diag_handover.py): the PassArgs::dbg & 4 counters, sync[kSyncDbg + i], i < n ≤ 16
+int ekf_debug_counters(ekf_t h, unsigned* out, int n) {
+  if (!h || !out || n < 0 || n > 16) return EKF_E_ARG;
+  if (int rc = settle(h)) return rc;
+  HIPCHK(hipMemcpy(out, h->sync + kSyncDbg, n * sizeof(unsigned), hipMemcpyDeviceToHost));
+  return EKF_OK;
+}
+
+// dev only: the PassArgs::dlog checksums (EKF_DBG_ORDER & 4096), kDlogKinds·64·64·8 words
+int ekf_debug_log(ekf_t h, unsigned long long* out) {
+  if (!h || !out || !h->dlog) return EKF_E_ARG;
+  if (int rc = settle(h)) return rc;
+  HIPCHK(hipMemcpy(out, h->dlog, sizeof(unsigned long long) * kDlogKinds * 64 * 64 * 8,
+                   hipMemcpyDeviceToHost));
+  return EKF_OK;
+}
 
 double ekf_sigma_pass_bytes(ekf_t h, int nf) {
   if (!h) return 0.0;

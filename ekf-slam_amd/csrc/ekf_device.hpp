@@ -26,6 +26,8 @@ constexpr int kSyncPlan = 32;    // (t, f) descriptors device replays have plann
                                  // its own 128-B line: the planner waves' fetch_adds do not contend
                                  // with the polls of the Σ epoch in word 0)
 constexpr int kSyncChain = 64;   // [F]: epoch of each filter's last complete chain
+constexpr int kSyncDbg = 48;     // dev only (PassArgs::dbg & 4): [0] chains, [1] factor kernels that
+                                 // started before their producer's epoch was visible, [2] checks
 
 // MsgDesc.flags
 constexpr int kFirst = 1;    // chunk carries the predict (slam.cpp:184-198) for this message

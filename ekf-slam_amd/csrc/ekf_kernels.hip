@@ -230,9 +230,39 @@ __device__ __forceinline__ void lds_wait_ge3(const __attribute__((address_space(
 // J: a Joseph chunk (m ≤ kMaxJoseph). Every step then also subtracts V_c·K_cᵀ, V_c = Σ_c·Hᵀ − K_c·S_c
 // (slam.cpp:264-265's update as (I − KH)Σ(I − KH)ᵀ + K·R·Kᵀ expanded), always after the K_c·M_c term
 // — the order wave 3 uses, so an entry both waves compute has the same bits.
+// The diagnostic build (EKF_DIAG_STAMPS, libekfslam_diag.so) also carries the hand-off
+// instrumentation behind PassArgs::dbg (EKF_DBG_ORDER, tools/diag_handover.py, tools/diag_dlog.py);
+// in the product library every such branch folds away.
+#ifdef EKF_DIAG_STAMPS
+constexpr bool kDiagBuild = true;
+#else
+constexpr bool kDiagBuild = false;
+#endif
+
+// dev only (PassArgs::dbg & 16): order-independent wrapping sums of the bit patterns a kernel read
+// or wrote, A.dlog[kind][seq % 64][f % 64][slot]
+__device__ __forceinline__ unsigned long long dbits(double v) {
+  return static_cast<unsigned long long>(__double_as_longlong(v));
+}
+__device__ __forceinline__ unsigned long long dbits(float v) { return __float_as_uint(v); }
+template <typename T>
+__device__ __forceinline__ void dlog_add(const PassArgs<T>& A, int kind, unsigned seq, int f,
+                                         int slot, unsigned long long v) {
+  atomicAdd(A.dlog + ((static_cast<size_t>(kind) * 64 + (seq & 63u)) * 64 + (f & 63)) * 8 + slot, v);
+}
+
+// dev only (PassArgs::dbg & 16): step c's wrapping sums at lg[(kChainLogKind + c)·64·64·8 + slot]
+constexpr int kChainLogKind = 5;
+__device__ __forceinline__ unsigned long long dbits0(double v) {
+  return static_cast<unsigned long long>(__double_as_longlong(v));
+}
+__device__ __forceinline__ void steplog(unsigned long long* lg, int c, int slot, unsigned long long v) {
+  atomicAdd(lg + static_cast<size_t>(kChainLogKind + c) * 64 * 64 * 8 + slot, v);
+}
+
 template <bool J>
 __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int m, int nu,
-                                         double r_noise, unsigned seq) {
+                                         double r_noise, unsigned seq, unsigned long long* lg) {
   LdsChain& sh = *shp;
   LdsDesc& d = *dp;
   const int lane = threadIdx.x & 63;
@@ -357,6 +387,15 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
         }
       }
     }
+    if (kDiagBuild && lg) {
+      if (lane == 0) {
+        steplog(lg, c, 0, dbits0(Sm_keep[0]) + dbits0(Sm_keep[1]) + dbits0(Sm_keep[2]) +
+                              dbits0(Sm_keep[3]) + dbits0(Si[0]) + dbits0(Si[3]));
+        steplog(lg, c, 1, dbits0(nv0) + dbits0(nv1) + dbits0(zhat[0]) + dbits0(zhat[1]) +
+                              dbits0(H0[1]) + dbits0(H1[2]));
+      }
+      if (lane < nu) steplog(lg, c, 2, dbits0(ka) + dbits0(kb) + dbits0(mm0) + dbits0(mm1));
+    }
     // The next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}) after step c−1. Pose columns /
     // rows: pk / pm (pA ⊃ pose). The nx columns / rows were read one step back (rn / qn, after
     // step c−2) and get step c−1's rank-2 term here from registers: K_{c−1} of this lane (kp)
@@ -410,6 +449,12 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
         qn[j] = sh.P[pb][nx + 2 + j][lr];
       }
     }
+    if (kDiagBuild && lg && lane < nu) {
+      unsigned long long v = 0;
+      for (int k = 0; k < 5; ++k) v += dbits0(xr[k]) + dbits0(xq[k]);
+      steplog(lg, c, 3, v);
+      steplog(lg, c, 7, dbits0(rn[0]) + dbits0(rn[1]) + dbits0(qn[0]) + dbits0(qn[1]));
+    }
     const int jx = __builtin_amdgcn_readlane(ul, pj);  // sh.u[pj] (ul = sh.u[lane], pj < kMaxU)
     EKF_STAMP(67 + 8 * c);
     const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
@@ -431,6 +476,10 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       }
       xl = xt;
       *(lane < nu ? &sh.xU[0][lane] : &sh.junk[0][lane]) = xt;
+      if (kDiagBuild && lg && lane < nu) {
+        steplog(lg, c, 4, dbits0(K0) + dbits0(K1));
+        steplog(lg, c, 5, dbits0(xt));
+      }
     }
     {
       const bool in = lane < nu, st = lane < kMaxU;
@@ -504,6 +553,11 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
         if (J) v = rank2_sub(v, vx0[k], vx1[k], K0, K1);
         pm[k] = v;
         *(later ? &sh.P[pb][row][lane] : &sh.junk[0][lane]) = v;
+      }
+      if (kDiagBuild && lg && lane < nu) {
+        unsigned long long v = 0;
+        for (int k = 0; k < 5; ++k) v += dbits0(pk[k]) + dbits0(pm[k]);
+        steplog(lg, c, 6, v);
       }
       // (the Bx × Bx entries: lane `row` stored the same value as its pk, same operands)
       kp0 = K0;
@@ -785,6 +839,13 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
       acc1 = mfma_f64(z1, av[s], acc1);
       acc2 = mfma_f64(zx, av[s], acc2);
     }
+    if (kDiagBuild && (A.dbg & 16)) {  // Σ_in as read, x_in as read
+      unsigned long long s2 = 0;
+#pragma unroll
+      for (int s = 0; s < 9; ++s) s2 += dbits(raw[s]);
+      s2 += dbits(r0t);
+      dlog_add(A, 4, A.seq, f, 2, s2);
+    }
     if (vi && ks == 0) {  // the predict's two rank-1 factors (slam.cpp:198)
       kc[0 * ldk + i] = static_cast<T>(first ? -ai : 0.0);
       kc[1 * ldk + i] = static_cast<T>(first ? -(r0raw + ai * s00) : 0.0);
@@ -793,6 +854,10 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
 #pragma unroll
       for (int k = kMaxU - 1; k >= 0; --k) pos = (k < nu && sh.u[k] == i) ? k : pos;
       xout[i] = pos < nu ? xfin[pos] : xin[i] + acc2[0];
+      if (kDiagBuild && (A.dbg & 16)) {
+        dlog_add(A, 4, A.seq, f, 3, dbits(xin[i]));
+        dlog_add(A, 4, A.seq, f, 4, dbits(pos < nu ? xfin[pos] : xin[i] + acc2[0]));
+      }
     }
     if (vi) {
 #pragma unroll
@@ -833,6 +898,16 @@ __host__ __device__ inline int factor_waves(const PassArgs<T>& a) {
 // chain's own final block into the next chunk instead was 6 % faster but let the chain's block and
 // the HBM Σ drift apart — two roundings of the 1e7-prior first sightings — until a survey replay
 // went non-finite; the rebuild keeps every schedule bit-identical)
+// dev only (PassArgs::dbg & 8): kernel `k` (0 chain, 1 factors, 2 Σ pass) of filter f runs with
+// launch epoch e; the launches of a kind are stream-ordered, so e must exceed the last one seen
+// (a kernel that runs with an older launch's arguments counts at sync[kSyncDbg + 3 + k])
+template <typename T>
+__device__ void dbg_seq_check(const PassArgs<T>& A, int k, int f, unsigned e) {
+  unsigned* last = A.sync + kSyncChain + (1 + k) * A.rec_stride + f;
+  if (static_cast<int>(e - *last) <= 0) atomicAdd(A.sync + kSyncDbg + 3 + k, 1u);
+  *last = e;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchunks) {
   __shared__ ChainShared sh;
@@ -849,7 +924,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // so padding rows / columns that feed MFMA or dot products as zeros really are zeros
   for (int e = tid; e < static_cast<int>(sizeof(ChainShared) / 8); e += blockDim.x)
     reinterpret_cast<double*>(&sh)[e] = 0.0;
+  // Every wave's zeroing stores must land before the one below: the word npose_ci lives in is
+  // zeroed by a thread of another wave, and without the barrier that store could come after this
+  // one (npose_ci = 0 made chunk 0 copy a never-computed predicted pose, (0, 0, 0)). The race
+  // showed where the chain's waves run at different paces — on CUs shared with the bulk stream's
+  // kernels (two streams without CU masks: > 32 filters with EKF_SERIAL=0), DESIGN.md §5.
+  __syncthreads();
   if (tid == 0) sh.npose_ci = -1;  // (ordered before its first reader by the chunk loop's barriers)
+  if (kDiagBuild && (A.dbg & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   bool pre = false;        // sdesc[ci & 1] was prefetched by the previous chunk's epilogue
   unsigned pending = 0;    // chain epoch of the previous chunk, not yet published (its record
                            // stores are still in flight; see the epilogue)
@@ -880,10 +962,15 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
   if (!active) continue;  // this filter sits the chunk out
   const unsigned seq = A.seq + static_cast<unsigned>(ci);
+  if ((kDiagBuild && (A.dbg & 8)) && tid == 0) dbg_seq_check(A, 0, f, seq + 1u);
   // Σ_in / x / records a rebuilding chain reads come from the Σ pass two launches back (bulk
   // stream), and this record parity is free again once that pass is done (its factor kernel read
   // it); a chunk that gathers its own Σ_in needs the pass one back.
   const unsigned need = look ? (seq >= 2 ? seq - 1 : 0u) : seq;
+  if ((kDiagBuild && (A.dbg & 4)) && need && tid == 0) {
+    if (static_cast<int>(epoch_load(A.sync + kSyncSigma) - need) < 0) atomicAdd(A.sync + kSyncDbg, 1u);
+    atomicAdd(A.sync + kSyncDbg + 2, 1u);
+  }
   // A0's associated ids (k_assoc, earlier on this stream), loaded unconditionally (clamped) and
   // here, so that the barrier below completes them: under A0's branch the load was waited for,
   // vmcnt(0), together with every early load below
@@ -910,6 +997,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // V_c = G_c − K_c·S_c beside K_c, column factor K_cᵀ beside M_c: the record's Z carries V_c's
   // row map in columns 2m + 2c.., the chain's block gets the term step by step.
   const bool joseph = (d.flags & kJoseph) != 0;
+  if ((kDiagBuild && (A.dbg & 16)) && tid < static_cast<int>(sizeof(MsgDesc) / 8))
+    dlog_add(A, 0, seq, f, 0, reinterpret_cast<const unsigned long long*>(&d)[tid]);
 
   // kLook: this chunk's Σ_in is still being written by the previous chunk's Σ pass. Rebuild what
   // the chain needs from the chunk before: Σ_in' (the other buffer, complete) and its record.
@@ -1034,6 +1123,23 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       pa1 = rp->a1;
       pa2 = rp->a2;
       tq = ctl->tmo[tid < 3 ? tid : 0];
+    }
+    if (kDiagBuild && (A.dbg & 16)) {
+      unsigned long long s2 = 0, s4 = 0;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) {
+        s2 += dbits(vd[i]) + dbits(vr[i]) + dbits(vc[i]);
+        s4 += dbits(vz[i]) + dbits(vy[i]);
+      }
+      if (tid < kMaxU) {
+        s2 += dbits(r0u) + dbits(c0u) + dbits(r0p) + dbits(c0p);
+        s4 += dbits(x0) + dbits(x1);
+        dlog_add(A, 0, seq, f, 3, dbits(x2));
+      }
+      if (tid == 0) s4 += static_cast<unsigned>(pflags) + dbits(pa1) + dbits(pa2);
+      if (tid < 3) dlog_add(A, 0, seq, f, 1, dbits(tq));
+      dlog_add(A, 0, seq, f, 2, s2);
+      dlog_add(A, 0, seq, f, 4, s4);
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
@@ -1237,6 +1343,14 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const double xv = xin[sh.u[tid < nu ? tid : 0]];
     const double xq = xin[tid < 3 ? tid : 0];
     const double tq = ctl->tmo[tid < 3 ? tid : 0];
+    if (kDiagBuild && (A.dbg & 16)) {
+      unsigned long long s2 = 0;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) s2 += dbits(vd[i]);
+      dlog_add(A, 0, seq, f, 2, s2);
+      dlog_add(A, 0, seq, f, 3, dbits(xv) + dbits(xq));
+      if (tid < 3) dlog_add(A, 0, seq, f, 1, dbits(tq));
+    }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * kChainThreads;
@@ -1316,10 +1430,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   }
   EKF_STAMP(19);
   if (wave == 0) {
+    unsigned long long* lg =
+        (kDiagBuild && (A.dbg & 16)) ? A.dlog + (static_cast<size_t>(seq & 63u) * 64 + (f & 63)) * 8 : nullptr;
     if (joseph)
-      chain_wave0<true>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq);
+      chain_wave0<true>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq, lg);
     else
-      chain_wave0<false>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq);
+      chain_wave0<false>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq, lg);
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
     // lane → column 3+(lane&31), rows 3.. of parity lane>>5. The lane's 16 entries stay in
     // registers for the whole chunk: every step's rank-2 term is applied to all of them — also to
@@ -1381,6 +1497,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       ctl->tmo[0] = tmo.theta;
       ctl->tmo[1] = tmo.x;
       ctl->tmo[2] = tmo.y;
+      if (kDiagBuild && (A.dbg & 16))
+        dlog_add(A, 0, A.seq + static_cast<unsigned>(ci), f, 6,
+                 dbits(tmo.theta) + dbits(tmo.x) + dbits(tmo.y));
       sh.tmo[0] = tmo.theta;
       sh.tmo[1] = tmo.x;
       sh.tmo[2] = tmo.y;
@@ -1775,6 +1894,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       const double zx = sh.Zx[tid];  // (wave 1's sum over the corrections)
       const bool in = tid < nu;
       st_wt(&rec->Zx[tid], zx);
+      if (kDiagBuild && (A.dbg & 16)) dlog_add(A, 0, seq, f, 5, dbits(zx) + dbits(in ? xfin[tid] : 0.0));
       st_wt(&rec->u[tid], sh.u[tid]);
       st_wt(&rec->alphaU[tid], in ? sh.alphaU[tid] : 0.0);
       st_wt(&rec->row0raw[tid], in ? sh.row0raw[tid] : 0.0);
@@ -1802,6 +1922,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     __syncthreads();
     if (tid == 0) epoch_store(A.sync + kSyncChain + f, pending);
   }
+  if (kDiagBuild && (A.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
 template <typename T>
@@ -1819,11 +1940,16 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
   // the previous chunk's Σ pass ended before this launch (same stream): its epoch, for the chains
   if (A.pub_sigma && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     epoch_store(A.sync + kSyncSigma, A.pub_sigma);
+  if (kDiagBuild && (A.dbg & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (fb >= nf) return;
   const MsgDesc& d = A.desc[fb];
   if (!(d.flags & kActive)) return;
   const int f = A.f0 + fb;
   const int tid = threadIdx.x;
+  if ((kDiagBuild && (A.dbg & 4)) && tid == 0 &&
+      static_cast<int>(epoch_load(A.sync + kSyncChain + f) - (A.seq + 1u)) < 0)
+    atomicAdd(A.sync + kSyncDbg + 1, 1u);
+  if ((kDiagBuild && (A.dbg & 8)) && tid == 0 && bx == 0) dbg_seq_check(A, 1, f, A.seq + 1u);
   const ChunkRec* rec = A.rec + static_cast<size_t>(d.parity) * A.rec_stride + f;
   // the chain of this chunk runs on the other stream: wait for its record
   if (A.polls && tid == 0 && !epoch_wait_acquire(A.sync + kSyncChain + f, A.seq + 1u))
@@ -1832,7 +1958,20 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
   __syncthreads();
   factor_record(rec, sh, tid);
   __syncthreads();
+  if ((kDiagBuild && (A.dbg & 16)) && bx == 0) {  // the record as this kernel read it
+    unsigned long long s1 = 0;
+    for (int e = tid; e < kMaxU * kZC; e += 256)
+      s1 += dbits(sh.Z[e / kZC][e % kZC]) + dbits(sh.Y[e / kMaxU][e % kMaxU]);
+    if (tid < kMaxU)
+      s1 += static_cast<unsigned>(sh.u[tid]) + dbits(sh.alphaU[tid]) + dbits(sh.row0raw[tid]) +
+            dbits(sh.col0raw[tid]) + dbits(sh.Zx[tid]) + dbits(sh.xU[tid]);
+    if (tid == 0) s1 += dbits(sh.a1) + dbits(sh.a2) + dbits(sh.s00) + static_cast<unsigned>(sh.nu);
+    dlog_add(A, 4, A.seq, f, 1, s1);
+    if (tid < static_cast<int>(sizeof(MsgDesc) / 8))
+      dlog_add(A, 4, A.seq, f, 0, reinterpret_cast<const unsigned long long*>(&d)[tid]);
+  }
   factor_wave<T>(A, d, f, bx * (blockDim.x >> 6) + (tid >> 6), sh, tid & 63);
+  if (kDiagBuild && (A.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
 // ---- Σ pass on MFMA -------------------------------------------------------------------------
@@ -2128,6 +2267,7 @@ template <typename T, bool WIDE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : (sizeof(T) == 8 ? 4 : 6)))) void k_sigma_pass(PassArgs<T> A, int tcols, int xcd_b, int nf) {
   using Tile = PassTile<T, WIDE>;
   SIG_STAMP(0);
+  if (kDiagBuild && (A.dbg & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   int fb = blockIdx.y, bx = blockIdx.x;
   if (xcd_b > 0) {
     const int L = blockIdx.x, j = L >> 3;
@@ -2213,6 +2353,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
   } else if ((d.flags & kActive) && ok) {
     SIG_STAMP(1);
     const int f = A.f0 + fb;
+    if ((kDiagBuild && (A.dbg & 8)) && t == 0 && lane == 0) dbg_seq_check(A, 2, f, A.seq + 1u);
     // this filter's rank (Joseph: K·M and V·Kᵀ per marker); rows beyond are stale
     const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
     Tile::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
@@ -2220,6 +2361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
               (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane,
               tT[threadIdx.x >> 6]);
   }
+  if (kDiagBuild && (A.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   SIG_STAMP(3);
 }
 
@@ -2501,6 +2643,62 @@ __global__ void k_init_diag(T* sig, size_t stride, int n, int ld, double v, int 
     sig[f * stride + static_cast<size_t>(i) * ld + i] = static_cast<T>(v);
 }
 
+// dev only (PassArgs::dbg & 16): one workgroup per filter sums what the surrounding kernels left in
+// memory (launch_dbg_sum's kinds), in stream order
+template <typename T>
+__global__ __launch_bounds__(256) void k_dbg_sum(PassArgs<T> A, int kind, int nf) {
+  const int fb = blockIdx.x;
+  if (fb >= nf) return;
+  const MsgDesc& d = A.desc[fb];
+  if (!(d.flags & kActive)) return;
+  const int f = A.f0 + fb, p = d.parity, n = A.n, tid = threadIdx.x;
+  unsigned long long s[6] = {0, 0, 0, 0, 0, 0};
+  if (kind == 1) {
+    const double* xo = A.x[p ^ 1] + f * A.x_stride;
+    for (int i = tid; i < n; i += 256) s[0] += dbits(xo[i]);
+    const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
+    const T* kc = A.kcat + f * A.km_stride;
+    const T* mc = A.mcat + f * A.km_stride;
+    for (int e = tid; e < kw * n; e += 256) {
+      const size_t o = static_cast<size_t>(e / n) * A.ldk + e % n;
+      s[1] += dbits(kc[o]);
+      s[2] += dbits(mc[o]);
+    }
+  } else if (kind == 2) {
+    const T* so = A.sig[p ^ 1] + f * A.sig_stride;
+    for (int e = tid; e < n * n; e += 256) s[0] += dbits(so[static_cast<size_t>(e / n) * A.ld + e % n]);
+  } else {
+    const T* sp = A.sig[p ^ 1] + f * A.sig_stride;
+    const T* si = A.sig[p] + f * A.sig_stride;
+    for (int e = tid; e < n * n; e += 256) {
+      const size_t o = static_cast<size_t>(e / n) * A.ld + e % n;
+      s[0] += dbits(sp[o]);
+      s[4] += dbits(si[o]);
+    }
+    const double* xp = A.x[p ^ 1] + f * A.x_stride;
+    const double* xi = A.x[p] + f * A.x_stride;
+    for (int i = tid; i < n; i += 256) {
+      s[1] += dbits(xp[i]);
+      s[5] += dbits(xi[i]);
+    }
+    const unsigned long long* rw = reinterpret_cast<const unsigned long long*>(
+        A.rec + static_cast<size_t>(p ^ 1) * A.rec_stride + f);
+    for (int e = tid; e < static_cast<int>(sizeof(ChunkRec) / 8); e += 256) s[2] += rw[e];
+    if (tid < 3) s[3] += dbits(A.ctl[f].tmo[tid]);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    if (s[k]) dlog_add(A, kind, A.seq, f, k, s[k]);
+}
+
+template <typename T>
+hipError_t launch_dbg_sum(const PassArgs<T>& a, int nf, int kind, hipStream_t s) {
+  hipLaunchKernelGGL(k_dbg_sum<T>, dim3(nf), dim3(256), 0, s, a, kind, nf);
+  return hipGetLastError();
+}
+template hipError_t launch_dbg_sum<double>(const PassArgs<double>&, int, int, hipStream_t);
+template hipError_t launch_dbg_sum<float>(const PassArgs<float>&, int, int, hipStream_t);
+
 // ---- launchers ------------------------------------------------------------------------------
 // With events, the launch carries them in its dispatch (hipExtLaunchKernelGGL): they time the
 // kernel's own execution, not the queueing / dispatch latency around it.
@@ -2565,7 +2763,8 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool st
   }
   if (stage) hipLaunchKernelGGL(k_patch_stage<T>, dim3(nf), dim3(256), 0, s, a);
   // the pass's epoch (otherwise published by the next chunk's factor kernel, PassArgs::pub_sigma)
-  if (publish && a.polls) hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
+  if ((publish && a.polls) || (a.dbg & 4))
+    hipLaunchKernelGGL(k_sigma_epoch, dim3(1), dim3(64), 0, s, a.sync, a.seq + 1u);
   return hipGetLastError();
 }
 

@@ -43,7 +43,18 @@ struct PassArgs {
   int n, ld, N, f0;
   double q, r, gate;
   int joseph;           // resident path: Joseph-form Σ update (ekf_set_joseph)
+  int dbg;              // dev only (EKF_DBG_ORDER >> 8, tools/diag_handover.py): 1 agent acquire at
+                        // the start of chain / factors / Σ pass, 2 agent release at their end,
+                        // 4 count hand-offs whose producer epoch is not yet visible (sync[48..]),
+                        // 8 check launch epochs, 16 chain / factor kernels log checksums (dlog), 32 k_dbg_sum
+                        // kernels around them (EKF_DBG_ORDER 8192)
+  unsigned long long* dlog;  // dev only: [kDlogKinds][64 seq][64 filters][8 slots] wrapping sums
 };
+constexpr int kDlogKinds = 21;  // 0 chain, 1-3 k_dbg_sum, 4 factor kernel, 5 + c chain step c
+// dev only: checksums of what a kernel pair left in memory (kind 1: after the factor kernel, x_out
+// Kcat Mcat; 2: after the Σ pass, Σ_out; 3: before the chain, Σ_in' x_in' record' tmo Σ_in x_in)
+template <typename T>
+hipError_t launch_dbg_sum(const PassArgs<T>& a, int n_filters, int kind, hipStream_t s);
 
 // Chain kernel: the chunk's sequential corrections on the |U|×|U| block (predict folded in),
 // one workgroup per filter → ChunkRec.

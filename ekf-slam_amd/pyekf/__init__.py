@@ -20,6 +20,7 @@ EKF_E_TIMEOUT = -7
 EKF_FLAG_RANGE, EKF_FLAG_NUMERIC, EKF_FLAG_TIMEOUT = 1, 2, 4
 EKF_ASSOC_MARKER, EKF_ASSOC_CHUNK, EKF_ASSOC_CHUNK_XCD = 0, 1, 2
 EKF_SCHED_DEVSYNC, EKF_SCHED_SERIAL = 1, 4
+EKF_SCHED_BUILDER = 2  # deprecated, never set (include/ekf.h)
 EKF_F64, EKF_F32 = 0, 1
 EKF_PATH_PIPELINE, EKF_PATH_RESIDENT = 0, 1
 ADD, DELETE = 0, 2

@@ -103,9 +103,11 @@ int ekf_get_assoc_route(ekf_t h, int* route);
  *                      fill every CU, so two streams overlap nothing; the staged rebuild operands
  *                      are off there too, EKF_STAGE=1 restores them); EKF_SERIAL=1 forces it for
  *                      any handle, EKF_SERIAL=0 keeps two streams (HIP events) for > 32 filters.
- * Every schedule gives bit-identical results. (Bit 2, a block-builder schedule of earlier
- * releases, is retired and never set.) */
+ * Every schedule gives bit-identical results.
+ *   EKF_SCHED_BUILDER  deprecated: a block-builder schedule of earlier releases, retired; the bit is
+ *                      never set (the name stays so that code written against it still compiles). */
 #define EKF_SCHED_DEVSYNC 1
+#define EKF_SCHED_BUILDER 2
 #define EKF_SCHED_SERIAL 4
 int ekf_get_schedule(ekf_t h, int* flags);
 

@@ -86,7 +86,7 @@ def _close(a, b, tol, stol=SIGMA_TOL):
 @pytest.mark.parametrize("F,env", [(1, {}), (4, {}), (1, {"EKF_DEVSYNC": "0"}),
                                    (4, {"EKF_SERIAL": "1"}), (3, {"EKF_STAGE": "0"})],
                          ids=["1filter", "4filters", "1filter_events", "4filters_serial",
-                              "3filters_nostage_norows"])
+                              "3filters_nostage"])
 def test_device_replay_equals_host_replay(monkeypatch, F, env):
     """fp64 N = 96 (the HBM pipeline), 30 messages, every schedule: the device-planned replay ends
     where the host-planned one does, holes (empty and all-DELETE messages) included."""
@@ -118,17 +118,8 @@ def test_device_replay_chains_with_host_calls():
     assert np.abs(mixed[0][1] - o["sigma"]).max() < 1e-7
 
 
-# The two-stream HIP-event schedule at > 32 filters (opt-in: EKF_SERIAL=0) failed this test in two
-# of five runs at the end of round 5 (one filter's pose off by 6.1 rad / 0.36 m after the host span;
-# DESIGN.md §5, the 36-filter hand-over paragraph): a missing ordering edge in that schedule's device-replay
-# hand-over, not yet found. Kept as a non-strict xfail so the default schedules stay gating.
-_EVENTS_36 = pytest.param({"EKF_SERIAL": "0"}, id="36filters_events", marks=pytest.mark.xfail(
-    strict=False, reason="intermittent: device -> device -> host hand-over under the opt-in "
-                         "two-stream event schedule at 36 filters (2 failures in 5 runs, round 5)"))
-
-
-@pytest.mark.parametrize("env", [pytest.param({}, id="36filters_serial"), _EVENTS_36,
-                                 pytest.param({"EKF_CU_SPLIT": "8"}, id="36filters_device_epochs")])
+@pytest.mark.parametrize("env", [{}, {"EKF_SERIAL": "0"}, {"EKF_CU_SPLIT": "8"}],
+                         ids=["36filters_serial", "36filters_events", "36filters_device_epochs"])
 def test_device_device_host_handover_36_filters(monkeypatch, env):
     """36 filters (more than 32: one stream by default; EKF_SERIAL=0 keeps the chain and bulk
     streams with HIP events; a CU split of 8 per XCD holds all 36 chains, so device epochs), fp64
@@ -136,7 +127,10 @@ def test_device_device_host_handover_36_filters(monkeypatch, env):
     first device call; the host call adopts the device's planning state. Round 4 saw exactly this
     hand-over off by 3.29 on the state under a since-removed schedule; the wait that fixed it
     (a device replay's chain waits for the pass two back) is what this test pins, against the whole
-    drive planned on the host, without any pairing of filters."""
+    drive planned on the host, without any pairing of filters.
+    The events case failed intermittently until round 6 (2 of 5 runs, one filter's pose 6.1 rad
+    off): the chain kernel's LDS zeroing raced with its own npose_ci initialisation when its waves
+    ran at different paces on CUs shared with the bulk stream (k_chain); it gates."""
     for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():

@@ -8,7 +8,7 @@ import sys
 os.environ["EKF_LIB"] = "libekfslam_diag.so"
 sys.argv = [sys.argv[0]]
 HERE = os.path.dirname(os.path.abspath(__file__))
-exec(open(os.path.join(HERE, "diag_numeric.py")).read().split("for env in ({\"EKF_ROWS\"")[0])
+exec(open(os.path.join(HERE, "diag_numeric.py")).read().split("for env in ({},)")[0])
 import ctypes as C  # noqa: E402
 
 lib = pyekf.lib()

@@ -64,7 +64,7 @@ def status_after(upto, env=None):
 
 
 def state_after(upto, env):
-    for k in ("EKF_SERIAL", "EKF_DEVSYNC", "EKF_ROWS"):
+    for k in ("EKF_SERIAL", "EKF_DEVSYNC"):
         os.environ.pop(k, None)
     os.environ.update(env)
     e = pyekf.EKF(n_landmarks=N)
@@ -81,7 +81,7 @@ def ucols(t):
     return [0, 1, 2] + [v for j in sc.ids[t, :c] for v in (3 + 2 * int(j), 4 + 2 * int(j))]
 
 
-for env in ({"EKF_ROWS": "0"}, {}):
+for env in ({},):  # (the device-epoch default)
     lo, hi = 0, W
     def bad(k):
         xd, Sd = state_after(k, env)

@@ -32,7 +32,7 @@ print(f"N={N} messages={W} (survey {sc.n_warm}) markers/msg {sc.count.mean():.2f
 
 
 def run(env, per_msg=False, dtype=pyekf.EKF_F64, upto=None):
-    for k in ("EKF_SERIAL", "EKF_DEVSYNC", "EKF_ROWS", "EKF_CU_SPLIT", "EKF_RESIDENT"):
+    for k in ("EKF_SERIAL", "EKF_DEVSYNC", "EKF_CU_SPLIT", "EKF_RESIDENT"):
         os.environ.pop(k, None)
     os.environ.update(env)
     e = pyekf.EKF(n_landmarks=N, dtype=dtype)
@@ -67,7 +67,6 @@ def run(env, per_msg=False, dtype=pyekf.EKF_F64, upto=None):
 
 
 for env, pm in (({}, False), ({"EKF_SERIAL": "1"}, False), ({"EKF_DEVSYNC": "1"}, False),
-                ({"EKF_ROWS": "0"}, False), ({"EKF_SERIAL": "1", "EKF_ROWS": "0"}, False),
                 ({}, True), ({"EKF_SERIAL": "1"}, True)):
     run(env, pm)
 
