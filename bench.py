@@ -552,6 +552,9 @@ def run(args, rank, world, local, backend=None):
         clk.append(("enqueued", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                     time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
     ekf.sync()  # the library's streams
+    if trace:
+        clk.append(("lib_synced", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+                    time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
     be.sync()   # device-wide (torch.cuda.synchronize on the GPU): nothing may be left running
     # this rank's own region (its K messages, enqueue to device-wide sync); the closing barrier
     # aligns the ranks, and reduce_ranks takes the MAX of these over ranks

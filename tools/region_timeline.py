@@ -26,7 +26,8 @@ for r in (csv.DictReader(open(glob.glob(d + "/*hip_api_trace.csv")[0]))
         api.append((a, b, r["Function"]))
 api.sort()
 us = lambda t: (t - t0) / 1e3
-print(f"host: enqueue returns {us(tq):.1f} us, synced {us(t1):.1f} us")
+print(f"host: enqueue returns {us(tq):.1f} us, synced {us(t1):.1f} us" +
+      (f" (library streams synced {us(clk['lib_synced']):.1f} us)" if "lib_synced" in clk else ""))
 first_api = api[0] if api else None
 if first_api:
     print(f"first HIP API call {first_api[2]} at {us(first_api[0]):.1f} us")
