@@ -56,12 +56,12 @@ WORKLOADS = {
                                               "N=1024 slots, 960 mapped landmarks, fp32"),
     "n1024_fp64_assoc": (1024, "f64", 1, 16, "configs[2] with unknown association (sensor_cb): "
                                               "N=1024 slots, 960 mapped landmarks, fp64"),
-    # the Joseph-form covariance update (BASELINE.json north_star, ekf_set_joseph): chunks of ≤ 8
-    # markers, two Σ passes per 16-marker message, each of rank 2 + 4m
+    # the Joseph-form covariance update (BASELINE.json north_star, ekf_set_joseph): one chunk per
+    # 16-marker message, one Σ pass of rank 2 + 4m
     "n1024_fp32_joseph": (1024, "f32", 1, 16, "configs[2] with the Joseph-form Sigma update "
                                                "(north_star): N=1024, 1 filter, fp32"),
 }
-JOSEPH_CHUNK = 8  # markers per Joseph-form chunk (kMaxJoseph, ekf_device.hpp)
+JOSEPH_CHUNK = 16  # markers per Joseph-form chunk (kMaxJoseph, ekf_device.hpp)
 ASSOC_FREE_SLOTS = 64  # association workloads map N − 64 landmarks (room for new ones)
 
 
@@ -622,7 +622,7 @@ def run(args, rank, world, local, backend=None):
         wsz = 4 if dt == "f32" else 8
         n = 3 + 2 * N
         # the rank-(2+2m) update's useful flops (fp64: the upper triangle, the symmetric pass);
-        # Joseph: rank 2 + 4·8 per pass, ⌈m/8⌉ passes per message
+        # Joseph: rank 2 + 4m per pass, ⌈m/16⌉ = 1 pass per message
         rank_k = 2 + 4 * min(m, JOSEPH_CHUNK) if joseph else 2 + 2 * m
         passes = -(-m // JOSEPH_CHUNK) if joseph else 1
         mfma_flops = 2.0 * rank_k * (n * n if wsz == 4 else n * (n + 1) / 2) * F
@@ -674,13 +674,13 @@ def run(args, rank, world, local, backend=None):
                          "frac": mfma_flops / avg_sig_s / 1e12 / MFMA_PEAK_TF[dt] if n_sig else 0.0,
                          "formula": (f"2*k*n^2*F = 2*{rank_k}*{n}^2*{F}" if wsz == 4 else
                                      f"2*k*n(n+1)/2*F = 2*{rank_k}*{n}*{n + 1}/2*{F}") +
-                                    f", k = {'2+4*8 (Joseph chunk)' if joseph else '2+2m'}",
+                                    f", k = {'2+4m (Joseph)' if joseph else '2+2m'}",
                          "pmc": traffic.get("mfma_busy") if traffic else traffic_err},
                 "chain_kernel_avg_us": ms_gain / max(n_gain, 1) * 1e3,
                 "factor_kernel_avg_us": ms_fac / max(n_fac, 1) * 1e3,
                 # the whole step against the rank-2m ceiling: one Σ pass per
-                # message is the algorithmic minimum, sigma_pass_bytes per step (Joseph: one
-                # pass per chunk of 8, two per message)
+                # message is the algorithmic minimum, sigma_pass_bytes per step (the Joseph form
+                # too: one pass of rank 2 + 4m per message)
                 "end_to_end": {
                     "bytes_per_step": passes * bytes_per_launch,
                     "passes_per_step": passes,

@@ -426,8 +426,8 @@ int assoc(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, bool poll) {
 // absent[k] (batch paths): filter f0+k receives no message this step — its descriptor is inactive,
 // nothing of it changes (an empty MarkerArray is rejected before anything changes, EKF_E_EMPTY).
 void plan_known(ekf_ctx* h, int f0, int nf, bool predict, const char* absent = nullptr) {
-  // Joseph form on the pipeline: ≤ kMaxJoseph markers per chunk (the chain's row map Z holds K's and
-  // V = ΣHᵀ − K·S's columns, 4 per marker; k_chain)
+  // Joseph form on the pipeline: ≤ kMaxJoseph (= kMaxChunk) markers per chunk (the chain's row map
+  // Z holds K's and V = ΣHᵀ − K·S's columns, 4 per marker; k_chain<T, true>)
   const bool jos = h->joseph && !h->resident;
   const int cm = jos ? kMaxJoseph : kMaxChunk;
   int chunks = 1;
@@ -1358,10 +1358,7 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
     return EKF_E_ARG;
   if (h->resident) return EKF_E_ARG;
   if (T == 0) return EKF_OK;
-  // Joseph form: every message plans as two chunks of ≤ kMaxJoseph markers (the second one empty
-  // when the message has fewer: an exact copy pass), descriptors [2T][F]
-  const int jsh = h->joseph ? 1 : 0;
-  const int Tc = T << jsh;
+  // (Joseph form: one chunk per message too, kMaxJoseph = kMaxChunk, flagged kJoseph)
   hipSetDevice(h->cfg.device);
   if (int rc = flush(h)) return rc;  // what the host planned before runs first
   const size_t F = static_cast<size_t>(h->F);
@@ -1372,7 +1369,7 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
                       hipHostMallocDefault) != hipSuccess)
       return EKF_E_NOMEM;
   }
-  if (int rc = reserve_device(h, static_cast<size_t>(Tc) * F)) return rc;  // (no host staging)
+  if (int rc = reserve_device(h, static_cast<size_t>(T) * F)) return rc;  // (no host staging)
   // device epochs: the planner runs on the bulk stream — ahead of the group's factor kernels and
   // Σ passes in stream order — and counts its descriptors, which the chain launch polls: the chain
   // starts beside the planner instead of behind a main → bulk event hop (≈ 6 µs of each replay)
@@ -1416,7 +1413,7 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   a.st_out = h->dstate[h->dstate_cur ^ 1];
   a.desc = h->ddesc;
   a.T = T;
-  a.jsh = jsh;
+  a.joseph = h->joseph ? 1 : 0;
   a.F = h->F;
   a.M = m_max;
   a.N = h->cfg.n_landmarks;
@@ -1426,7 +1423,7 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   h->dstate_cur ^= 1;
   h->plan_stream = ps;
   if (beside) {
-    h->plan_total += static_cast<unsigned>(Tc) * static_cast<unsigned>(h->F);
+    h->plan_total += static_cast<unsigned>(T) * static_cast<unsigned>(h->F);
     h->need_plan = h->plan_total;
   } else {
     // the bulk stream reads these descriptors too: one main → bulk hop (recorded before the
@@ -1439,15 +1436,15 @@ int ekf_replay_device(ekf_t h, int T, int m_max, const int* d_counts, const int*
   int rc = EKF_OK;
   if (h->devsync && !h->serial) {
     // (the device planner stages only for chunks two on inside this replay: kStageOut needs next2)
-    rc = group(h, h->ddesc, nullptr, 0, h->F, Tc, true, true, false, stg ? Tc - 2 : 0);
+    rc = group(h, h->ddesc, nullptr, 0, h->F, T, true, true, false, stg ? T - 2 : 0);
   } else {
     // Events: a chunk t ≥ 1 needs the Σ pass two back (kLook), or — no message of its filter
     // earlier in this replay — the passes before the replay, which the first chunk's join covers:
     // the wait on the pass two back suffices, and the chain of t runs beside the factor kernel and
     // Σ pass of t − 1 where the CUs allow (not a join of the whole bulk stream per message)
-    for (int t = 0; t < Tc && !rc; ++t)
+    for (int t = 0; t < T && !rc; ++t)
       rc = group(h, h->ddesc + static_cast<size_t>(t) * F, nullptr, 0, h->F, 1, true, t == 0, true,
-                 stg && t + 2 < Tc ? 1 : 0);
+                 stg && t + 2 < T ? 1 : 0);
   }
   h->main_dirty = true;
   if (!rc && (h->dbg_order & 32u) && drain(h)) return EKF_E_HIP;
@@ -1532,6 +1529,14 @@ int ekf_get_assoc_route(ekf_t h, int* route) {
 int ekf_set_joseph(ekf_t h, int on) {
   if (!h) return EKF_E_ARG;
   if (int rc = flush(h)) return rc;  // what is planned runs with the form it was planned in
+  if (h->joseph == (on != 0)) return EKF_OK;
+  // a simple-form chain cannot rebuild from a Joseph chunk's record (its V columns): the first
+  // chunk of each filter after a switch gathers its rows from Σ instead (no kLook)
+  if (int rc = adopt_device_plan(h)) return rc;
+  for (int f = 0; f < h->F; ++f) {
+    h->prev_m[f] = -1;
+    forget_desc(h, f);
+  }
   h->joseph = on != 0;
   return EKF_OK;
 }

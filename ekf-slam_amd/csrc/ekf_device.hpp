@@ -14,11 +14,14 @@ namespace ekfslam {
 
 constexpr int kMaxChunk = 16;                    // markers folded into one Σ pass (EKF_MAX_CHUNK)
 constexpr int kMaxU = 3 + 2 * kMaxChunk;         // touched rows/cols of one chunk: pose + 2 per marker
-constexpr int kMaxKW = ((2 + 2 * kMaxChunk + 3) / 4) * 4;  // rank of the fused update, padded to 4
 constexpr int kMaxAssoc = 64;                    // association slots per filter per upload
 constexpr int kZC = 2 * kMaxChunk;               // correction columns of Z / rows of Y
-constexpr int kMaxJoseph = kMaxChunk / 2;        // markers of a Joseph-form chunk: its row map Z
-                                                 // holds K's and V's columns (4 per marker)
+constexpr int kMaxJoseph = kMaxChunk;            // markers of a Joseph-form chunk (round 6: a whole
+                                                 // message, one Σ pass); its row map Z holds K's and
+                                                 // V's columns, 4 per marker
+constexpr int kZJ = 4 * kMaxJoseph;              // the record's Z columns (Joseph: Z then Zv)
+// rank of the fused update, padded to 4: 2 + 2m (simple form), 2 + 4m (Joseph form)
+constexpr int kMaxKW = ((2 + 4 * kMaxJoseph + 3) / 4) * 4;
 
 // Device epochs (unsigned words of the handle's sync buffer, each polled word on its own line):
 constexpr int kSyncSigma = 0;    // epoch (seq + 1) of the last complete Σ pass (k_sigma_epoch)
@@ -86,7 +89,7 @@ struct alignas(16) ChunkRec {
   double col0raw[kMaxU];             // Σ_in[u_a][0]
   double Zx[kMaxU];
   double xU[kMaxU];
-  double Z[kMaxU][kZC];
+  double Z[kMaxU][kZJ];   // columns 0..2m−1: Z; Joseph also 2m..4m−1: Zv (the rest zero)
   double Y[kZC][kMaxU];
   double Pend[kMaxU][kMaxU];         // the chain's final Σ[U, U] (fp64): written over the Σ pass's
                                      // block so fp32 Σ keeps first sightings (1e7 − (1e7 − δ))

@@ -129,7 +129,13 @@ __device__ __forceinline__ d4 mfma_f64(double a, double b, d4 c) {
 
 
 
-struct ChainShared {
+// J: the Joseph-form instantiation (round 6: a whole message of ≤ 16 markers per chunk): its row
+// maps Z hold Zv beside Z (4m ≤ 64 columns) and V, S, C', D' are kept per step; the simple form's
+// instantiation keeps the round-5 layout (ZC = 32 columns, one unused slot for the Joseph arrays).
+template <bool J>
+struct ChainSharedT {
+  static constexpr int ZC = J ? kZJ : kZC;     // Z columns (the chain's and the rebuilt pv.Z / pv.K)
+  static constexpr int JM = J ? kMaxJoseph : 1;  // Joseph steps kept
   int u[kMaxU];
   int skip[kMaxChunk];
   double alphaU[kMaxU];
@@ -141,7 +147,7 @@ struct ChainShared {
   double Dy[kMaxChunk][4];  // wave 2, step c: D_k = H·K_k[pA_c] (2×2) for k < c
   double KU[kMaxChunk][kMaxU][2];
   double MU[kMaxChunk][kMaxU][2];
-  double Z[kMaxU][kZC + 1];      // K_c[i] = r_0(i)[U] · Z[:, 2c..2c+1]
+  double Z[kMaxU][ZC + 1];       // K_c[i] = r_0(i)[U] · Z[:, 2c..2c+1] (Joseph: Zv in 2m + 2c..)
   double Y[kZC][kMaxU + 1];      // M_c[:, j] = Y[2c..2c+1, :] · c_0(j)[U]
   double Zx[kMaxU];              // Σ_c Z_c ν_c: x_i += r_0(i)[U] · Zx
   double nu[kMaxChunk][2];
@@ -149,10 +155,10 @@ struct ChainShared {
   double Sis[kMaxChunk][4];      // S_c⁻¹
   // Joseph chunks (m ≤ kMaxJoseph): V_c = (Σ_c·Hᵀ − K_c·S_c)[U] and S_c per step (wave 0), wave 1's
   // C'_k = K_k[pA_c]ᵀ·Hᵀ and wave 2's D'_k = H·V_k[pA_c]
-  double VU[kMaxJoseph][kMaxU][2];
-  double Ss[kMaxJoseph][4];
-  double Cv[kMaxJoseph][4];
-  double Dv[kMaxJoseph][4];
+  double VU[JM][kMaxU][2];
+  double Ss[JM][4];
+  double Cv[JM][4];
+  double Dv[JM][4];
   // kLook: the previous chunk's record and the blocks rebuilt from it
   struct {
     int u[kMaxU];
@@ -160,11 +166,11 @@ struct ChainShared {
     double a1, a2, s00;
     double xU[kMaxU], Zx[kMaxU];
     // k (over U') padded to kMaxU + 1 = 36 with zeros, so MFMA operand reads need no predicate
-    double Z[kMaxU + 1][kZC + 1];
+    double Z[kMaxU + 1][ZC + 1];
     double Y[kZC][kMaxU + 1];
     double R[kMaxU][kMaxU + 1];       // Σ_pred'[U][U']  (U' = previous chunk's index set)
     double C[kMaxU + 1][kMaxU + 1];   // Σ_pred'[U'][U]
-    double K[kMaxU][kZC + 1];     // R·Z'  = the previous K_c at U
+    double K[kMaxU][ZC + 1];      // R·Z'  = the previous K_c at U (Joseph: and V_c at U)
     double M[kZC][kMaxU + 1];     // Y'·C  = the previous M_c at U
     double r0U[kMaxU], c0U[kMaxU], r0P[kMaxU], c0P[kMaxU];
     double xg[kMaxU];             // x_in'[u] for this chunk's U (rows the previous chunk missed)
@@ -213,7 +219,8 @@ __device__ __forceinline__ void lds_wait_ge(const int* flag, int v) {
 // Wave 0's corrections (see k_chain, A2): a function of its own, so that its register allocation
 // is not the one of the kernel's four wave programs together (the shared allocation spilled
 // SGPRs, and their reloads sat in this loop). LDS through address-space-3 references.
-typedef __attribute__((address_space(3))) ChainShared LdsChain;
+template <bool J>
+using LdsChain = __attribute__((address_space(3))) ChainSharedT<J>;
 typedef __attribute__((address_space(3))) const MsgDesc LdsDesc;
 typedef __attribute__((address_space(3))) double ldsd;
 __device__ __forceinline__ void lds_publish3(__attribute__((address_space(3))) int* flag, int v) {
@@ -261,9 +268,10 @@ __device__ __forceinline__ void steplog(unsigned long long* lg, int c, int slot,
 }
 
 template <bool J>
-__device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int m, int nu,
+__device__ __noinline__ void chain_wave0(LdsChain<J>* shp, LdsDesc* dp, int pb, int m, int nu,
                                          double r_noise, unsigned seq, unsigned long long* lg) {
-  LdsChain& sh = *shp;
+  LdsChain<J>& sh = *shp;
+  constexpr int JM = ChainSharedT<J>::JM;
   LdsDesc& d = *dp;
   const int lane = threadIdx.x & 63;
   (void)seq;  // (diagnostic stamps)
@@ -424,7 +432,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       xq[3] = rank2_sub(qn[0], kqx, kqy, mp0, mp1);
       xq[4] = rank2_sub(qn[1], kq2x, kq2y, mp0, mp1);
       if (J) {  // − V_{c−1}·K_{c−1}ᵀ (step 0: vp = kp = 0)
-        const int cj = min(cp, kMaxJoseph - 1);
+        const int cj = min(cp, JM - 1);
         const double vqx = sh.VU[cj][l0][0], vqy = sh.VU[cj][l0][1];
         const double vq2x = sh.VU[cj][l0 + 1][0], vq2y = sh.VU[cj][l0 + 1][1];
         xr[3] = rank2_sub(xr[3], vp0, vp1, kqx, kqy);
@@ -490,7 +498,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
       md[0] = in ? mm0 : 0.0;
       md[1] = in ? mm1 : 0.0;
       if (J) {  // V and S of the step, for waves 1–3 and the fp32 block patch
-        const int cj = min(c, kMaxJoseph - 1);
+        const int cj = min(c, JM - 1);
         ldsd* vd = st ? &sh.VU[cj][lane][0] : &sh.junk2[lane][0];
         vd[0] = in ? V0 : 0.0;
         vd[1] = in ? V1 : 0.0;
@@ -525,7 +533,7 @@ __device__ __noinline__ void chain_wave0(LdsChain* shp, LdsDesc* dp, int pb, int
         mx0[k] = mkx;
         mx1[k] = mky;
         if (J) {
-          const int cj = min(c, kMaxJoseph - 1);
+          const int cj = min(c, JM - 1);
           vx0[k] = sh.VU[cj][l][0];
           vx1[k] = sh.VU[cj][l][1];
         }
@@ -600,8 +608,8 @@ __device__ __forceinline__ void special_entry(int s, int& a, int& b) {
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void rebuild_rcd(ChainShared& sh, double (&P)[kMaxU][kMaxU + 1],
+template <typename T, typename Shared>
+__device__ __forceinline__ void rebuild_rcd(Shared& sh, double (&P)[kMaxU][kMaxU + 1],
                                             const T (&vd)[kRebPer], const T (&vr)[kRebPer],
                                             const T (&vc)[kRebPer], int tid, int nu, int np,
                                             double q) {
@@ -677,10 +685,12 @@ __device__ __forceinline__ void rebuild_rcd(ChainShared& sh, double (&P)[kMaxU][
   }
 }
 
-struct FactorShared {
+template <bool J>
+struct FactorSharedT {
+  static constexpr int ZC = J ? kZJ : kZC;  // the record's Z columns in use (Joseph: Z and Zv)
   int u[kMaxU + 1];
   double alphaU[kMaxU], row0raw[kMaxU], col0raw[kMaxU], Zx[kMaxU], xU[kMaxU];
-  double Z[kMaxU][kZC + 1];
+  double Z[kMaxU][ZC + 1];
   double Y[kZC][kMaxU + 1];
   double a1, a2, s00;
   int nu;
@@ -689,22 +699,35 @@ struct FactorShared {
 // The factor kernel's two halves: a chunk's record into LDS, then one wave's 16 indices of Kcat = R_pred·Z (rows) and
 // Mcat = Y·C_pred (columns) on f64 MFMA, plus the new state.
 // R_pred(i)[b] = Σ_pred[i][u_b], C_pred(j)[a] = Σ_pred[u_a][j].
-__device__ __forceinline__ void factor_record(const ChunkRec* rec, FactorShared& sh, int tid) {
+template <bool J>
+__device__ __forceinline__ void factor_record(const ChunkRec* rec, FactorSharedT<J>& sh, int tid) {
+  constexpr int ZC = FactorSharedT<J>::ZC;
   {  // the record into LDS: every load of a thread issued before its first LDS store
     constexpr int kPer = (kMaxU * kZC + 255) / 256;  // 5
-    double vz[kPer], vy[kPer];
+    constexpr int kPerZ = (kMaxU * ZC + 255) / 256;  // 5 (Joseph: 9)
+    double vz[kPerZ], vy[kPer];
+#pragma unroll
+    for (int i = 0; i < kPerZ; ++i) {  // (the record's rows are kZJ wide)
+      const int e = min(tid + 256 * i, kMaxU * ZC - 1);
+      vz[i] = rec->Z[e / ZC][e % ZC];
+    }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = min(tid + 256 * i, kMaxU * kZC - 1);
-      vz[i] = (&rec->Z[0][0])[e];
       vy[i] = (&rec->Y[0][0])[e];
+    }
+#pragma unroll
+    for (int i = 0; i < kPerZ; ++i) {
+      const int e = tid + 256 * i;
+      if (e < kMaxU * ZC) {
+        const int b = e / ZC, k = e - b * ZC;
+        sh.Z[b][k] = vz[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + 256 * i;
       if (e < kMaxU * kZC) {
-        const int b = e / kZC, k = e - b * kZC;
-        sh.Z[b][k] = vz[i];
         const int k2 = e / kMaxU, b2 = e - k2 * kMaxU;
         sh.Y[k2][b2] = vy[i];
       }
@@ -726,9 +749,10 @@ __device__ __forceinline__ void factor_record(const ChunkRec* rec, FactorShared&
   }
 }
 
-template <typename T>
+template <typename T, bool J>
 __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc& d, int f, int wg,
-                                            const FactorShared& sh, int lane) {
+                                            const FactorSharedT<J>& sh, int lane) {
+  constexpr int NG = FactorSharedT<J>::ZC / 16;  // 16-column groups of Z: 2 (Joseph: 4)
   const int n = A.n, ld = A.ld, ldk = A.ldk;
   const T* S = A.sig[d.parity] + f * A.sig_stride;
   const double* xin = A.x[d.parity] + f * A.x_stride;
@@ -736,7 +760,7 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
   T* kc = A.kcat + f * A.km_stride;
   T* mc = A.mcat + f * A.km_stride;
   const bool first = (d.flags & kFirst) != 0;
-  const bool joseph = (d.flags & kJoseph) != 0;
+  const bool joseph = J && (d.flags & kJoseph) != 0;
   // Joseph: Mcat rows 2 + 2m .. 2 + 4m − 1 hold K_c (the V_c·K_cᵀ term's column factor), written
   // by the row waves; the column waves leave them alone
   const int jk0 = joseph ? 2 * d.m : kZC, jk1 = joseph ? 4 * d.m : kZC;
@@ -826,17 +850,18 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
       }
       av[s] = v;
     }
-    d4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, acc2 = {0, 0, 0, 0};
+    d4 acc[NG], acc2 = {0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[g] = d4{0, 0, 0, 0};
 #pragma unroll
     for (int s = 0; s < 9; ++s) {
       const int k = 4 * s + ks;
-      const double z0 = k < kMaxU ? sh.Z[k][l16] : 0.0;
-      const double z1 = k < kMaxU ? sh.Z[k][16 + l16] : 0.0;
       const double zx = (k < kMaxU && l16 == 0) ? sh.Zx[k] : 0.0;
       // Zᵀ·R rather than R·Z: the lane then holds Kcat[c = ks + 4r][i = R0 + l16], so each store
       // covers 4 factor rows × 128 B instead of 16 rows × 32 B (the same products and sums)
-      acc0 = mfma_f64(z0, av[s], acc0);
-      acc1 = mfma_f64(z1, av[s], acc1);
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+        acc[g] = mfma_f64(k < kMaxU ? sh.Z[k][16 * g + l16] : 0.0, av[s], acc[g]);
       acc2 = mfma_f64(zx, av[s], acc2);
     }
     if (kDiagBuild && (A.dbg & 16)) {  // Σ_in as read, x_in as read
@@ -861,14 +886,15 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
     }
     if (vi) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = ks + 4 * r;
-        kc[(2 + c) * ldk + i] = static_cast<T>(acc0[r]);
-        kc[(18 + c) * ldk + i] = static_cast<T>(acc1[r]);
-        // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
-        // (2m ≤ 16: acc0 holds every K_c)
-        if (joseph && c < jk0) mc[(2 + jk0 + c) * ldk + i] = static_cast<T>(acc0[r]);
-      }
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * g + ks + 4 * r;
+          kc[(2 + c) * ldk + i] = static_cast<T>(acc[g][r]);
+          // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
+          // (Z columns 0 .. 2m − 1 ≤ 31: the first two groups hold every K_c)
+          if (J && g < 2 && joseph && c < jk0) mc[(2 + jk0 + c) * ldk + i] = static_cast<T>(acc[g][r]);
+        }
     }
     if (merged) columns(i, raw, r0t);
   } else if (!merged && wg < 2 * row_tiles) {
@@ -908,9 +934,10 @@ __device__ void dbg_seq_check(const PassArgs<T>& A, int k, int f, unsigned e) {
   *last = e;
 }
 
-template <typename T>
+template <typename T, bool J>
 __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchunks) {
-  __shared__ ChainShared sh;
+  __shared__ ChainSharedT<J> sh;
+  constexpr int ZC = ChainSharedT<J>::ZC, JM = ChainSharedT<J>::JM;
   // The descriptor is read every step: keep it in LDS. Two buffers: a chunk's epilogue prefetches
   // the next one's (and computes its predicted pose from it).
   __shared__ MsgDesc sdesc[2];
@@ -922,7 +949,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   FilterCtl* ctl = A.ctl + f;
   // LDS starts as whatever the CU's previous kernel left (possibly NaN bit patterns): zero it once,
   // so padding rows / columns that feed MFMA or dot products as zeros really are zeros
-  for (int e = tid; e < static_cast<int>(sizeof(ChainShared) / 8); e += blockDim.x)
+  for (int e = tid; e < static_cast<int>(sizeof(sh) / 8); e += blockDim.x)
     reinterpret_cast<double*>(&sh)[e] = 0.0;
   // Every wave's zeroing stores must land before the one below: the word npose_ci lives in is
   // zeroed by a thread of another wave, and without the barrier that store could come after this
@@ -996,7 +1023,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // i.e. (I−KH)Σ(I−KH)ᵀ + K·R·Kᵀ expanded (slam.cpp:264-265's update in Joseph form). Row factor
   // V_c = G_c − K_c·S_c beside K_c, column factor K_cᵀ beside M_c: the record's Z carries V_c's
   // row map in columns 2m + 2c.., the chain's block gets the term step by step.
-  const bool joseph = (d.flags & kJoseph) != 0;
+  const bool joseph = J && (d.flags & kJoseph) != 0;
   if ((kDiagBuild && (A.dbg & 16)) && tid < static_cast<int>(sizeof(MsgDesc) / 8))
     dlog_add(A, 0, seq, f, 0, reinterpret_cast<const unsigned long long*>(&d)[tid]);
 
@@ -1006,10 +1033,12 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
 
   constexpr int kW = kMaxU + 1;  // block entries are indexed e = a·36 + b (constant divisor)
   constexpr int kPer = (kW * kW + kChainThreads - 1) / kChainThreads;  // 6
+  // the previous record's Z (|U| rows of ZC, the record's rows kZJ wide) and Y (kZC rows)
+  constexpr int kPerZ = (kMaxU * ZC + kChainThreads - 1) / kChainThreads;  // 5 (Joseph: 9)
   // kLook with staged operands: the loads do not depend on A0's index sets, so they are issued
   // here and land during A0 (whose barrier orders LDS only)
   const bool early = look && (d.flags & kStageIn);
-  double vz[kPer], vy[kPer];
+  double vz[kPerZ], vy[kPer];
   T vd[kPer], vr[kPer], vc[kPer];  // (as stored: half the registers at fp32 while A0 runs)
   double r0u = 0.0, c0u = 0.0, r0p = 0.0, c0p = 0.0, x2 = 0.0;
   double x0 = 0.0, x1 = 0.0, pa1 = 0.0, pa2 = 0.0, tq = 0.0;
@@ -1027,9 +1056,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     constexpr unsigned oZ = offsetof(ChunkRec, Z), oY = offsetof(ChunkRec, Y);
     constexpr unsigned oV = offsetof(StageRec<T>, v), oT = kW * kW * sizeof(T);
 #pragma unroll
+    for (int i = 0; i < kPerZ; ++i) {
+      const int e = tid + i * kChainThreads, ez = e < kMaxU * ZC ? e : 0;
+      vz[i] = ld_f64(rr, oZ + 8u * ((ez / ZC) * kZJ + ez % ZC), 0);
+    }
+#pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * kChainThreads, es = min(e, kW * kW - 1);
-      vz[i] = ld_f64(rr, oZ + 8u * (e < kMaxU * kZC ? e : 0), 0);
       vy[i] = ld_f64(rr, oY + 8u * (e < kZC * kMaxU ? e : 0), 0);
       vd[i] = ld_t(rs, oV + sizeof(T) * es, T{});
       vr[i] = ld_t(rs, oV + oT + sizeof(T) * es, T{});
@@ -1099,9 +1132,13 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const int tc = tid < kMaxU ? tid : 0;
     if (!early) {  // (early: the staged operands and the record's values are in registers)
 #pragma unroll
+      for (int i = 0; i < kPerZ; ++i) {
+        const int e = tid + i * kChainThreads, ez = e < kMaxU * ZC ? e : 0;
+        vz[i] = rp->Z[ez / ZC][ez % ZC];
+      }
+#pragma unroll
       for (int i = 0; i < kPer; ++i) {
         const int e = tid + i * kChainThreads;
-        vz[i] = (&rp->Z[0][0])[e < kMaxU * kZC ? e : 0];
         vy[i] = (&rp->Y[0][0])[e < kZC * kMaxU ? e : 0];
         const int a = min(e / kW, kMaxU - 1), b = min(e % kW, kMaxU - 1);  // clamped: in bounds
         const size_t ua = static_cast<size_t>(sh.u[a]) * ld, pa = static_cast<size_t>(sh.pv.u[b]);
@@ -1129,8 +1166,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
 #pragma unroll
       for (int i = 0; i < kPer; ++i) {
         s2 += dbits(vd[i]) + dbits(vr[i]) + dbits(vc[i]);
-        s4 += dbits(vz[i]) + dbits(vy[i]);
+        s4 += dbits(vy[i]);
       }
+#pragma unroll
+      for (int i = 0; i < kPerZ; ++i) s4 += dbits(vz[i]);
       if (tid < kMaxU) {
         s2 += dbits(r0u) + dbits(c0u) + dbits(r0p) + dbits(c0p);
         s4 += dbits(x0) + dbits(x1);
@@ -1142,15 +1181,17 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       dlog_add(A, 0, seq, f, 4, s4);
     }
 #pragma unroll
+    for (int i = 0; i < kPerZ; ++i) {
+      const int e = tid + i * kChainThreads;
+      if (e < kMaxU * ZC) (&sh.pv.Z[0][0])[(e / ZC) * (ZC + 1) + e % ZC] = vz[i];
+    }
+#pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = tid + i * kChainThreads;
-      if (e < kMaxU * kZC) (&sh.pv.Z[0][0])[(e / kZC) * (kZC + 1) + e % kZC] = vz[i];
       if (e < kZC * kMaxU) (&sh.pv.Y[0][0])[(e / kMaxU) * (kMaxU + 1) + e % kMaxU] = vy[i];
     }
-    if (tid < kZC) {  // the 36th k row / column
-      sh.pv.Z[kMaxU][tid] = 0.0;
-      sh.pv.Y[tid][kMaxU] = 0.0;
-    }
+    if (tid < ZC) sh.pv.Z[kMaxU][tid] = 0.0;  // the 36th k row / column
+    if (tid < kZC) sh.pv.Y[tid][kMaxU] = 0.0;
     if (tid < kMaxU) {
       sh.pv.r0U[tid] = r0u;
       sh.pv.c0U[tid] = c0u;
@@ -1180,6 +1221,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // outputs, k ≥ |U'| is zero-padded in both operands, so every k-step runs: its MFMA adds exact
     // zeros). A wave's tiles and its VALU work are one basic block (operand reads first, then two
     // interleaved accumulation chains beside the dot product): the MFMA and VALU pipes overlap.
+    if constexpr (!J) {
     auto kmphase = [&](auto w3c) {
       constexpr bool W3 = decltype(w3c)::value;
       double av[2][9], bv[2][9];
@@ -1264,17 +1306,6 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     EKF_STAMP(7);
     __syncthreads();
     EKF_STAMP(5);
-    // a Joseph chunk before: its V'·K'ᵀ terms as rank 2m'..4m'−1 (K' columns 2m'.. are
-    // V' = R·Z'[:, 2m'..]; M' rows 2m'.. become K'ᵀ, the column factor)
-    const bool pj = sh.pv.joseph != 0;
-    const int pm2 = 2 * min(sh.pv.m, kMaxJoseph);
-    if (pj) {
-      for (int e = tid; e < pm2 * kW; e += blockDim.x) {
-        const int k = e / kW, b = e - k * kW;
-        sh.pv.M[pm2 + k][b] = b < kMaxU ? sh.pv.K[b][k] : 0.0;
-      }
-      __syncthreads();
-    }
     // P = D − K'·M' on the 48×48 padded block: 9 tiles over the 4 waves (K' columns and M' rows
     // ≥ 2m' are zero because Z' / Y' are; a Joseph chunk's are ≥ 4m')
     // (every k-step runs: K' columns and M' rows beyond the chunk's rank are zero, so their MFMAs
@@ -1310,6 +1341,117 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         if (row < nu && col < nu) P[row][col] = acc[r];
       }
       if (tid < 201 && brow < nu && bcol < nu) P[brow][bcol] = bv0 - ((bs[0] + bs[1]) + (bs[2] + bs[3]));
+    }
+    } else {
+    // Joseph form (ZC = 64): K' = R·Z' is 35 × 4m' (K' then V' columns), M' = Y'·C is 2m' × 35.
+    // Their 16 × 16 cores are 12 tiles, three per wave (one after another, each operand read waited
+    // for once); the bands K'[32..34][·] (192 outputs) and M'[·][32..34] (96) are VALU dot products
+    // of waves 0–2 (two per thread for the first 96), wave 3 forms x_in[U] as in the simple form.
+    auto kmphase = [&](auto w3c) {
+      constexpr bool W3 = decltype(w3c)::value;
+#pragma unroll 1
+      for (int q = 0; q < 3; ++q) {
+        const int tt = wv + 4 * q;  // 0..7 K' tiles (2 × 4), 8..11 M' tiles (2 × 2)
+        const bool kt = tt < 8;
+        const int ti = kt ? tt >> 2 : (tt - 8) >> 1, tj = kt ? tt & 3 : (tt - 8) & 1;
+        const double* pa = kt ? &sh.pv.R[16 * ti + i16][0] : &sh.pv.Y[16 * ti + i16][0];
+        const double* pb = kt ? &sh.pv.Z[0][16 * tj + i16] : &sh.pv.C[0][16 * tj + i16];
+        const int sb = kt ? ZC + 1 : kMaxU + 1;
+        double av[9], bv[9];
+#pragma unroll
+        for (int s0 = 0; s0 < 9; ++s0) {
+          av[s0] = pa[4 * s0 + k4];
+          bv[s0] = pb[(4 * s0 + k4) * sb];
+        }
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s0 = 0; s0 < 9; ++s0) acc = mfma_f64(av[s0], bv[s0], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (kt) sh.pv.K[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[r];
+          else sh.pv.M[16 * ti + k4 + 4 * r][16 * tj + i16] = acc[r];
+        }
+      }
+      if (!W3) {
+#pragma unroll 1
+        for (int t = tid; t < 288; t += 192) {
+          const bool bk = t < 192;  // K'[32 + t/64][t%64] = R[row]·Z'[:, col], else M'[u/3][32 + u%3]
+          const int u = t - 192;
+          const int brow = bk ? 32 + (t >> 6) : u / 3, bcol = bk ? (t & 63) : 32 + u % 3;
+          const double* ra = bk ? &sh.pv.R[min(brow, kMaxU - 1)][0] : &sh.pv.Y[brow][0];
+          const double* cb = bk ? &sh.pv.Z[0][bcol] : &sh.pv.C[0][min(bcol, kMaxU)];
+          const int sc = bk ? ZC + 1 : kMaxU + 1;
+          double bacc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int k = 0; k < kMaxU + 1; ++k) bacc[k & 3] = fma(ra[k], cb[k * sc], bacc[k & 3]);
+          const double v = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);
+          if (bk) sh.pv.K[brow][bcol] = v;
+          else if (bcol < kMaxU) sh.pv.M[brow][bcol] = v;
+        }
+      } else {
+        // x_in[U]: the previous chunk's x[U'] where it has it, else x' + r'(i)·Zx'
+        const int l = ln < kMaxU ? ln : kMaxU - 1;
+        const int u = sh.u[l];
+        int pos = -1;
+#pragma unroll
+        for (int k = kMaxU - 1; k >= 0; --k) pos = (k < np && sh.pv.u[k] == u) ? k : pos;
+        double bacc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < kMaxU; ++k) bacc[k & 3] = fma(sh.pv.R[l][k], sh.pv.Zx[k], bacc[k & 3]);
+        const double r = (bacc[0] + bacc[1]) + (bacc[2] + bacc[3]);  // R[·][k ≥ |U'|] = 0
+        const double xres = pos >= 0 ? sh.pv.xU[pos] : sh.pv.xg[l] + r;
+        if (ln < nu) sh.xU[0][ln] = xres;
+        if (ln < 3) sh.xpose[ln] = sh.pv.xU[ln];  // pose ∈ U' always
+      }
+    };
+    if (wv == 3)
+      kmphase(std::true_type{});
+    else
+      kmphase(std::false_type{});
+    EKF_STAMP(7);
+    __syncthreads();
+    EKF_STAMP(5);
+    // P = D − K'·M'full with M'full = [M' (2m' rows); K'[:, 0..2m')ᵀ (a Joseph chunk before: its
+    // V'·K'ᵀ terms, V' = K' columns 2m'..4m')], k < 4m' ≤ 64: 16 k-steps of the 32 × 32 core, one
+    // 16 × 16 tile per wave, and the 3-wide bands (201 entries) as VALU dot products. The k order is
+    // the round-5 form's (M' rows, then K'ᵀ, then zeros), so up to 8 markers the same sums.
+    {
+      const bool pj = sh.pv.joseph != 0;
+      const int pm2 = 2 * sh.pv.m, pk2 = pj ? 4 * sh.pv.m : 2 * sh.pv.m;
+      auto mfull = [&](int k, int c) {  // M'full[k][c], c < kMaxU (every operand read clamped)
+        const double vm = sh.pv.M[min(k, kZC - 1)][c];
+        const double vk = sh.pv.K[c][max(min(k - pm2, ZC - 1), 0)];
+        return k < pm2 ? vm : (k < pk2 ? vk : 0.0);
+      };
+      const int ti = wv >> 1, tj = wv & 1;
+      const int col = 16 * tj + i16, ar = 16 * ti + i16;
+      double av[16], bv[16];
+#pragma unroll
+      for (int s0 = 0; s0 < 16; ++s0) {
+        av[s0] = -sh.pv.K[ar][4 * s0 + k4];
+        bv[s0] = mfull(4 * s0 + k4, col);
+      }
+      d4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = P[16 * ti + k4 + 4 * r][col];
+      // band entry: t < 105 → rows 32..34 × columns 0..34, then rows 0..31 × columns 32..34
+      const int t = tid < 201 ? tid : 200;
+      const int brow = t < 105 ? 32 + t / 35 : (t - 105) / 3;
+      const int bcol = t < 105 ? t - 35 * (t / 35) : 32 + (t - 105) - 3 * ((t - 105) / 3);
+      const int br = min(brow, kMaxU - 1), bc = min(bcol, kMaxU - 1);
+      double bs[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 8
+      for (int k = 0; k < ZC; ++k) bs[k & 3] = fma(sh.pv.K[br][k], mfull(k, bc), bs[k & 3]);
+      const double bv0 = P[br][bc];
+#pragma unroll
+      for (int s0 = 0; s0 < 16; ++s0) acc = mfma_f64(av[s0], bv[s0], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * ti + k4 + 4 * r;
+        if (row < nu && col < nu) P[row][col] = acc[r];
+      }
+      if (tid < 201 && brow < nu && bcol < nu) P[brow][bcol] = bv0 - ((bs[0] + bs[1]) + (bs[2] + bs[3]));
+    }
     }
     EKF_STAMPT(10, 64);
     EKF_STAMPT(11, 128);
@@ -1432,10 +1574,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   if (wave == 0) {
     unsigned long long* lg =
         (kDiagBuild && (A.dbg & 16)) ? A.dlog + (static_cast<size_t>(seq & 63u) * 64 + (f & 63)) * 8 : nullptr;
-    if (joseph)
-      chain_wave0<true>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq, lg);
-    else
-      chain_wave0<false>((LdsChain*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq, lg);
+    chain_wave0<J>((LdsChain<J>*)(&sh), (LdsDesc*)(&d), 0, m, nu, A.r, seq, lg);
   } else if (wave == 3) {  // P outside the cross: rows and columns ∉ the next marker's Bx
     // lane → column 3+(lane&31), rows 3.. of parity lane>>5. The lane's 16 entries stay in
     // registers for the whole chunk: every step's rank-2 term is applied to all of them — also to
@@ -1445,24 +1584,24 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     const int hb = lane & 31, hr = lane >> 5;
     const int b = min(3 + hb, kMaxU - 1);
     auto rest = [&](auto jc) {  // (Joseph: V_c[a]·K_c[b] after the K·M term, as wave 0 does)
-      constexpr bool J = decltype(jc)::value;
+      constexpr bool JR = decltype(jc)::value;
       double pv[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) pv[i] = P[min(3 + hr + 2 * i, kMaxU - 1)][b];  // clamped rows
       for (int c = 0; c + 1 < m; ++c) {
         lds_wait_ge(&sh.pub, c + 1);
         EKF_STAMPT(192 + 2 * c, 192);
-        const int nx = 5 + 2 * c, cj = min(c, kMaxJoseph - 1);
+        const int nx = 5 + 2 * c, cj = min(c, JM - 1);
         const bool colok = 3 + hb < nu && b != nx && b != nx + 1;
         const double mb0 = sh.MU[c][b][0], mb1 = sh.MU[c][b][1];
-        const double kb0 = J ? sh.KU[c][b][0] : 0.0, kb1 = J ? sh.KU[c][b][1] : 0.0;
+        const double kb0 = JR ? sh.KU[c][b][0] : 0.0, kb1 = JR ? sh.KU[c][b][1] : 0.0;
         double k0[16], k1[16], w0[16], w1[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {  // clamped rows: unconditional reads, no per-row wait
           const int a = min(3 + hr + 2 * i, kMaxU - 1);
           k0[i] = sh.KU[c][a][0];
           k1[i] = sh.KU[c][a][1];
-          if (J) {
+          if (JR) {
             w0[i] = sh.VU[cj][a][0];
             w1[i] = sh.VU[cj][a][1];
           }
@@ -1474,7 +1613,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           const int a = 3 + hr + 2 * i;
           const bool ok = colok && a < nu && a != nx && a != nx + 1;
           double v = rank2_sub(pv[i], k0[i], k1[i], mb0, mb1);
-          if (J) v = rank2_sub(v, w0[i], w1[i], kb0, kb1);
+          if (JR) v = rank2_sub(v, w0[i], w1[i], kb0, kb1);
           pv[i] = v;
           *(ok ? &P[a][b] : &sh.junk[3][lane]) = v;
         }
@@ -1482,10 +1621,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         EKF_STAMPT(193 + 2 * c, 192);
       }
     };
-    if (joseph)
-      rest(std::true_type{});
-    else
-      rest(std::false_type{});
+    rest(std::integral_constant<bool, J>{});
     // The posterior t_map_odom = T(x, y, θ)·t_odom_robot⁻¹ (slam.cpp:273-277) as soon as wave 0 has
     // published the last step (its x is stored before that), beside waves 1–2's last Z / Y and off
     // the epilogue (a pose composition's sin / cos on one lane)
@@ -1541,7 +1677,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     {  // columns ≥ 2m of the record's Z are zero (the factor kernel and a rebuilding chain read
        // them); Joseph keeps columns 2m..4m for V
       const int z0c = joseph ? 4 * m : 2 * m;
-      const int zw = kZC - z0c;
+      const int zw = ZC - z0c;
       for (int e = lane; e < kMaxU * zw; e += 64) {
         const int b = e / zw, k = z0c + (e - b * zw);
         st_wt(&rec->Z[b][k], 0.0);
@@ -1549,7 +1685,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     }
     const int li = lane < kMaxU ? lane : kMaxU - 1;
     double zxa = 0.0;  // Σ_c Z_c ν_c of row `lane`, accumulated as the Z_c come (the record's Zx)
-    if (!joseph) {
+    if constexpr (!J) {
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
       const int pj = 3 + 2 * c;
@@ -1630,7 +1766,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         if (lane < kMaxU) {
           sh.Z[lane][2 * c] = Z0;
           sh.Z[lane][2 * c + 1] = Z1;
-          st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
+          st_wt2(rr, oZ + 8 * (kZJ * lane + 2 * c), Z0, Z1);
         }
       }
       EKF_STAMPT(320 + c, 64);
@@ -1721,8 +1857,8 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           sh.Z[lane][2 * c + 1] = Z1;
           sh.Z[lane][cols + 2 * c] = V0;
           sh.Z[lane][cols + 2 * c + 1] = V1;
-          st_wt2(rr, oZ + 8 * (kZC * lane + 2 * c), Z0, Z1);
-          st_wt2(rr, oZ + 8 * (kZC * lane + cols + 2 * c), V0, V1);
+          st_wt2(rr, oZ + 8 * (kZJ * lane + 2 * c), Z0, Z1);
+          st_wt2(rr, oZ + 8 * (kZJ * lane + cols + 2 * c), V0, V1);
         }
       }
       lds_publish(&sh.zdone, c + 1);  // (wave 2 reads Z_c, Zv_c)
@@ -1773,7 +1909,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         dd[2] = d10;
         dd[3] = d11;
         if (joseph) {
-          const int kj = min(k, kMaxJoseph - 1);
+          const int kj = min(k, JM - 1);
           double v0[5], v1[5];
 #pragma unroll
           for (int a = 0; a < 5; ++a) {
@@ -1831,7 +1967,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           y0 = fma(-d01, yk1, fma(-d00, yk0, y0));
           y1 = fma(-d11, yk1, fma(-d10, yk0, y1));
           if (joseph) {
-            const int kj = min(k, kMaxJoseph - 1);
+            const int kj = min(k, JM - 1);
             const double zk0 = sh.Z[lj][2 * k], zk1 = sh.Z[lj][2 * k + 1];
             const double e00 = sh.Dv[kj][0], e01 = sh.Dv[kj][1], e10 = sh.Dv[kj][2], e11 = sh.Dv[kj][3];
             y0 = fma(-e01, zk1, fma(-e00, zk0, y0));
@@ -1866,7 +2002,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
       if (m > 0)
         v = rank2_sub(v, sh.KU[c][a][0], sh.KU[c][a][1], sh.MU[c][b][0], sh.MU[c][b][1]);
       if (m > 0 && joseph) {  // − V_c[a]·K_c[b]ᵀ
-        const int cj = min(c, kMaxJoseph - 1);
+        const int cj = min(c, JM - 1);
         v = rank2_sub(v, sh.VU[cj][a][0], sh.VU[cj][a][1], sh.KU[c][b][0], sh.KU[c][b][1]);
       }
       if (a < nu && b < nu) st_wt(&rec->Pend[a][b], v);
@@ -1925,9 +2061,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   if (kDiagBuild && (A.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
-template <typename T>
+template <typename T, bool J>
 __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int nf) {
-  __shared__ FactorShared sh;
+  __shared__ FactorSharedT<J> sh;
+  constexpr int ZC = FactorSharedT<J>::ZC;
   // xcd_b = 0: grid (blocks per filter, filters). xcd_b = B > 0 (swarms): the Σ pass's XCD-aware
   // 1-D grid — block L on XCD L % 8 takes filter 8·⌊(L/8)/B⌋ + L % 8, block (L/8) % B — so a
   // filter's record is fetched into one L2 instead of eight. Placement only changes speed.
@@ -1960,8 +2097,8 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
   __syncthreads();
   if ((kDiagBuild && (A.dbg & 16)) && bx == 0) {  // the record as this kernel read it
     unsigned long long s1 = 0;
-    for (int e = tid; e < kMaxU * kZC; e += 256)
-      s1 += dbits(sh.Z[e / kZC][e % kZC]) + dbits(sh.Y[e / kMaxU][e % kMaxU]);
+    for (int e = tid; e < kMaxU * ZC; e += 256) s1 += dbits(sh.Z[e / ZC][e % ZC]);
+    for (int e = tid; e < kMaxU * kZC; e += 256) s1 += dbits(sh.Y[e / kMaxU][e % kMaxU]);
     if (tid < kMaxU)
       s1 += static_cast<unsigned>(sh.u[tid]) + dbits(sh.alphaU[tid]) + dbits(sh.row0raw[tid]) +
             dbits(sh.col0raw[tid]) + dbits(sh.Zx[tid]) + dbits(sh.xU[tid]);
@@ -1970,7 +2107,7 @@ __global__ __launch_bounds__(256) void k_factors(PassArgs<T> A, int xcd_b, int n
     if (tid < static_cast<int>(sizeof(MsgDesc) / 8))
       dlog_add(A, 4, A.seq, f, 0, reinterpret_cast<const unsigned long long*>(&d)[tid]);
   }
-  factor_wave<T>(A, d, f, bx * (blockDim.x >> 6) + (tid >> 6), sh, tid & 63);
+  factor_wave<T, J>(A, d, f, bx * (blockDim.x >> 6) + (tid >> 6), sh, tid & 63);
   if (kDiagBuild && (A.dbg & 2)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 }
 
@@ -1995,11 +2132,12 @@ constexpr unsigned kOOB = 0x80000000u;  // voffset past any Σ panel descriptor 
 template <typename T>
 struct SigmaTile;
 
-// The factor rank is at most 2 + 2·kMaxChunk = 34 (a Joseph chunk: 2 + 4): 17 k-steps of the
-// 32×32×2 MFMA. (kw, the rank rounded up to 4 for the fp64 tiles, would make it 18, the last one
-// on the two zero rows 34–35.)
+// The simple form's factor rank is at most 2 + 2·kMaxChunk = 34: 17 k-steps of the 32×32×2 MFMA.
+// (kw, the rank rounded up to 4 for the fp64 tiles, would make it 18, the last one on the two zero
+// rows 34–35.) A Joseph chunk's rank 2 + 4m ≤ 66 (kw ≤ 68) takes a second block of 17 k-steps
+// (KB = 2): the operand registers are loaded again for it, so the tile keeps its register count.
 constexpr int kSteps = (2 + 2 * kMaxChunk + 1) / 2;
-static_assert(2 + 4 <= 2 * kSteps, "Joseph rank within the fp32 k-steps");
+static_assert(kMaxKW <= 4 * kSteps, "Joseph rank within two blocks of fp32 k-steps");
 struct F32TileRegs {  // one fp32 tile's loads
   float a[kSteps], b[kSteps], sv[16];
 };
@@ -2026,13 +2164,16 @@ struct SigmaTile<float> {
     __builtin_amdgcn_sched_barrier(0);
     load_sig(g, Sin, n, ld, R0, C0, lane);
   }
+  // block kb: factor rows 2·kSteps·kb + 2s + (lane ≥ 32)
   static __device__ __forceinline__ void load_ops(F32TileRegs& g, const float* kc, const float* mc,
-                                                  int n, int ldk, int R0, int C0, int lane) {
+                                                  int n, int ldk, int R0, int C0, int lane,
+                                                  int kb = 0) {
     const int kr = lane >> 5, kcol = lane & 31;
     const unsigned kbytes = static_cast<unsigned>(kMaxKW) * ldk * 4u;
     const auto rk = buf_rsrc(kc, kbytes), rm = buf_rsrc(mc, kbytes);
-    const unsigned ko = static_cast<unsigned>(kr * ldk + R0 + kcol) * 4u;
-    const unsigned mo = static_cast<unsigned>(kr * ldk + min(C0 + kcol, n - 1)) * 4u;
+    const int k0 = 2 * kSteps * kb;
+    const unsigned ko = static_cast<unsigned>((k0 + kr) * ldk + R0 + kcol) * 4u;
+    const unsigned mo = static_cast<unsigned>((k0 + kr) * ldk + min(C0 + kcol, n - 1)) * 4u;
     const unsigned kstep = 2u * ldk * 4u;
 #pragma unroll
     for (int s = 0; s < kSteps; ++s) {
@@ -2064,24 +2205,45 @@ struct SigmaTile<float> {
                                                 int kw, bool first, double qd, int R0, int C0,
                                                 int lane, const int* pm = nullptr,
                                                 const ChunkRec* rec = nullptr) {
+    f16v acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    mma(g, kw, 0, acc);
+    store(g, acc, Sout, n, ld, first, qd, R0, C0, lane, pm, rec);
+  }
+  // the k-steps of one operand block (k0: its first factor row): every MFMA issued, factor rows
+  // ≥ kw (stale) zeroed by a select — a branch per k-step let the compiler sink each operand load
+  // into its branch behind a vmcnt(0)
+  static __device__ __forceinline__ void mma(const F32TileRegs& g, int kw, int k0, f16v& acc) {
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      const bool live = k0 + 2 * s < kw;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(live ? g.a[s] : 0.0f, live ? g.b[s] : 0.0f, acc,
+                                                 0, 0, 0);
+    }
+  }
+  // Joseph: the two operand blocks (the first loaded before Σ_in, the second after its MFMAs)
+  static __device__ __forceinline__ void finish2(F32TileRegs& g, const float* kc, const float* mc,
+                                                 int ldk, float* Sout, int n, int ld, int kw,
+                                                 bool first, double qd, int R0, int C0, int lane,
+                                                 const int* pm, const ChunkRec* rec) {
+    f16v acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    mma(g, kw, 0, acc);
+    load_ops(g, kc, mc, n, ldk, R0, C0, lane, 1);
+    mma(g, kw, 2 * kSteps, acc);
+    store(g, acc, Sout, n, ld, first, qd, R0, C0, lane, pm, rec);
+  }
+  static __device__ __forceinline__ void store(const F32TileRegs& g, const f16v& acc, float* Sout,
+                                               int n, int ld, bool first, double qd, int R0,
+                                               int C0, int lane, const int* pm,
+                                               const ChunkRec* rec) {
     const int kr = lane >> 5, col = C0 + (lane & 31);
     const auto rout = panel(Sout, n, ld, R0);
     const unsigned so = soff(n, ld, C0, lane);
     const unsigned rstride = static_cast<unsigned>(ld) * 4u;
-    const float* a = g.a;
-    const float* b = g.b;
     const float* sv = g.sv;
-    f16v acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-    // every MFMA issued, factor rows ≥ kw (stale) zeroed by a select: a branch per k-step let
-    // the compiler sink each operand load into its branch behind a vmcnt(0)
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-      const bool live = 2 * s < kw;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(live ? a[s] : 0.0f, live ? b[s] : 0.0f, acc, 0,
-                                                 0, 0);
-    }
     SIG_STAMP(2);
     const float q = static_cast<float>(qd);
     if (!pm) {  // (two loops: the common one keeps the plain store sequence)
@@ -2135,6 +2297,9 @@ struct SigmaTile64 {
   static constexpr int kPol = TJ == 4 ? EKF_SIG_POL : 0;
   static constexpr int kRows = 32, kCols = 16 * TJ;
   static constexpr int kLds = kCols * kTS;  // doubles of the wave's transposed tile
+  // KB operand blocks of 36 factor rows (Joseph: 2, rank 2 + 4m ≤ 66; the second block's operands
+  // reuse the first's registers after its MFMAs)
+  template <int KB = 1>
   static __device__ __forceinline__ void run(const double* Sin, double* Sout, const double* kc,
                                              const double* mc, int n, int ld, int ldk, int kw,
                                              bool first, double q, int R0, int C0, int lane,
@@ -2161,13 +2326,16 @@ struct SigmaTile64 {
       so[tj] = col < n ? static_cast<unsigned>(kr * ld + col) * 8u : kOOB;
     }
     const unsigned kstep = 4u * ldk * 8u;
+    auto load_ops = [&](int kb) {
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      a[0][s] = ld_f64(rk, ko, s * kstep);
-      a[1][s] = ld_f64(rk, ko + 16 * 8, s * kstep);
+      for (int s = 0; s < 9; ++s) {
+        a[0][s] = ld_f64(rk, ko, (9 * kb + s) * kstep);
+        a[1][s] = ld_f64(rk, ko + 16 * 8, (9 * kb + s) * kstep);
 #pragma unroll
-      for (int tj = 0; tj < TJ; ++tj) b[tj][s] = ld_f64(rm, mo[tj], s * kstep);
-    }
+        for (int tj = 0; tj < TJ; ++tj) b[tj][s] = ld_f64(rm, mo[tj], (9 * kb + s) * kstep);
+      }
+    };
+    load_ops(0);
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -2181,14 +2349,21 @@ struct SigmaTile64 {
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) acc[ti][tj] = d4{0, 0, 0, 0};
+    auto mma = [&](int kb) {
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {  // unconditional, stale rows ≥ kw zeroed (see the fp32 tile)
-      const bool live = 4 * s < kw;
+      for (int s = 0; s < 9; ++s) {  // unconditional, stale rows ≥ kw zeroed (see the fp32 tile)
+        const bool live = 36 * kb + 4 * s < kw;
 #pragma unroll
-      for (int ti = 0; ti < 2; ++ti)
+        for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-        for (int tj = 0; tj < TJ; ++tj)
-          acc[ti][tj] = mfma_f64(live ? a[ti][s] : 0.0, live ? b[tj][s] : 0.0, acc[ti][tj]);
+          for (int tj = 0; tj < TJ; ++tj)
+            acc[ti][tj] = mfma_f64(live ? a[ti][s] : 0.0, live ? b[tj][s] : 0.0, acc[ti][tj]);
+      }
+    };
+    mma(0);
+    if (KB == 2) {
+      load_ops(1);
+      mma(1);
     }
     SIG_STAMP(2);
 #pragma unroll
@@ -2263,7 +2438,8 @@ __host__ __device__ inline int region_tiles(int trows, int tcols) {  // the larg
 // in VGPRs instead of AGPRs (no v_accvgpr_read before the Σ_in subtraction and the stores): swarm
 // message 0.719 → 0.703 ms, N = 1024 fp64 pass 16.4 → 15.9 µs, fp32 unchanged
 // (profiles/r3/p3r_vgpr_acc_ab.txt, two alternating runs each)
-template <typename T, bool WIDE>
+// KB: operand blocks of the rank (the Joseph form's instantiation: 2)
+template <typename T, bool WIDE, int KB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : (sizeof(T) == 8 ? 4 : 6)))) void k_sigma_pass(PassArgs<T> A, int tcols, int xcd_b, int nf) {
   using Tile = PassTile<T, WIDE>;
   SIG_STAMP(0);
@@ -2346,9 +2522,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         pm = map;
       }
-      Tile::finish(g, A.sig[d.parity ^ 1] + f * A.sig_stride, A.n, A.ld, kw,
-                   (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane, pm,
-                   rec);
+      if constexpr (KB == 1)
+        Tile::finish(g, A.sig[d.parity ^ 1] + f * A.sig_stride, A.n, A.ld, kw,
+                     (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane, pm,
+                     rec);
+      else
+        Tile::finish2(g, A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.ldk,
+                      A.sig[d.parity ^ 1] + f * A.sig_stride, A.n, A.ld, kw,
+                      (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane, pm,
+                      rec);
     }
   } else if ((d.flags & kActive) && ok) {
     SIG_STAMP(1);
@@ -2356,7 +2538,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WIDE ? 2 : 
     if ((kDiagBuild && (A.dbg & 8)) && t == 0 && lane == 0) dbg_seq_check(A, 2, f, A.seq + 1u);
     // this filter's rank (Joseph: K·M and V·Kᵀ per marker); rows beyond are stale
     const int kw = ((2 + ((d.flags & kJoseph) ? 4 : 2) * d.m + 3) / 4) * 4;
-    Tile::run(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
+    Tile::template run<KB>(A.sig[d.parity] + f * A.sig_stride, A.sig[d.parity ^ 1] + f * A.sig_stride,
               A.kcat + f * A.km_stride, A.mcat + f * A.km_stride, A.n, A.ld, A.ldk, kw,
               (d.flags & kFirst) != 0, A.q, tr * Tile::kRows, tc * Tile::kCols, lane,
               tT[threadIdx.x >> 6]);
@@ -2714,7 +2896,9 @@ void launch(K kernel, dim3 grid, dim3 block, hipStream_t s, hipEvent_t e0, hipEv
 template <typename T>
 hipError_t launch_chain(const PassArgs<T>& a, int nf, int nchunks, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1) {
-  launch(k_chain<T>, dim3(1, nf), dim3(kChainThreads), s, e0, e1, a, nchunks);
+  // (the Joseph form's instantiation: a handle's chunks are all of its form, ekf_set_joseph)
+  launch(a.joseph ? k_chain<T, true> : k_chain<T, false>, dim3(1, nf), dim3(kChainThreads), s, e0,
+         e1, a, nchunks);
   return hipGetLastError();
 }
 
@@ -2722,11 +2906,12 @@ template <typename T>
 hipError_t launch_factors(const PassArgs<T>& a, int nf, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1) {
   const int per_filter = (factor_waves(a) + 3) / 4;
+  // (the Joseph form's instantiation: Z's 4m columns; a handle's chunks are all of its form)
+  auto k = a.joseph ? k_factors<T, true> : k_factors<T, false>;
   if (nf >= 16) {  // XCD-aware 1-D grid, as the swarm's Σ pass
-    launch(k_factors<T>, dim3(8 * ((nf + 7) / 8) * per_filter), dim3(256), s, e0, e1, a,
-           per_filter, nf);
+    launch(k, dim3(8 * ((nf + 7) / 8) * per_filter), dim3(256), s, e0, e1, a, per_filter, nf);
   } else {
-    launch(k_factors<T>, dim3(per_filter, nf), dim3(256), s, e0, e1, a, 0, nf);
+    launch(k, dim3(per_filter, nf), dim3(256), s, e0, e1, a, 0, nf);
   }
   return hipGetLastError();
 }
@@ -2746,7 +2931,7 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool st
     const int tcols = (a.n + Tile::kCols - 1) / Tile::kCols;
     const int per_filter = (tiles(trows, tcols, Tile{}) + wpb - 1) / wpb;
     const dim3 grid(8 * ((nf + 7) / 8) * per_filter);
-    launch(k_sigma_pass<T, true>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, per_filter, nf);
+    launch(a.joseph ? k_sigma_pass<T, true, 2> : k_sigma_pass<T, true, 1>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, per_filter, nf);
   } else {
     using Tile = PassTile<T, false>;
     const int trows = (a.n + Tile::kRows - 1) / Tile::kRows;
@@ -2754,11 +2939,11 @@ hipError_t launch_sigma_pass(const PassArgs<T>& a, int nf, bool publish, bool st
     if (trows >= 2 * kRegRows && tcols >= 2 * kRegCols) {  // XCD regions (k_sigma_pass)
       const int per_x = sizeof(T) == 8 ? (tiles(trows, tcols, Tile{}) + 7) / 8 : region_tiles(trows, tcols);
       const dim3 grid(8 * ((per_x + wpb - 1) / wpb), nf);
-      launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, -1, nf);
+      launch(a.joseph ? k_sigma_pass<T, false, 2> : k_sigma_pass<T, false, 1>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, -1, nf);
     } else {
       const int per_filter = (tiles(trows, tcols, Tile{}) + wpb - 1) / wpb;
       const dim3 grid(per_filter, nf);
-      launch(k_sigma_pass<T, false>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
+      launch(a.joseph ? k_sigma_pass<T, false, 2> : k_sigma_pass<T, false, 1>, grid, dim3(64 * wpb), s, e0, e1, a, tcols, 0, nf);
     }
   }
   if (stage) hipLaunchKernelGGL(k_patch_stage<T>, dim3(nf), dim3(256), 0, s, a);

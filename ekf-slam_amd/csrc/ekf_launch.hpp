@@ -143,10 +143,9 @@ struct ReplayArgs {
   const double* odom;     // [T][F][3]
   const PlanState* st_in; // [F]
   PlanState* st_out;      // [F]
-  MsgDesc* desc;          // [T << jsh][F]
+  MsgDesc* desc;          // [T][F]
   int T, F, M, N;
-  int jsh;                // 1: Joseph form, each message planned as two chunks of ≤ kMaxJoseph
-                          // markers (desc [2T][F]); 0: one chunk of ≤ kMaxChunk (desc [T][F])
+  int joseph;             // 1: Joseph form (every chunk flagged kJoseph)
   int stage;              // staged rebuild operands (kStageOut / kStageIn)
   unsigned* plan_count;   // non-null: every wave adds 1 here once its descriptor is stored (the
                           // chain polls it instead of waiting for the planner's kernel boundary)

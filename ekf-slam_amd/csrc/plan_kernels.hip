@@ -8,9 +8,7 @@
 // after next), and the active messages before t (the parity).
 // A message with count 0 is no message (ekf_batch_sensor: the filter sits the step out); one
 // whose markers are all DELETE is a predict + posterior (slam.cpp:205), as on the host.
-// Joseph form (A.jsh = 1): every message is two chunks (t, h), h = 0 / 1, descriptor index 2t + h:
-// its non-DELETE markers [8h, 8h + 8), the predict on h = 0 and the posterior on h = 1; the scans
-// below then run over these 2T chunks (chunk 2t + h is active when message t is).
+// Joseph form (A.joseph = 1): the same chunks, flagged kJoseph (kMaxJoseph = kMaxChunk markers).
 #include <hip/hip_runtime.h>
 
 #include "ekf.h"
@@ -34,12 +32,10 @@ __device__ __forceinline__ int lo_bit(unsigned long long b) { return b ? __ffsll
 
 __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
   __shared__ PlanShared sh;
-  // t: the chunk (= the message unless Joseph), rt: its message, half: its marker window
-  const int t = blockIdx.x, f = blockIdx.y, lane = threadIdx.x, js = A.jsh;
-  const int F = A.F, M = A.M, T = A.T << js, rt = t >> js;
-  const int cap = js ? kMaxJoseph : kMaxChunk;  // markers per chunk
-  const size_t tf = static_cast<size_t>(t) * F + f, rtf = static_cast<size_t>(rt) * F + f;
-  auto cnt = [&](int tt) { return A.counts[static_cast<size_t>(tt >> js) * F + f]; };
+  const int t = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  const int F = A.F, M = A.M, T = A.T;
+  const size_t tf = static_cast<size_t>(t) * F + f;
+  auto cnt = [&](int tt) { return A.counts[static_cast<size_t>(tt) * F + f]; };
   const PlanState& s0 = A.st_in[f];
   // ---- round trip 1: the counts of messages t − 64 .. t + 63 (bit l of lo ↔ t − 64 + l, of hi ↔
   // t + l); the neighbours almost always lie in this window, the loops below are the fallback ----
@@ -83,32 +79,30 @@ __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     c4[k] = mi[k] >= 0 ? min(cnt(mi[k]), M) : 0;
-    const size_t o = (static_cast<size_t>(mi[k] >= 0 ? mi[k] >> js : 0) * F + f) * M + min(lane, M - 1);
+    const size_t o = (static_cast<size_t>(mi[k] >= 0 ? mi[k] : 0) * F + f) * M + min(lane, M - 1);
     id4[k] = M > 0 ? A.ids[o] : 0;
     del4[k] = A.actions && M > 0 && A.actions[o] == EKF_MARKER_DELETE;
   }
-  const size_t o0 = rtf * M + min(lane, M - 1);
+  const size_t o0 = tf * M + min(lane, M - 1);
   const double rx = M > 0 ? A.rel[2 * o0] : 0.0, ry = M > 0 ? A.rel[2 * o0 + 1] : 0.0;
-  const double od = lane < 3 ? A.odom[rtf * 3 + lane] : 0.0;
-  // the non-DELETE markers of each slot, compacted (slam.cpp:205's skip), from the slot's window
+  const double od = lane < 3 ? A.odom[tf * 3 + lane] : 0.0;
+  // the non-DELETE markers of each slot, compacted (slam.cpp:205's skip)
   int pos0 = 0;
   bool add0 = false;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int w0 = js && mi[k] >= 0 ? cap * (mi[k] & 1) : 0;
     const bool add = lane < c4[k] && !del4[k];
     const unsigned long long bal = __ballot(add);
-    // (__popcll is unsigned: signed counts before the window's offset comes off)
-    const int pos = static_cast<int>(__popcll(bal & ((1ull << lane) - 1ull))) - w0;
+    const int pos = static_cast<int>(__popcll(bal & ((1ull << lane) - 1ull)));
     if (lane < kMaxChunk) sh.ids[k][lane] = 0;
-    if (lane == 0) sh.m[k] = min(max(static_cast<int>(__popcll(bal)) - w0, 0), cap);
+    if (lane == 0) sh.m[k] = min(static_cast<int>(__popcll(bal)), kMaxChunk);
     if (k == 0) {
       pos0 = pos;
       add0 = add;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
-    if (add && pos >= 0 && pos < cap) sh.ids[k][pos] = id4[k];
+    if (add && pos < kMaxChunk) sh.ids[k][pos] = id4[k];
   }
   uint4* dz = reinterpret_cast<uint4*>(&sh.d);
   for (int e = lane; e < static_cast<int>(sizeof(MsgDesc) / 16); e += 64) dz[e] = uint4{0, 0, 0, 0};
@@ -132,7 +126,7 @@ __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
     const int m = sh.m[0];
     const int prev_m = prev >= 0 ? sh.m[1] : s0.prev_m;
     MsgDesc& d = sh.d;
-    if (add0 && pos0 >= 0 && pos0 < cap) {  // z: slam.cpp:208-210 (std::pow(x, 2) is x·x; sqrt rounds alike)
+    if (add0 && pos0 < kMaxChunk) {  // z: slam.cpp:208-210 (std::pow(x, 2) is x·x; sqrt rounds alike)
       d.z[pos0][0] = sqrt(rx * rx + ry * ry);
       d.z[pos0][1] = atan2(ry, rx);
     }
@@ -142,9 +136,7 @@ __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
     }
     if (lane < 3) d.odom[lane] = od;
     if (lane == 0) {
-      // (Joseph: the predict on the message's first chunk, the posterior on its second)
-      int flags = kActive | (js ? ((t & 1) ? kLast | kJoseph : kFirst | kJoseph) : kFirst | kLast) |
-                  (prev_m >= 0 ? kLook : 0);
+      int flags = kActive | kFirst | kLast | (A.joseph ? kJoseph : 0) | (prev_m >= 0 ? kLook : 0);
       // the chain two chunks on rebuilds from operands this chunk's Σ pass stages (plan_known:
       // both chunks in this plan); this chunk reads the ones staged two chunks back
       if (A.stage && prev_m >= 0 && prev2 >= 0) flags |= kStageIn;
@@ -177,7 +169,7 @@ __global__ __launch_bounds__(64) void k_plan_replay(ReplayArgs A) {
 
 hipError_t launch_plan_replay(const ReplayArgs& a, hipStream_t s) {
   if (a.T <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_plan_replay, dim3(a.T << a.jsh, a.F), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_plan_replay, dim3(a.T, a.F), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -300,12 +300,9 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
         return EKF_E_ARG;
     }
   if (int rc = handle_info(s->h, &s->info)) return rc;  // host-planned work first, bulk joined
-  // Joseph form on the HBM pipeline takes ≤ kMaxJoseph markers per chunk: the parallel form's
-  // ekf_replay_device plans two chunks per message; the sequential form writes one chunk per
-  // message, so it refuses the form rather than run the simple one silently (the resident path
-  // carries the form in its own kernel)
+  // (Joseph form on the HBM pipeline: both forms write kJoseph chunks of ≤ kMaxJoseph = kMaxChunk
+  // markers; the resident path carries the form in its own kernel)
   const bool par = parallel_ok(s, T, sense);
-  if (s->info.joseph && !s->info.resident && !par) return EKF_E_ARG;
   hipSetDevice(s->info.device);
   if (int rc = reserve(s, T)) return rc;
   if (par) return run_parallel(s, T, wheel_cmd, sense);
@@ -361,6 +358,7 @@ int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense) {
   a.range = s->cfg.max_range;
   a.radius = s->cfg.wheel_radius;
   a.track = s->cfg.track_width;
+  a.joseph = s->info.joseph && !s->info.resident;
   if (launch_sim(a, st) != hipSuccess) return EKF_E_HIP;
   // each filter's final parity (its inactive messages do not flip it) and odometry: the host mirror
   if (hipMemcpyAsync(s->host_par_pinned, s->par, F * sizeof(int), hipMemcpyDeviceToHost, st) !=

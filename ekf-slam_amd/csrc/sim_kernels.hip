@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs A) {
     }
     if (lane == 0) {
       d->m = m;
-      d->flags = kActive | kFirst | kLast | (prev_m >= 0 ? kLook : 0);
+      d->flags = kActive | kFirst | kLast | (prev_m >= 0 ? kLook : 0) | (A.joseph ? kJoseph : 0);
       d->parity = par;
       d->odom[0] = oth;
       d->odom[1] = ox;

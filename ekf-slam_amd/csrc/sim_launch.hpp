@@ -31,6 +31,7 @@ struct SimArgs {
   unsigned long long seed;
   long long tick0, msg0;   // global tick / message index of this run's first
   int f0, F, L, T, tpm, m, M, N;
+  int joseph;              // the descriptors carry kJoseph (ekf_set_joseph on the HBM pipeline)
   double slip, sigma, range, radius, track;
   double start[3];
 };

@@ -170,10 +170,10 @@ int ekf_posterior(ekf_t h, int filter);
 /* Joseph-form covariance update, opt-in (off by default, like the reference, which applies
  * Σ ← (I − KH)Σ at slam.cpp:264-265): Σ ← (I − KH)Σ(I − KH)ᵀ + KRKᵀ for every later correction.
  * Equal in exact arithmetic with the optimal gain; it differs only in rounding. Resident path: its
- * own kernel instantiation. HBM pipeline (fp32 and fp64): chunks of <= 8 markers, each folded into
- * one Σ pass of rank 2 + 4m (K_c·M_c and (Σ_cHᵀ − K_c·S_c)·K_cᵀ per correction), so two Σ passes
- * per 16-marker message instead of one; ekf_replay_device and the simulator's parallel form plan
- * two chunks per message on the GPU. */
+ * own kernel instantiation. HBM pipeline (fp32 and fp64): the same chunks of <= 16 markers, each
+ * folded into one Σ pass of rank 2 + 4m (K_c·M_c and (Σ_cHᵀ − K_c·S_c)·K_cᵀ per correction), so one
+ * Σ pass per message as in the simple form. A switch makes each filter's next chunk gather its rows
+ * from Σ (the chunk before cannot be rebuilt across forms). */
 int ekf_set_joseph(ekf_t h, int on);
 
 /* Deferred submission. While on, the callbacks above only plan their work on the host; the plan

@@ -70,9 +70,7 @@ int ekf_sim_destroy(ekf_sim_t s);
  * call waits only for the device planning). A filter with no marker in a message gets no message
  * (as ekf_replay with counts 0). Afterwards the handle's t_odom_robot is the run's last odometry
  * pose, as if ekf_set_odom had been called with it (the next host-planned call predicts from it).
- * EKF_E_ARG when ekf_set_joseph is on and the handle runs the HBM pipeline (fp32, or n > 128): the
- * device planner writes one multi-marker chunk per message, the Joseph form there needs one marker
- * per chunk (the resident path honours it). */
+ * With ekf_set_joseph on, the chunks are Joseph-form ones. */
 int ekf_sim_run(ekf_sim_t s, int T, const double* wheel_cmd, const int* sense);
 
 /* With cfg.record: the last run's inputs as ekf_replay would take them — counts[T][F],

@@ -245,17 +245,17 @@ def test_device_replay_rejects():
                                    (2, {"EKF_SERIAL": "1"})],
                          ids=["1filter", "4filters", "3filters_events", "2filters_serial"])
 def test_device_replay_joseph_equals_host(monkeypatch, F, env):
-    """Joseph form (ekf_set_joseph) through the device planner: every message becomes two chunks of
-    ≤ 8 markers (plan_kernels.hip, the second one empty for a short message), the host plans chunks
-    of ≤ 8 (plan_known). fp64 N = 96, up to 12 markers per message, holes (empty and all-DELETE
-    messages): the two end alike, and filter 0 equals the C oracle's Joseph mode."""
+    """Joseph form (ekf_set_joseph) through the device planner: one kJoseph chunk per message
+    (plan_kernels.hip), as the host plans it (plan_known, kMaxJoseph = kMaxChunk). fp64 N = 96, up
+    to 12 markers per message, holes (empty and all-DELETE messages): the two end alike, and filter
+    0 equals the C oracle's Joseph mode."""
     for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     pyekf.poison_lds()
     scs = []
-    for k in range(3):  # messages of 12, 5, 8, 9 and 1 markers: one or two chunks of ≤ 8
+    for k in range(3):  # messages of 12, 5, 8, 9 and 1 markers
         s0 = synth.synthetic(96, 30, seed=7 + k, max_markers=12)
         cnt = np.minimum(s0.count, np.roll([12, 5, 8, 9, 1], k)[np.arange(30) % 5]).astype(s0.count.dtype)
         scs.append(synth.Scenario(s0.n_landmarks, s0.landmarks, s0.wheel, s0.ids, s0.actions,
@@ -274,8 +274,8 @@ def test_device_replay_joseph_equals_host(monkeypatch, F, env):
 @pytest.mark.parametrize("dtype", [pyekf.EKF_F32, pyekf.EKF_F64], ids=["f32", "f64"])
 def test_device_replay_joseph_n1024(dtype):
     """The Joseph form at the headline shape (bench.py --workload n1024_fp32_joseph): N = 1024 from
-    an fp64 survey, 12 messages of 16 markers through the device planner — two chunks of 8 per
-    message, each chunk's V_c·K_cᵀ terms folded into its one Σ pass — against the fp64 oracle's
+    an fp64 survey, 12 messages of 16 markers through the device planner — one chunk per message,
+    its V_c·K_cᵀ terms folded into its one rank-66 Σ pass — against the fp64 oracle's
     Joseph mode from the same state, at the fp32 tolerances of tests/test_gpu_scale.py (pose 1e-6,
     state 1e-5, Σ 5e-5) or the fp64 populated-map ones (state 5e-8, Σ 1e-7)."""
     N, warm, T = 1024, 40, 12

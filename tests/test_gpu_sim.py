@@ -244,13 +244,14 @@ def test_sim_parallel_form_sense_all_on_the_pipeline(monkeypatch):
     e.close()
 
 
-def test_sim_joseph_on_the_pipeline(monkeypatch):
-    """ekf_set_joseph on an HBM-pipeline handle: the parallel form (ekf_replay_device's planner, two
-    chunks of ≤ 8 markers per message) runs the Joseph form — basic_world forced onto the pipeline
-    over two runs, against the oracle's Joseph mode fed the device's markers (1e-8). The sequential
-    form writes one chunk per message, so it returns EKF_E_ARG instead of running the simple form."""
+@pytest.mark.parametrize("parallel", ["1", "0"], ids=["parallel", "sequential"])
+def test_sim_joseph_on_the_pipeline(monkeypatch, parallel):
+    """ekf_set_joseph on an HBM-pipeline handle: both forms write kJoseph chunks, one per message
+    (the parallel form through ekf_replay_device's planner, the sequential one from k_sim) —
+    basic_world forced onto the pipeline over two runs, against the oracle's Joseph mode fed the
+    device's markers (1e-8)."""
     monkeypatch.setenv("EKF_RESIDENT", "0")
-    monkeypatch.delenv("EKF_SIM_PARALLEL", raising=False)
+    monkeypatch.setenv("EKF_SIM_PARALLEL", parallel)
     F, T1, T2 = 4, 12, 10
     drive = synth.circle_drive(T1 + T2 + 1, 0.3, sense=synth.SENSE_ALL)
     seeds = np.uint64(5151) + np.arange(F, dtype=np.uint64)
@@ -267,11 +268,5 @@ def test_sim_joseph_on_the_pipeline(monkeypatch):
         xr, Sr, _, _ = _oracle(50, cnt, ids, act, rel, odom, f, joseph=True)
         assert np.abs(x - xr).max() < POSE_TOL, f
         assert np.abs(S - Sr).max() < POSE_TOL, f
-    monkeypatch.setenv("EKF_SIM_PARALLEL", "0")
-    tpm = sw.wheel.shape[1]
-    T = T1 + T2
-    with pytest.raises(pyekf.EkfError) as ei:
-        sim.run(sw.cmd[T * tpm:(T + 1) * tpm], sw.sense[T:T + 1])
-    assert ei.value.rc == pyekf.EKF_E_ARG
     sim.close()
     e.close()

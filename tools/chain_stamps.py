@@ -46,6 +46,8 @@ if DT == "f32":
     e.set_state(x, S, tmo=tmo, counter=cnt)
 else:
     e = e64
+if os.environ.get("EKF_STAMP_JOSEPH") == "1":  # the Joseph-form chain (ekf_set_joseph)
+    assert e.set_joseph(True) == 0
 replay(e, slice(w, w + T))
 e.sync()
 print("status", e.status())
