@@ -890,10 +890,20 @@ __device__ __forceinline__ void factor_wave(const PassArgs<T>& A, const MsgDesc&
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = 16 * g + ks + 4 * r;
-          kc[(2 + c) * ldk + i] = static_cast<T>(acc[g][r]);
-          // Joseph: K at this index is also the column factor of the (ΣHᵀ − K·S)·Kᵀ term
-          // (Z columns 0 .. 2m − 1 ≤ 31: the first two groups hold every K_c)
-          if (J && g < 2 && joseph && c < jk0) mc[(2 + jk0 + c) * ldk + i] = static_cast<T>(acc[g][r]);
+          // Joseph: Z columns 0 .. 2m − 1 (the first two groups) are K, which is also the column
+          // factor of the (ΣHᵀ − K·S)·Kᵀ term (Mcat rows 2 + 2m + c); columns 32 + c are V, Kcat
+          // rows 2 + 2m + c — the rank-(2 + 4m) factors packed, zero columns not stored
+          if (!joseph) {
+            if (g < 2) kc[(2 + c) * ldk + i] = static_cast<T>(acc[g][r]);
+          } else if (g < 2) {
+            if (c < jk0) {
+              kc[(2 + c) * ldk + i] = static_cast<T>(acc[g][r]);
+              mc[(2 + jk0 + c) * ldk + i] = static_cast<T>(acc[g][r]);
+            }
+          } else if (c - kZC < jk0 + 2) {  // (+ the two zero rows up to kw = 4m + 4: the
+            // pass reads them, and a longer chunk before may have left V rows there)
+            kc[(2 + jk0 + c - kZC) * ldk + i] = static_cast<T>(acc[g][r]);
+          }
         }
     }
     if (merged) columns(i, raw, r0t);
@@ -1411,46 +1421,49 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     EKF_STAMP(7);
     __syncthreads();
     EKF_STAMP(5);
-    // P = D − K'·M'full with M'full = [M' (2m' rows); K'[:, 0..2m')ᵀ (a Joseph chunk before: its
-    // V'·K'ᵀ terms, V' = K' columns 2m'..4m')], k < 4m' ≤ 64: 16 k-steps of the 32 × 32 core, one
-    // 16 × 16 tile per wave, and the 3-wide bands (201 entries) as VALU dot products. The k order is
-    // the round-5 form's (M' rows, then K'ᵀ, then zeros), so up to 8 markers the same sums.
-    {
+    // P = D − K'·M'full with M'full = [M' (rows 0..31); K'[:, 0..32)ᵀ (rows 32..63: a Joseph chunk
+    // before, its V'·K'ᵀ terms, V' = K' columns 32..63)] — zero beyond each part's rank 2m', and
+    // the K'ᵀ part zero after a simple-form chunk (its record's columns ≥ 32 are not V'). The
+    // 48 × 48 padded block as 9 tiles on f64 MFMA, k < 64 in 16 k-steps: waves 0–2 one row tile
+    // each (its K' rows read once) × the three column tiles, interleaved. Rows / columns ≥ kMaxU
+    // are clamped on read and never stored; a wave reads and writes only its own rows.
+    if (wv < 3) {
       const bool pj = sh.pv.joseph != 0;
-      const int pm2 = 2 * sh.pv.m, pk2 = pj ? 4 * sh.pv.m : 2 * sh.pv.m;
-      auto mfull = [&](int k, int c) {  // M'full[k][c], c < kMaxU (every operand read clamped)
-        const double vm = sh.pv.M[min(k, kZC - 1)][c];
-        const double vk = sh.pv.K[c][max(min(k - pm2, ZC - 1), 0)];
-        return k < pm2 ? vm : (k < pk2 ? vk : 0.0);
-      };
-      const int ti = wv >> 1, tj = wv & 1;
-      const int col = 16 * tj + i16, ar = 16 * ti + i16;
-      double av[16], bv[16];
+      const int ar = min(16 * wv + i16, kMaxU - 1);
+      double av[16];
 #pragma unroll
-      for (int s0 = 0; s0 < 16; ++s0) {
-        av[s0] = -sh.pv.K[ar][4 * s0 + k4];
-        bv[s0] = mfull(4 * s0 + k4, col);
+      for (int s0 = 0; s0 < 16; ++s0) av[s0] = -sh.pv.K[ar][4 * s0 + k4];
+      d4 acc[3];
+#pragma unroll
+      for (int tj = 0; tj < 3; ++tj) {
+        const int bc = min(16 * tj + i16, kMaxU - 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[tj][r] = P[min(16 * wv + k4 + 4 * r, kMaxU - 1)][bc];
       }
-      d4 acc;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = P[16 * ti + k4 + 4 * r][col];
-      // band entry: t < 105 → rows 32..34 × columns 0..34, then rows 0..31 × columns 32..34
-      const int t = tid < 201 ? tid : 200;
-      const int brow = t < 105 ? 32 + t / 35 : (t - 105) / 3;
-      const int bcol = t < 105 ? t - 35 * (t / 35) : 32 + (t - 105) - 3 * ((t - 105) / 3);
-      const int br = min(brow, kMaxU - 1), bc = min(bcol, kMaxU - 1);
-      double bs[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-      for (int k = 0; k < ZC; ++k) bs[k & 3] = fma(sh.pv.K[br][k], mfull(k, bc), bs[k & 3]);
-      const double bv0 = P[br][bc];
+      for (int h = 0; h < 2; ++h) {  // k < 32 (M' rows), then k ≥ 32 (K'ᵀ)
+        double bv[3][8];
 #pragma unroll
-      for (int s0 = 0; s0 < 16; ++s0) acc = mfma_f64(av[s0], bv[s0], acc);
+        for (int tj = 0; tj < 3; ++tj) {
+          const int bc = min(16 * tj + i16, kMaxU - 1);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * ti + k4 + 4 * r;
-        if (row < nu && col < nu) P[row][col] = acc[r];
+          for (int s0 = 0; s0 < 8; ++s0)
+            bv[tj][s0] = h == 0 ? sh.pv.M[4 * s0 + k4][bc] : (pj ? sh.pv.K[bc][4 * s0 + k4] : 0.0);
+        }
+#pragma unroll
+        for (int s0 = 0; s0 < 8; ++s0)
+#pragma unroll
+          for (int tj = 0; tj < 3; ++tj) acc[tj] = mfma_f64(av[8 * h + s0], bv[tj][s0], acc[tj]);
       }
-      if (tid < 201 && brow < nu && bcol < nu) P[brow][bcol] = bv0 - ((bs[0] + bs[1]) + (bs[2] + bs[3]));
+#pragma unroll
+      for (int tj = 0; tj < 3; ++tj) {
+        const int col = 16 * tj + i16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * wv + k4 + 4 * r;
+          if (row < nu && col < nu) P[row][col] = acc[tj][r];
+        }
+      }
     }
     }
     EKF_STAMPT(10, 64);
@@ -1675,11 +1688,11 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         __builtin_amdgcn_make_buffer_rsrc(rec, 0, static_cast<int>(sizeof(ChunkRec)), 0x00020000);
     constexpr int oZ = static_cast<int>(offsetof(ChunkRec, Z));
     {  // columns ≥ 2m of the record's Z are zero (the factor kernel and a rebuilding chain read
-       // them); Joseph keeps columns 2m..4m for V
-      const int z0c = joseph ? 4 * m : 2 * m;
-      const int zw = ZC - z0c;
-      for (int e = lane; e < kMaxU * zw; e += 64) {
-        const int b = e / zw, k = z0c + (e - b * zw);
+       // them); Joseph: columns 2m..32 and 32 + 2m..64 (V in 32..32 + 2m)
+      const int zw = kZC - 2 * m, nz = J ? 2 : 1;
+      for (int e = lane; e < kMaxU * zw * nz; e += 64) {
+        const int h = e >= kMaxU * zw ? 1 : 0, e2 = e - h * kMaxU * zw;
+        const int b = e2 / zw, k = 2 * m + (e2 - b * zw) + kZC * h;
         st_wt(&rec->Z[b][k], 0.0);
       }
     }
@@ -1776,9 +1789,10 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // W_c = Φ_c[:, pA]·Hᵀ = E_c·Hᵀ − Σ_{k<c} (Z_k·C_k + Zv_k·C'_k), C_k = M_k[:, pA_c]·Hᵀ and
     // C'_k = K_k[pA_c]ᵀ·Hᵀ (2×2 each); then Z_c = W_c·S_c⁻¹ (K_c = G_c·S⁻¹, G_c[i] = r_0(i)·W_c) and
     // Zv_c = W_c − Z_c·S_c (V_c = G_c − K_c·S_c). One marker: Z_0 = E·Hᵀ·S⁻¹, as the simple form.
-    const int cols = 2 * min(m, kMaxJoseph);
+    constexpr int cols = kZC;  // V_c in columns 32 + 2c.. (fixed: the rebuild's K'ᵀ rows start at 32)
     for (int c = 0; c < m && c < kMaxJoseph; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
+      EKF_STAMPT(460 + c, 64);
       const int pj = 3 + 2 * c;
       double H0[5], H1[5], Si[4], Sc[4];
 #pragma unroll
@@ -1827,6 +1841,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         ed[3] = e11;
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: LDS keeps its order)
+      EKF_STAMPT(480 + c, 64);
       {  // row li of W_c, then of Z_c and Zv_c
         const int pos = li < 3 ? li : (li == pj ? 3 : (li == pj + 1 ? 4 : -1));
         double w0 = 0.0, w1 = 0.0;
@@ -1835,16 +1850,45 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           w0 = pos == a ? H0[a] : w0;
           w1 = pos == a ? H1[a] : w1;
         }
-#pragma unroll 4
-        for (int k = 0; k < c; ++k) {
-          const double zk0 = sh.Z[li][2 * k], zk1 = sh.Z[li][2 * k + 1];
-          const double vk0 = sh.Z[li][cols + 2 * k], vk1 = sh.Z[li][cols + 2 * k + 1];
-          const double c00 = sh.Cz[k][0], c01 = sh.Cz[k][1], c10 = sh.Cz[k][2], c11 = sh.Cz[k][3];
-          const double e00 = sh.Cv[k][0], e01 = sh.Cv[k][1], e10 = sh.Cv[k][2], e11 = sh.Cv[k][3];
-          w0 = fma(-zk1, c10, fma(-zk0, c00, w0));
-          w1 = fma(-zk1, c11, fma(-zk0, c01, w1));
-          w0 = fma(-vk1, e10, fma(-vk0, e00, w0));
-          w1 = fma(-vk1, e11, fma(-vk0, e01, w1));
+        // the history in groups of 4 terms, each group's 24 LDS reads issued together (one
+        // read-wait round trip per term made this wave the chunk's last, ≈ 200 cycles a term)
+        auto jterm = [&](const double* zz, const double* cz) {
+          w0 = fma(-zz[1], cz[2], fma(-zz[0], cz[0], w0));
+          w1 = fma(-zz[1], cz[3], fma(-zz[0], cz[1], w1));
+          w0 = fma(-zz[3], cz[6], fma(-zz[2], cz[4], w0));
+          w1 = fma(-zz[3], cz[7], fma(-zz[2], cz[5], w1));
+        };
+        int k = 0;
+        for (; k + 4 <= c; k += 4) {
+          double zz[4][4], cz[4][8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            zz[q][0] = sh.Z[li][2 * (k + q)];
+            zz[q][1] = sh.Z[li][2 * (k + q) + 1];
+            zz[q][2] = sh.Z[li][cols + 2 * (k + q)];
+            zz[q][3] = sh.Z[li][cols + 2 * (k + q) + 1];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              cz[q][e] = sh.Cz[k + q][e];
+              cz[q][4 + e] = sh.Cv[k + q][e];
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) jterm(zz[q], cz[q]);
+        }
+        for (; k < c; ++k) {
+          double zz[4], cz[8];
+          zz[0] = sh.Z[li][2 * k];
+          zz[1] = sh.Z[li][2 * k + 1];
+          zz[2] = sh.Z[li][cols + 2 * k];
+          zz[3] = sh.Z[li][cols + 2 * k + 1];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            cz[e] = sh.Cz[k][e];
+            cz[4 + e] = sh.Cv[k][e];
+          }
+          jterm(zz, cz);
         }
         const bool in = lane < nu;
         const double Z0 = in ? w0 * Si[0] + w1 * Si[2] : 0.0;
@@ -1878,7 +1922,9 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
     // D'_k = H·V_k[pA_c], with wave 1's Z_k (flag zdone)
     for (int c = 0; c < m; ++c) {
       lds_wait_ge(&sh.pub, c + 1);
+      EKF_STAMPT(400 + c, 128);
       if (joseph && c > 0) lds_wait_ge(&sh.zdone, min(c, kMaxJoseph));
+      EKF_STAMPT(420 + c, 128);
       const int pj = 3 + 2 * c;
       double H0[5], H1[5];
 #pragma unroll
@@ -1933,6 +1979,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
         }
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      EKF_STAMPT(440 + c, 128);
       {  // column lj of Y_c
         const int pos = lj < 3 ? lj : (lj == pj ? 3 : (lj == pj + 1 ? 4 : -1));
         double y0 = 0.0, y1 = 0.0;
@@ -1942,7 +1989,32 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
           y1 = pos == a ? H1[a] : y1;
         }
         int k0 = 0;
-        if (!joseph) {  // (uniform) groups of 4 terms, reads issued together (as wave 1's Z)
+        if (joseph) {  // (uniform) groups of 4 terms with D'_k·Z_kᵀ, reads issued together
+          for (; k0 + 4 <= c; k0 += 4) {
+            double yy[4][4], dy[4][8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int kj = min(k0 + q, JM - 1);
+              yy[q][0] = sh.Y[2 * (k0 + q)][lj];
+              yy[q][1] = sh.Y[2 * (k0 + q) + 1][lj];
+              yy[q][2] = sh.Z[lj][2 * (k0 + q)];
+              yy[q][3] = sh.Z[lj][2 * (k0 + q) + 1];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                dy[q][e] = sh.Dy[k0 + q][e];
+                dy[q][4 + e] = sh.Dv[kj][e];
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              y0 = fma(-dy[q][1], yy[q][1], fma(-dy[q][0], yy[q][0], y0));
+              y1 = fma(-dy[q][3], yy[q][1], fma(-dy[q][2], yy[q][0], y1));
+              y0 = fma(-dy[q][5], yy[q][3], fma(-dy[q][4], yy[q][2], y0));
+              y1 = fma(-dy[q][7], yy[q][3], fma(-dy[q][6], yy[q][2], y1));
+            }
+          }
+        } else {  // (uniform) groups of 4 terms, reads issued together (as wave 1's Z)
           for (; k0 + 4 <= c; k0 += 4) {
             double yy[4][2], dy[4][4];
 #pragma unroll

@@ -84,3 +84,6 @@ for c in (0, 1, m // 2, m - 2):
     print(f"   wave3: pub seen at {s[192 + 2 * c] - s[b]}, pdone at {s[193 + 2 * c] - s[b]} "
           f"(wave0 publish at {s[b + 4] - s[b]}, next-step pdone wait at {s[b + 8 + 2] - s[b]})")
     print(f"   wave1 Z_c done at {s[320 + c] - s[b]}, wave2 Y_c done at {s[360 + c] - s[b]} (from wave 0's step start)")
+    if os.environ.get("EKF_STAMP_JOSEPH") == "1":
+        print(f"   wave1 pub seen {s[460 + c] - s[b]}, C done {s[480 + c] - s[b]}; wave2 pub seen "
+              f"{s[400 + c] - s[b]}, zdone seen {s[420 + c] - s[b]}, D done {s[440 + c] - s[b]}")
