@@ -60,13 +60,16 @@ WORKLOADS = {
     # 16-marker message, one Σ pass of rank 2 + 4m
     "n1024_fp32_joseph": (1024, "f32", 1, 16, "configs[2] with the Joseph-form Sigma update "
                                                "(north_star): N=1024, 1 filter, fp32"),
+    "n1024_fp32_assoc_joseph": (1024, "f32", 1, 16, "configs[2] with unknown association "
+                                                     "(sensor_cb) in the Joseph form: N=1024 "
+                                                     "slots, 960 mapped landmarks, fp32"),
 }
 JOSEPH_CHUNK = 16  # markers per Joseph-form chunk (kMaxJoseph, ekf_device.hpp)
 ASSOC_FREE_SLOTS = 64  # association workloads map N − 64 landmarks (room for new ones)
 
 
 def is_assoc(workload):
-    return workload.endswith("_assoc")
+    return workload.endswith("_assoc") or workload.endswith("_assoc_joseph")
 
 
 def is_joseph(workload):

@@ -72,7 +72,9 @@ struct ekf_ctx {
                                  // launch: the next flush joins the bulk stream on the host)
   AmArgs am{};                   // k_assoc_msg scratch (allocated at the first association chunk)
   int am_route = 0;              // unknown association: EKF_ASSOC_* (fixed at ekf_create)
+  int am_route_j = 0;            // ... for the Joseph-form kernel (its larger LDS may fit fewer)
   int am_group = 1;              // filters per k_assoc_msg launch (co-resident, assoc_msg_group)
+  int am_group_j = 1;            // ... Joseph form
   int bulk_cus_per_xcd = 0;      // CUs the bulk stream may use on each XCD
   int main_cus_per_xcd = 0;      // CUs the main stream may use on each XCD (0: every CU, no mask)
   unsigned* fatal_h = nullptr;   // host-mapped: a device poll timed out (EKF_E_TIMEOUT)
@@ -531,10 +533,11 @@ void plan_assoc(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0
 int assoc_cus_per_xcd(const ekf_ctx* h) {
   return h->serial && h->main_cus_per_xcd > 0 ? h->main_cus_per_xcd : h->bulk_cus_per_xcd;
 }
-int am_route(ekf_ctx* h) {
+int am_route(ekf_ctx* h, bool joseph = false) {
   if (h->resident || !h->assoc_msg) return EKF_ASSOC_MARKER;
   const int G = (h->cfg.n_landmarks + kAmSlots - 1) / kAmSlots;
-  const int per_xcd = assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32) * assoc_cus_per_xcd(h);
+  const int per_xcd =
+      assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32, joseph) * assoc_cus_per_xcd(h);
   const char* e = std::getenv("EKF_AM_XCD");  // EKF_AM_XCD=0: the agent placement only
   if (G > 1 && G <= per_xcd && !(e && std::atoi(e) == 0)) return EKF_ASSOC_CHUNK_XCD;
   if ((G + 7) / 8 <= per_xcd) return EKF_ASSOC_CHUNK;
@@ -571,8 +574,12 @@ int ensure_am(ekf_ctx* h) {
     return EKF_E_HIP;
   }
   h->am = b;
-  const int slots_x = assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32) * assoc_cus_per_xcd(h);
-  h->am_group = b.xcd ? 8 * std::max(1, slots_x / G) : std::max(1, 8 * slots_x / G);
+  for (int jv = 0; jv < 2; ++jv) {
+    const int slots_x =
+        assoc_msg_blocks_per_cu(h->cfg.dtype == EKF_F32, jv != 0) * assoc_cus_per_xcd(h);
+    (jv ? h->am_group_j : h->am_group) =
+        b.xcd ? 8 * std::max(1, slots_x / G) : std::max(1, 8 * slots_x / G);
+  }
   return EKF_OK;
 }
 
@@ -601,7 +608,7 @@ void plan_assoc_msg(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, in
       }
       const int b = i0 + chunk * kMaxChunk;
       const int m = std::max(0, std::min(kMaxChunk, mf - b));
-      int flags = kActive | kNoInit;
+      int flags = kActive | kNoInit | (h->joseph ? kJoseph : 0);
       h->prev_m[f] = -1;  // association chunks run unpipelined
       forget_desc(h, f);
       if (b == 0 && (predict || h->pending[f])) flags |= kFirst;
@@ -620,12 +627,13 @@ void plan_assoc_msg(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, in
   }
 }
 
-// Route unknown association: whole chunks through k_assoc_msg on the HBM pipeline (simple form);
-// the resident path, the Joseph form, EKF_ASSOC_MSG=0 and maps too large for the bulk stream's
-// CUs to hold a filter's workgroups at once (am_route) take one marker per launch.
+// Route unknown association: whole chunks through k_assoc_msg on the HBM pipeline (either form:
+// k_assoc_msg<T, J>); the resident path, EKF_ASSOC_MSG=0 and maps too large for the bulk stream's
+// CUs to hold a filter's workgroups at once (am_route; the Joseph kernel's own occupancy, in the
+// placement fixed at creation) take one marker per launch.
 void plan_unknown(ekf_ctx* h, int f0, int nf, bool predict, bool posterior, int i0, int i1,
                   const char* absent = nullptr) {
-  if (!h->joseph && h->am_route != EKF_ASSOC_MARKER)
+  if (h->am_route != EKF_ASSOC_MARKER && (!h->joseph || h->am_route_j == h->am_route))
     plan_assoc_msg(h, f0, nf, predict, posterior, i0, i1, absent);
   else
     plan_assoc(h, f0, nf, predict, posterior, i0, i1, absent);
@@ -649,7 +657,7 @@ int assoc_msg_group(ekf_ctx* h, const MsgDesc* dptr, int f0, int nf, bool publis
   // placement ⌊slots per XCD / G⌋ filters on each of the 8 XCDs (filter k of a launch on XCD
   // k mod 8), agent placement ⌊slots / G⌋ filters spread over all of them. Filters are
   // independent, so any grouping gives the same bits.
-  const int group_nf = h->am_group;
+  const int group_nf = h->joseph ? h->am_group_j : h->am_group;
   auto run = [&](auto tag) -> int {
     using T = decltype(tag);
     PassArgs<T> a = args<T>(h, dptr, f0);
@@ -1105,6 +1113,7 @@ int ekf_create(ekf_t* out, const ekf_config* cfg_in) {
     if (!e && !h->devsync && h->F > kCuSplitMaxFilters) h->serial = true;
   }
   h->am_route = am_route(h);
+  h->am_route_j = am_route(h, true);
   if (hipHostMalloc(reinterpret_cast<void**>(&h->fatal_h), 64,
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
     return fail(EKF_E_NOMEM);
@@ -1522,7 +1531,8 @@ int ekf_get_schedule(ekf_t h, int* flags) {
 
 int ekf_get_assoc_route(ekf_t h, int* route) {
   if (!h || !route) return EKF_E_ARG;
-  *route = h->am_route;
+  // (the route in effect: the Joseph form keeps the chunk route only where its kernel fits alike)
+  *route = h->joseph && h->am_route_j != h->am_route ? EKF_ASSOC_MARKER : h->am_route;
   return EKF_OK;
 }
 

@@ -70,11 +70,17 @@ namespace {
 // not need them.
 constexpr int kAmThreads = 3 * kAmSlots;
 
-struct AmShared {
-  alignas(16) double hkm[kMaxChunk][kAmSlots][8];  // wave 0's K_c[k] (0..3) and M_c[:, k] (4..7), by lane:
-                                       // a lane's step in 64 contiguous bytes (ds_read_b128 × 4)
+// J: the Joseph form (ekf_set_joseph; every descriptor kJoseph). Each step then also subtracts
+// V_c·K_cᵀ, V_c = Σ_c·Hᵀ − K_c·S_c (slam.cpp:264-265's update as (I − KH)Σ(I − KH)ᵀ + K·R·Kᵀ
+// expanded, as k_chain's Joseph form), after the K_c·M_c term: the history carries V too.
+template <bool J>
+struct AmSharedT {
+  static constexpr int HW = J ? 12 : 8;  // history doubles per (step, slot): K, M (, V)
+  alignas(16) double hkm[kMaxChunk][kAmSlots][HW];  // wave 0's K_c[k] (0..3), M_c[:, k] (4..7)
+                                       // (and V_c[k], 8..11), by lane: a lane's step in 64 (96)
+                                       // contiguous bytes (ds_read_b128 × 4 (6))
   double es[2][8][kAmSlots];          // waves 1 / 2: the even / odd steps' history sums, by lane
-  double jh[kMaxChunk][8];            // the step's landmark: K (0..3) and M (4..7) of every step
+  double jh[kMaxChunk][HW];           // the step's landmark: K (0..3), M (4..7) (, V) of every step
   double jc[18];                      // its block and state (AmCur, x included)
   double pb[kMaxChunk][18];           // fp32 patch: every marker's landmark's final block
   double pp[9];                       // fp32 patch: the final pose block
@@ -178,14 +184,10 @@ __device__ __forceinline__ void put_cur_m(AmCur* blk, int lane, const double (&k
   st_x2<LOC>(r, o + 128, xk[0], xk[1]);
 }
 template <bool LOC>
-__device__ __forceinline__ void put_hist_m(AmHist* blk, int lane, double k0, double k1, double k2,
-                                           double k3, double m0, double m1, double m2, double m3) {
+__device__ __forceinline__ void put_hist_m(AmHist* blk, int lane, const double* h, int hw) {
   const auto r = buf_rsrc(blk, kAmSlots * sizeof(AmHist));
   const int o = lane * static_cast<int>(sizeof(AmHist));
-  st_x2<LOC>(r, o + 0, k0, k1);
-  st_x2<LOC>(r, o + 16, k2, k3);
-  st_x2<LOC>(r, o + 32, m0, m1);
-  st_x2<LOC>(r, o + 48, m2, m3);
+  for (int t = 0; t < hw; t += 2) st_x2<LOC>(r, o + 8 * t, h[t], h[t + 1]);  // (hw: 8 or 12)
 }
 
 __device__ __forceinline__ void put_cur(AmCur* blk, int lane, const double (&kk)[4],
@@ -194,11 +196,10 @@ __device__ __forceinline__ void put_cur(AmCur* blk, int lane, const double (&kk)
   if (loc) put_cur_m<true>(blk, lane, kk, kp, pk, xk);
   else put_cur_m<false>(blk, lane, kk, kp, pk, xk);
 }
-__device__ __forceinline__ void put_hist(AmHist* blk, int lane, double k0, double k1, double k2,
-                                         double k3, double m0, double m1, double m2, double m3,
-                                         bool loc) {
-  if (loc) put_hist_m<true>(blk, lane, k0, k1, k2, k3, m0, m1, m2, m3);
-  else put_hist_m<false>(blk, lane, k0, k1, k2, k3, m0, m1, m2, m3);
+// h: K (4), M (4) and, hw = 12, V (4) — the lane's LDS history row layout
+__device__ __forceinline__ void put_hist(AmHist* blk, int lane, const double* h, int hw, bool loc) {
+  if (loc) put_hist_m<true>(blk, lane, h, hw);
+  else put_hist_m<false>(blk, lane, h, hw);
 }
 
 // The G workgroups of a filter publish their (d, k) for exchange `c` and wait for everyone's:
@@ -318,19 +319,23 @@ __device__ bool same_xcd(unsigned long long* gran, int G, int g, unsigned tag, b
 // acc[4..7] += K_cc[j]·M_cc[:, k] (slam.cpp:264-265's rank-2 terms at (k, j) and (j, k)). The
 // operands (this lane's history, 4 × ds_read_b128, and j's, broadcast) are loaded apart from the
 // fmas so that several terms' reads can be in flight together.
+template <bool J>
 struct HistOps {
-  double2 o[4], jv[4];
+  static constexpr int kV = AmSharedT<J>::HW / 2;
+  double2 o[kV], jv[kV];
 };
-__device__ __forceinline__ void hist_load(const AmShared& sh, int cc, int lane, HistOps& p) {
+template <bool J>
+__device__ __forceinline__ void hist_load(const AmSharedT<J>& sh, int cc, int lane, HistOps<J>& p) {
   const double2* hl = reinterpret_cast<const double2*>(sh.hkm[cc][lane]);
   const double2* jl = reinterpret_cast<const double2*>(sh.jh[cc]);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < HistOps<J>::kV; ++i) {
     p.o[i] = hl[i];
     p.jv[i] = jl[i];
   }
 }
-__device__ __forceinline__ void hist_fma(const HistOps& p, double (&acc)[8]) {
+template <bool J>
+__device__ __forceinline__ void hist_fma(const HistOps<J>& p, double (&acc)[8]) {
   const double ok0 = p.o[0].x, ok1 = p.o[0].y, ok2 = p.o[1].x, ok3 = p.o[1].y;
   const double om0 = p.o[2].x, om1 = p.o[2].y, om2 = p.o[3].x, om3 = p.o[3].y;
   const double jk[4] = {p.jv[0].x, p.jv[0].y, p.jv[1].x, p.jv[1].y};
@@ -343,6 +348,18 @@ __device__ __forceinline__ void hist_fma(const HistOps& p, double (&acc)[8]) {
   acc[5] = fma(jk[1], om3, fma(jk[0], om1, acc[5]));
   acc[6] = fma(jk[3], om2, fma(jk[2], om0, acc[6]));
   acc[7] = fma(jk[3], om3, fma(jk[2], om1, acc[7]));
+  if constexpr (J) {  // + V_cc[k]·K_cc[j]ᵀ at (k, j) and V_cc[j]·K_cc[k]ᵀ at (j, k)
+    const double ov0 = p.o[4].x, ov1 = p.o[4].y, ov2 = p.o[5].x, ov3 = p.o[5].y;
+    const double jv0 = p.jv[4].x, jv1 = p.jv[4].y, jv2 = p.jv[5].x, jv3 = p.jv[5].y;
+    acc[0] = fma(ov1, jk[1], fma(ov0, jk[0], acc[0]));
+    acc[1] = fma(ov1, jk[3], fma(ov0, jk[2], acc[1]));
+    acc[2] = fma(ov3, jk[1], fma(ov2, jk[0], acc[2]));
+    acc[3] = fma(ov3, jk[3], fma(ov2, jk[2], acc[3]));
+    acc[4] = fma(jv1, ok1, fma(jv0, ok0, acc[4]));
+    acc[5] = fma(jv1, ok3, fma(jv0, ok2, acc[5]));
+    acc[6] = fma(jv3, ok1, fma(jv2, ok0, acc[6]));
+    acc[7] = fma(jv3, ok3, fma(jv2, ok2, acc[7]));
+  }
 }
 
 // Workgroup barrier ordering LDS only: the waves' global stores (tables, Kcat / Mcat rows) are not
@@ -357,7 +374,8 @@ __device__ __forceinline__ void lds_barrier() {
 // (sh.jh) — barrier A — this lane's sums over the steps cc < c with cc ≡ par (mod 2) of
 // K_cc[k]·M_cc[:, j] and K_cc[j]·M_cc[:, k] into sh.es[par], read by wave 0 after barrier B. Every
 // wave passes both barriers at every step, whatever the step decides.
-__device__ __forceinline__ void history_helper(AmShared& sh, int m, int k, int lane, int par) {
+template <bool J>
+__device__ __forceinline__ void history_helper(AmSharedT<J>& sh, int m, int k, int lane, int par) {
   for (int c = 0; c < m; ++c) {
     lds_barrier();  // A
     const int j = sh.jl[c];
@@ -365,7 +383,7 @@ __device__ __forceinline__ void history_helper(AmShared& sh, int m, int k, int l
     if (j >= 0) {  // (uniform; the lane k = j ignores its sums)
       int cc = par;
       for (; cc + 6 < c; cc += 8) {  // four terms' reads in flight, then their fmas in order
-        HistOps p0, p1, p2, p3;
+        HistOps<J> p0, p1, p2, p3;
         hist_load(sh, cc, lane, p0);
         hist_load(sh, cc + 2, lane, p1);
         hist_load(sh, cc + 4, lane, p2);
@@ -376,7 +394,7 @@ __device__ __forceinline__ void history_helper(AmShared& sh, int m, int k, int l
         hist_fma(p3, e);
       }
       for (; cc < c; cc += 2) {
-        HistOps p0;
+        HistOps<J> p0;
         hist_load(sh, cc, lane, p0);
         hist_fma(p0, e);
       }
@@ -389,9 +407,10 @@ __device__ __forceinline__ void history_helper(AmShared& sh, int m, int k, int l
 
 }  // namespace
 
-template <typename T>
+template <typename T, bool J>
 __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs B) {
-  __shared__ AmShared sh;
+  __shared__ AmSharedT<J> sh;
+  constexpr int HW = AmSharedT<J>::HW;
   const int G = B.G, fy = blockIdx.y;
   // XCD-local placement (B.xcd): the grid has 8 blocks per workgroup; filter fy's workgroups are
   // the blocks x ≡ fy (mod 8), which round-robin dispatch puts on one XCD (checked: same_xcd)
@@ -531,6 +550,9 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
     double Kk[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, Mk[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
     double Kp[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}}, Mp[2][3] = {{0.0, 0.0, 0.0},
                                                                          {0.0, 0.0, 0.0}};
+    // Joseph: V = Σ·Hᵀ − K·S at the pose (Vp) and at this lane's slot (Vk), and S (Sv)
+    double Vp[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}}, Vk[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    double Sv[4] = {0.0, 0.0, 0.0, 0.0};
     // the new landmark's state (slam.cpp:351-354, the pose before this marker's correction)
     double nx = 0.0, ny = 0.0;
     double rkj[4] = {0.0, 0.0, 0.0, 0.0}, rjk[4] = {0.0, 0.0, 0.0, 0.0};
@@ -545,16 +567,17 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
         }
       }
       // ---- j's block, state and history (one round of sc1 loads), crosses from Σ_in ----
-      double v[3];
+      constexpr int kJL = (18 + HW * (kMaxChunk - 1) + 63) / 64;  // 3 (Joseph: 4)
+      double v[kJL];
       const unsigned jco = static_cast<unsigned>((c * Np + j) * sizeof(AmCur));
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int e = lane + 64 * i;  // 0..17: the AmCur fields; then 8 per earlier step
+      for (int i = 0; i < kJL; ++i) {
+        const int e = lane + 64 * i;  // 0..17: the AmCur fields; then HW per earlier step
         v[i] = 0.0;
         if (G > 1 && e < 18) {
           v[i] = ld_xf64(cur_r, jco + 8 * e);
-        } else if (G > 1 && e < 18 + 8 * c) {
-          const int cc = (e - 18) >> 3, t = (e - 18) & 7;  // AmHist: k[4] then m[4]
+        } else if (G > 1 && e < 18 + HW * c) {
+          const int cc = (e - 18) / HW, t = (e - 18) % HW;  // AmHist: k[4], m[4] (, v[4])
           v[i] = ld_xf64(hist_r, static_cast<unsigned>((cc * Np + j) * sizeof(AmHist) + 8 * t));
         }
       }
@@ -571,10 +594,10 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
       rjk[3] = static_cast<double>(p0[ld + ix + 1]);
       if (G > 1) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
+        for (int i = 0; i < kJL; ++i) {
           const int e = lane + 64 * i;
           if (e < 18) sh.jc[e] = v[i];
-          else if (e < 18 + 8 * c) sh.jh[(e - 18) >> 3][(e - 18) & 7] = v[i];
+          else if (e < 18 + HW * c) sh.jh[(e - 18) / HW][(e - 18) % HW] = v[i];
         }
       } else {  // one workgroup: j's lane holds its block (v_readlane), its history is in LDS
         const int lj = j;
@@ -591,8 +614,8 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
 #pragma unroll
           for (int t = 0; t < 18; ++t) sh.jc[t] = jv[t];
         }
-        for (int e = lane; e < 8 * c; e += 64) {
-          const int cc = e >> 3, t = e & 7;
+        for (int e = lane; e < HW * c; e += 64) {
+          const int cc = e / HW, t = e % HW;
           sh.jh[cc][t] = sh.hkm[cc][lj][t];
         }
       }
@@ -661,7 +684,14 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
         for (int a = 0; a < 3; ++a) {
           Kp[a][0] = Gt[a][0] * Si[0] + Gt[a][1] * Si[2];
           Kp[a][1] = Gt[a][0] * Si[1] + Gt[a][1] * Si[3];
+          if (J) {  // (k_chain's V expression)
+            Vp[a][0] = Gt[a][0] - (Kp[a][0] * Sm[0] + Kp[a][1] * Sm[2]);
+            Vp[a][1] = Gt[a][1] - (Kp[a][0] * Sm[1] + Kp[a][1] * Sm[3]);
+          }
         }
+        if (J)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) Sv[t] = Sm[t];
 #pragma unroll
         for (int b = 0; b < 3; ++b) {  // (H·Σ)[:, pose b]
           const double e1 = P5[1][b] - P5[3][b], e2 = P5[2][b] - P5[4][b];
@@ -699,6 +729,10 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
           const double q1 = fma(g2, d2, fma(g1, d1, -kp[3 * a]));
           Kk[a][0] = q0 * Si[0] + q1 * Si[2];
           Kk[a][1] = q0 * Si[1] + q1 * Si[3];
+          if (J) {
+            Vk[a][0] = q0 - (Kk[a][0] * Sv[0] + Kk[a][1] * Sv[2]);
+            Vk[a][1] = q1 - (Kk[a][0] * Sv[1] + Kk[a][1] * Sv[3]);
+          }
         }
 #pragma unroll
         for (int b = 0; b < 2; ++b) {  // (H·Σ)[:, k_b]
@@ -707,22 +741,29 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
           Mk[1][b] = fma(g2, e2, fma(g1, e1, -pk[b]));
         }
         // ---- Σ ← Σ − K·M on the lane's block and the pose block; x += K·ν (slam.cpp:482-488) ----
+        // (Joseph: then − V·Kᵀ)
         double nkk[4], nkp[6], npk[6];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
+          for (int b = 0; b < 2; ++b) {
             nkk[2 * a + b] = rank2_sub(kk[2 * a + b], Kk[a][0], Kk[a][1], Mk[0][b], Mk[1][b]);
+            if (J) nkk[2 * a + b] = rank2_sub(nkk[2 * a + b], Vk[a][0], Vk[a][1], Kk[b][0], Kk[b][1]);
+          }
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-          for (int b = 0; b < 3; ++b)
+          for (int b = 0; b < 3; ++b) {
             nkp[3 * a + b] = rank2_sub(kp[3 * a + b], Kk[a][0], Kk[a][1], Mp[0][b], Mp[1][b]);
+            if (J) nkp[3 * a + b] = rank2_sub(nkp[3 * a + b], Vk[a][0], Vk[a][1], Kp[b][0], Kp[b][1]);
+          }
 #pragma unroll
         for (int a = 0; a < 3; ++a)
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
+          for (int b = 0; b < 2; ++b) {
             npk[2 * a + b] = rank2_sub(pk[2 * a + b], Kp[a][0], Kp[a][1], Mk[0][b], Mk[1][b]);
+            if (J) npk[2 * a + b] = rank2_sub(npk[2 * a + b], Vp[a][0], Vp[a][1], Kk[b][0], Kk[b][1]);
+          }
 #pragma unroll
         for (int t = 0; t < 4; ++t) kk[t] = nkk[t];
 #pragma unroll
@@ -736,7 +777,10 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
 #pragma unroll
         for (int a = 0; a < 3; ++a)
 #pragma unroll
-          for (int b = 0; b < 3; ++b) nP[a][b] = rank2_sub(Pp[a][b], Kp[a][0], Kp[a][1], Mp[0][b], Mp[1][b]);
+          for (int b = 0; b < 3; ++b) {
+            nP[a][b] = rank2_sub(Pp[a][b], Kp[a][0], Kp[a][1], Mp[0][b], Mp[1][b]);
+            if (J) nP[a][b] = rank2_sub(nP[a][b], Vp[a][0], Vp[a][1], Kp[b][0], Kp[b][1]);
+          }
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
 #pragma unroll
@@ -748,24 +792,31 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
     }
     AM_STAMP(c, 4);
     // ---- the step's factors: history (LDS + write-through table), Kcat / Mcat rows ----
+    // (Joseph: Kcat / Mcat rows 2 + 2m + 2c + e hold V_c / K_c, the V·Kᵀ term's factors)
+    const int jr = 2 + 2 * m + 2 * c;
     {
+      const double hrow[12] = {Kk[0][0], Kk[0][1], Kk[1][0], Kk[1][1], Mk[0][0], Mk[0][1],
+                               Mk[1][0], Mk[1][1], Vk[0][0], Vk[0][1], Vk[1][0], Vk[1][1]};
       double2* hl = reinterpret_cast<double2*>(sh.hkm[c][lane]);
-      hl[0] = make_double2(Kk[0][0], Kk[0][1]);
-      hl[1] = make_double2(Kk[1][0], Kk[1][1]);
-      hl[2] = make_double2(Mk[0][0], Mk[0][1]);
-      hl[3] = make_double2(Mk[1][0], Mk[1][1]);
-    }
-    if (valid) {
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        kc[(2 + 2 * c + e) * ldk + ix] = static_cast<T>(Kk[0][e]);
-        kc[(2 + 2 * c + e) * ldk + ix + 1] = static_cast<T>(Kk[1][e]);
-        mc[(2 + 2 * c + e) * ldk + ix] = static_cast<T>(Mk[e][0]);
-        mc[(2 + 2 * c + e) * ldk + ix + 1] = static_cast<T>(Mk[e][1]);
+      for (int t = 0; t < HW / 2; ++t) hl[t] = make_double2(hrow[2 * t], hrow[2 * t + 1]);
+      if (valid) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          kc[(2 + 2 * c + e) * ldk + ix] = static_cast<T>(Kk[0][e]);
+          kc[(2 + 2 * c + e) * ldk + ix + 1] = static_cast<T>(Kk[1][e]);
+          mc[(2 + 2 * c + e) * ldk + ix] = static_cast<T>(Mk[e][0]);
+          mc[(2 + 2 * c + e) * ldk + ix + 1] = static_cast<T>(Mk[e][1]);
+          if (J) {
+            kc[(jr + e) * ldk + ix] = static_cast<T>(Vk[0][e]);
+            kc[(jr + e) * ldk + ix + 1] = static_cast<T>(Vk[1][e]);
+            mc[(jr + e) * ldk + ix] = static_cast<T>(Kk[0][e]);
+            mc[(jr + e) * ldk + ix + 1] = static_cast<T>(Kk[1][e]);
+          }
+        }
+        if (G > 1 && c + 1 < m)
+          put_hist(hist + static_cast<size_t>(c) * Np + g * kAmSlots, lane, hrow, HW, loc);
       }
-      if (G > 1 && c + 1 < m)
-        put_hist(hist + static_cast<size_t>(c) * Np + g * kAmSlots, lane, Kk[0][0], Kk[0][1],
-                 Kk[1][0], Kk[1][1], Mk[0][0], Mk[0][1], Mk[1][0], Mk[1][1], loc);
     }
     if (g == 0 && lane < 3) {
 #pragma unroll
@@ -774,6 +825,11 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
         const double mv = lane == 0 ? Mp[e][0] : (lane == 1 ? Mp[e][1] : Mp[e][2]);
         kc[(2 + 2 * c + e) * ldk + lane] = static_cast<T>(kv);
         mc[(2 + 2 * c + e) * ldk + lane] = static_cast<T>(mv);
+        if (J) {
+          const double vv = lane == 0 ? Vp[0][e] : (lane == 1 ? Vp[1][e] : Vp[2][e]);
+          kc[(jr + e) * ldk + lane] = static_cast<T>(vv);
+          mc[(jr + e) * ldk + lane] = static_cast<T>(kv);
+        }
       }
     }
     if (valid && G > 1 && c + 1 < m)  // the slot's block and state as step c + 1 starts
@@ -783,7 +839,7 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
   AM_STAMP(kMaxChunk, 1);
   // ---- the chunk's remaining factor rows: the predict's two rank-1 terms (slam.cpp:198, as
   // k_factors writes them), zero rows up to the pass's rank kw ----
-  const int kw = ((2 + 2 * m + 3) / 4) * 4;
+  const int rank = 2 + (J ? 4 : 2) * m, kw = ((rank + 3) / 4) * 4;
   if (valid) {
     // Σ_in[ix + e][0] and Σ_in[0][ix + e] (raw, as slot_block read them)
     const double c0[2] = {static_cast<double>(S[static_cast<size_t>(ix) * ld]),
@@ -795,7 +851,7 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
       kc[1 * ldk + ix + e] = static_cast<T>(first ? -c0[e] : 0.0);  // −(Σ[i][0] + α_i·Σ[0][0])
       mc[0 * ldk + ix + e] = static_cast<T>(first ? r0[e] : 0.0);   // Σ[0][j]
       mc[1 * ldk + ix + e] = static_cast<T>(0.0);                  // α_j = 0
-      for (int rr = 2 + 2 * m; rr < kw; ++rr) {
+      for (int rr = rank; rr < kw; ++rr) {
         kc[rr * ldk + ix + e] = static_cast<T>(0.0);
         mc[rr * ldk + ix + e] = static_cast<T>(0.0);
       }
@@ -811,7 +867,7 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
     kc[1 * ldk + lane] = static_cast<T>(first ? -(rc0 + al * s00) : 0.0);
     mc[0 * ldk + lane] = static_cast<T>(first ? r0c : 0.0);
     mc[1 * ldk + lane] = static_cast<T>(first ? al : 0.0);
-    for (int rr = 2 + 2 * m; rr < kw; ++rr) {
+    for (int rr = rank; rr < kw; ++rr) {
       kc[rr * ldk + lane] = static_cast<T>(0.0);
       mc[rr * ldk + lane] = static_cast<T>(0.0);
     }
@@ -840,9 +896,8 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
   }
   if (G > 1) {  // the final blocks (cur[m]) and every history row published; then workgroup 0 only
     if (valid) {
-      const double* hl = sh.hkm[m - 1][lane];
-      put_hist(hist + static_cast<size_t>(m - 1) * Np + g * kAmSlots, lane, hl[0], hl[1], hl[2],
-               hl[3], hl[4], hl[5], hl[6], hl[7], loc);
+      put_hist(hist + static_cast<size_t>(m - 1) * Np + g * kAmSlots, lane, sh.hkm[m - 1][lane],
+               HW, loc);
       put_cur(cur + static_cast<size_t>(m) * Np + g * kAmSlots, lane, kk, kp, pk, xk, loc);
     }
     double dd = 0.0;
@@ -859,15 +914,15 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   const int nu = 3 + 2 * m;
-  double* ph = &sh.hkm[0][0][0];  // G > 1: [m][m][8] ≤ 2 048 doubles (the region holds 8 192)
+  double* ph = &sh.hkm[0][0][0];  // G > 1: [m][m][HW] ≤ 3 072 doubles (the region holds 64·HW·16)
   if (G > 1) {
     for (int e = lane; e < m * 18; e += 64) {
       const int c = e / 18, t = e - c * 18;
       sh.pb[c][t] = ld_xf64(
           cur_r, static_cast<unsigned>((m * Np + max(sh.jl[c], 0)) * sizeof(AmCur) + 8 * t));
     }
-    for (int e = lane; e < m * m * 8; e += 64) {
-      const int c = e / (8 * m), cc = (e >> 3) % m, t = e & 7;
+    for (int e = lane; e < m * m * HW; e += 64) {
+      const int c = e / (HW * m), cc = (e / HW) % m, t = e % HW;
       const double v = ld_xf64(
           hist_r, static_cast<unsigned>((cc * Np + max(sh.jl[c], 0)) * sizeof(AmHist) + 8 * t));
       __builtin_amdgcn_wave_barrier();  // every lane's loads issued before any lane overwrites
@@ -900,9 +955,9 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  // the history of marker position c's landmark at step cc: K (t < 4) and M (t ≥ 4)
+  // the history of marker position c's landmark at step cc: K (t < 4), M (t < 8), V (t < 12)
   auto hv = [&](int c, int cc, int t) -> double {
-    if (G > 1) return ph[(c * m + cc) * 8 + t];
+    if (G > 1) return ph[(c * m + cc) * HW + t];
     const int j = max(sh.jl[c], 0);
     return sh.hkm[cc][j][t];
   };
@@ -925,9 +980,13 @@ __global__ __launch_bounds__(kAmThreads) void k_assoc_msg(PassArgs<T> A, AmArgs 
     } else {  // two landmarks: Σ_in minus the chunk's rank-2 terms, as the lanes' crosses
       const int ja = 3 + 2 * sh.jl[ca] + ea, jb = 3 + 2 * sh.jl[cb] + eb;
       v = static_cast<double>(S[static_cast<size_t>(ja) * ld + jb]);
-      for (int cc = 0; cc < m; ++cc)
+      for (int cc = 0; cc < m; ++cc) {
         v = rank2_sub(v, hv(ca, cc, 2 * ea), hv(ca, cc, 2 * ea + 1), hv(cb, cc, 4 + eb),
                       hv(cb, cc, 4 + 2 + eb));
+        if (J)  // − V_cc[a]·K_cc[b]ᵀ
+          v = rank2_sub(v, hv(ca, cc, 8 + 2 * ea), hv(ca, cc, 8 + 2 * ea + 1), hv(cb, cc, 2 * eb),
+                        hv(cb, cc, 2 * eb + 1));
+      }
     }
     rec->Pend[a][b] = v;
   }
@@ -961,18 +1020,19 @@ template <typename T>
 hipError_t launch_assoc_msg(const PassArgs<T>& a, const AmArgs& b, int nf, hipStream_t s,
                             hipEvent_t e0, hipEvent_t e1) {
   const dim3 grid(b.xcd ? 8 * b.G : b.G, nf);
+  auto k = a.joseph ? k_assoc_msg<T, true> : k_assoc_msg<T, false>;
   if (e0 && e1)
-    hipExtLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmThreads), 0, s, e0, e1, 0, a, b);
+    hipExtLaunchKernelGGL(k, grid, dim3(kAmThreads), 0, s, e0, e1, 0, a, b);
   else
-    hipLaunchKernelGGL(k_assoc_msg<T>, grid, dim3(kAmThreads), 0, s, a, b);
+    hipLaunchKernelGGL(k, grid, dim3(kAmThreads), 0, s, a, b);
   return hipGetLastError();
 }
 
-int assoc_msg_blocks_per_cu(bool f32) {
+int assoc_msg_blocks_per_cu(bool f32, bool joseph) {
   int nb = 0;
-  const hipError_t e =
-      f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<float>, kAmThreads, 0)
-          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_assoc_msg<double>, kAmThreads, 0);
+  auto occ = [&](auto kern) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kAmThreads, 0); };
+  const hipError_t e = f32 ? (joseph ? occ(k_assoc_msg<float, true>) : occ(k_assoc_msg<float, false>))
+                           : (joseph ? occ(k_assoc_msg<double, true>) : occ(k_assoc_msg<double, false>));
   return e == hipSuccess ? nb : 0;
 }
 

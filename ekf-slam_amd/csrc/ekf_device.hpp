@@ -116,15 +116,16 @@ struct alignas(16) StageRec {
 constexpr int kAmSlots = 64;  // landmark slots per workgroup: one wave, one slot per lane
 // One slot's factors of one correction c: K_c at its rows {kx, ky} (k[2a + e] = K_c[a][e]) and
 // M_c at its columns (m[2e + b] = M_c[e][b]); written by the slot's lane, read by every workgroup
-// of the filter whenever the slot is a later marker's landmark.
+// of the filter whenever the slot is a later marker's landmark. Joseph form: also
+// V_c = Σ_c·Hᵀ − K_c·S_c at its rows (v[2a + e] = V_c[a][e]).
 struct alignas(16) AmHist {
-  double k[4], m[4];
+  double k[4], m[4], v[4];
 };
 // One slot's 16 entries of Σ over {θ, x, y, kx, ky} (kk = Σ[k][k], kp = Σ[k][pose],
 // pk = Σ[pose][k]) and its state, as correction c starts.
 struct alignas(16) AmCur {
   double kk[4], kp[6], pk[6], x[2], pad[2];
 };
-static_assert(sizeof(AmHist) == 64 && sizeof(AmCur) == 160, "AmHist / AmCur 16-byte rows");
+static_assert(sizeof(AmHist) == 96 && sizeof(AmCur) == 160, "AmHist / AmCur 16-byte rows");
 
 }  // namespace ekfslam

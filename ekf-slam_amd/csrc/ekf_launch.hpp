@@ -98,8 +98,9 @@ struct AmArgs {
 // Workgroups of k_assoc_msg one CU holds at once (its LDS bounds it), for the co-residency check:
 // a filter's G workgroups spin on each other, so all of them must fit the bulk stream's CUs
 // (per XCD in the XCD-local placement) at once, or the host routes the markers through the
-// one-marker-per-launch path instead (ekf_api.cpp am_route).
-int assoc_msg_blocks_per_cu(bool f32);
+// one-marker-per-launch path instead (ekf_api.cpp am_route). joseph: the Joseph-form kernel (its
+// history rows are 96 bytes, so its LDS is larger).
+int assoc_msg_blocks_per_cu(bool f32, bool joseph);
 // Scores, decides and corrects every marker of the chunk (slam.cpp:338-488) and writes the chunk's
 // Kcat / Mcat, the new state, t_map_odom and the decisions; the Σ pass then runs as for a known-id
 // chunk. One grid (G, n_filters) of 64-lane workgroups; a filter's G workgroups exchange each

@@ -89,8 +89,10 @@ int ekf_get_path(ekf_t h, int* path);
  *                        landmark slots, a filter's workgroups on one XCD exchanging through its L2;
  *   EKF_ASSOC_CHUNK      the same kernel with the workgroups anywhere (agent-coherent exchange;
  *                        EKF_AM_XCD=0 forces it);
- *   EKF_ASSOC_MARKER     one marker per launch (resident path, Joseph form, EKF_ASSOC_MSG=0, or a
- *                        map whose ceil(N/64) workgroups the CUs cannot hold at once). */
+ *   EKF_ASSOC_MARKER     one marker per launch (resident path, EKF_ASSOC_MSG=0, or a map whose
+ *                        ceil(N/64) workgroups the CUs cannot hold at once).
+ * The Joseph form (ekf_set_joseph) takes the chunk routes too, with its own kernel instantiation;
+ * the route reported is the one in effect for the current form. */
 #define EKF_ASSOC_MARKER 0
 #define EKF_ASSOC_CHUNK 1
 #define EKF_ASSOC_CHUNK_XCD 2

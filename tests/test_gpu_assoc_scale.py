@@ -79,9 +79,9 @@ def _open_map(N, n_map, T, seed=20240317):
     return sc, odom, (x, S, tmo, counter)
 
 
-def _oracle_run(N, sc, odom, ws, gate=2.0):
+def _oracle_run(N, sc, odom, ws, gate=2.0, joseph=False):
     x, S, tmo, cnt = ws
-    ref = orc.OracleEKF(n_landmarks=N, mah_gate=gate)
+    ref = orc.OracleEKF(n_landmarks=N, mah_gate=gate, joseph=joseph)
     ref.set(x, S, tmo, x[:3], cnt)
     out = []
     for t in range(sc.n_warm, sc.n_messages):
@@ -90,10 +90,13 @@ def _oracle_run(N, sc, odom, ws, gate=2.0):
     return ref, out
 
 
-def _gpu_sensor(N, sc, odom, ws, ref_out, dtype=pyekf.EKF_F64, gate=2.0, route=None):
+def _gpu_sensor(N, sc, odom, ws, ref_out, dtype=pyekf.EKF_F64, gate=2.0, route=None,
+                joseph=False):
     """ekf_sensor message by message (decisions read back), every decision against the oracle's."""
     x, S, tmo, cnt = ws
     e = pyekf.EKF(n_landmarks=N, dtype=dtype, mah_gate=gate)
+    if joseph:
+        assert e.set_joseph(True) == pyekf.EKF_OK
     if route is not None:
         assert e.assoc_route == route
     e.set_state(x, S, tmo=tmo, counter=cnt)
@@ -139,6 +142,49 @@ def test_assoc_n1024_decisions(map1024, xcd, dtype, monkeypatch):
     assert cg == cr > ws[3] >= 960
     pt, st, sg = ((POSE_TOL, STATE_TOL, SIGMA_TOL) if dtype == pyekf.EKF_F64 else
                   (F32_POSE_TOL, F32_STATE_TOL, F32_SIGMA_TOL))
+    assert perr < pt
+    assert np.abs(xg - xr).max() < st
+    assert np.abs(Sg - Sr).max() < sg
+
+
+@pytest.fixture(scope="module")
+def map1024_joseph(map1024):
+    """The same drive through the oracle's Joseph form (ekf_oracle.c orc_ekf_set_joseph)."""
+    sc, odom, ws, _, _ = map1024
+    ref, out = _oracle_run(1024, sc, odom, ws, joseph=True)
+    return sc, odom, ws, ref.get(), out
+
+
+@pytest.mark.parametrize("route", ["xcd_local", "agent", "marker"])
+@pytest.mark.parametrize("dtype", [pyekf.EKF_F64, pyekf.EKF_F32], ids=["f64", "f32"])
+def test_assoc_n1024_joseph(map1024_joseph, route, dtype, monkeypatch):
+    """Unknown association in the Joseph form (ekf_set_joseph; slam.cpp:485-486's update as
+    (I − KH)Σ(I − KH)ᵀ + KRKᵀ): whole chunks through k_assoc_msg<T, true> — every step's V_c·K_cᵀ
+    on the lanes' blocks, in the crosses' history sums and as the chunk's Kcat / Mcat rows 2 + 2m..
+    (one rank-(2 + 4m) Σ pass per chunk) — in both exchange transports, and the one-marker route
+    (EKF_ASSOC_MSG=0). Every decision equal to the oracle's Joseph sensor_cb, poses, state and Σ
+    within the fp64 / fp32 tolerances above — the fp32 one-marker route within 5e-6 / 1e-4 / 5e-5:
+    it rounds Σ to fp32 once per marker (160 Σ passes against the chunk route's 10; measured
+    2.3e-6 / 3.5e-5 / 8.1e-6)."""
+    env = {"xcd_local": {"EKF_AM_XCD": "1"}, "agent": {"EKF_AM_XCD": "0"},
+           "marker": {"EKF_ASSOC_MSG": "0"}}[route]
+    _env(monkeypatch, **env)
+    sc, odom, ws, (xr, Sr, _, cr), out = map1024_joseph
+    want = {"xcd_local": pyekf.EKF_ASSOC_CHUNK_XCD, "agent": pyekf.EKF_ASSOC_CHUNK,
+            "marker": pyekf.EKF_ASSOC_MARKER}[route]
+    perr, xg, Sg, cg, n_new, n_old = _gpu_sensor(1024, sc, odom, ws, out, dtype, joseph=True)
+    key = f"n1024_joseph_{'f64' if dtype == pyekf.EKF_F64 else 'f32'}_{route}"
+    ERRORS[key] = {"new": n_new, "associated": n_old, "counter": int(cg), "pose": perr,
+                   "state": float(np.abs(xg - xr).max()), "sigma": float(np.abs(Sg - Sr).max())}
+    e = pyekf.EKF(n_landmarks=1024, dtype=dtype)
+    assert e.set_joseph(True) == pyekf.EKF_OK
+    assert e.assoc_route == want
+    e.close()
+    assert n_new > 0 and n_old > 0
+    assert cg == cr > ws[3] >= 960
+    pt, st, sg = ((POSE_TOL, STATE_TOL, SIGMA_TOL) if dtype == pyekf.EKF_F64 else
+                  (F32_POSE_TOL, F32_STATE_TOL, F32_SIGMA_TOL) if route != "marker" else
+                  (5e-6, 1e-4, 5e-5))
     assert perr < pt
     assert np.abs(xg - xr).max() < st
     assert np.abs(Sg - Sr).max() < sg
