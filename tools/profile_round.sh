@@ -21,6 +21,7 @@ line n256_fp64_s20 --workload n256_fp64 --steps 20 --warmup 5 || exit 3
 line basic_world_s20 --workload basic_world --steps 20 --warmup 5 || exit 3
 line swarm_n256_fp64_s20 --workload swarm_n256_fp64 --steps 20 --warmup 5 || exit 3
 line n1024_fp32_joseph_s20 --workload n1024_fp32_joseph --steps 20 --warmup 5 || exit 3
+line n1024_fp32_assoc_joseph_s20 --workload n1024_fp32_assoc_joseph --steps 20 --warmup 5 || exit 3
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 for w in n1024_fp32 n1024_fp32_assoc; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof_$w -o prof --output-format csv -- \
