@@ -148,6 +148,53 @@ def test_device_device_host_handover_36_filters(monkeypatch, env):
     assert np.abs(ph - pm).max() <= STATE_TOL
 
 
+@pytest.mark.parametrize("env", [{}, {"EKF_SERIAL": "0"}, {"EKF_CU_SPLIT": "8"}],
+                         ids=["36filters_serial", "36filters_events", "36filters_device_epochs"])
+def test_joseph_handover_36_filters(monkeypatch, env):
+    """The hand-over above in the Joseph form (k_chain<T, true> in multi-filter launches, one
+    kJoseph chunk per message planned on the host and on the device): device → device → host spans
+    against the whole drive planned on the host, in each schedule; then a switch to the simple
+    form for the last span (ekf_set_joseph drops every filter's rebuild: its next chunk gathers)
+    against the same switch on the host."""
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pyekf.poison_lds()
+    F = 36
+    scs = [synth.synthetic(96, 30, seed=61 + k) for k in range(4)]
+    spans = [(0, 11), (11, 20), (20, 30)]
+    mixed, sm, pm = _run(scs, 96, F, spans, ["device", "device", "host"], holes=True, joseph=True)
+    for k in ("EKF_SERIAL", "EKF_CU_SPLIT", "EKF_DEVSYNC", "EKF_STAGE"):
+        monkeypatch.delenv(k, raising=False)
+    host, sh, ph = _run(scs, 96, F, [(0, 30)], ["host"], holes=True, joseph=True)
+    assert sm == sh == [0] * F
+    _close(host, mixed, STATE_TOL)
+    assert np.abs(ph - pm).max() <= STATE_TOL
+    # the form switched between spans: Joseph device span, then the simple form on the device
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    full = _inputs(scs, F, 0, 30, True)
+    res = []
+    for kinds in (("device", "device"), ("host", "host")):
+        e = pyekf.EKF(n_landmarks=96, n_filters=F)
+        assert e.set_joseph(True) == pyekf.EKF_OK
+        keep = []
+        for (t0, t1), kind, jos in zip([(0, 15), (15, 30)], kinds, (True, False)):
+            assert e.set_joseph(jos) == pyekf.EKF_OK
+            cnt, ids, act, rel, od = (np.ascontiguousarray(a[t0:t1]) for a in full)
+            if kind == "device":
+                g = _to_gpu((cnt, ids, act, rel, od))
+                keep.append(g)
+                e.replay_device(g[0], g[3], g[4], g[1], g[2])
+            else:
+                e.replay(cnt, rel, od, ids=ids, actions=act)
+        res.append(([e.state(f) for f in range(F)], [e.status(f) for f in range(F)]))
+        e.close()
+    assert res[0][1] == res[1][1] == [0] * F
+    _close(res[1][0], res[0][0], STATE_TOL)
+
+
 def test_posterior_then_device_replay(monkeypatch):
     """ekf_posterior enqueues k_posterior on the main stream, reading its descriptor in the upload
     buffer; with device epochs the next ekf_replay_device plans on the bulk stream and rewrites that
