@@ -554,14 +554,19 @@ def run(args, rank, world, local, backend=None):
     if trace:
         clk.append(("enqueued", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                     time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
-    ekf.sync()  # the library's streams
+    ekf.flush()  # everything planned is submitted (ekf_flush: no wait)
     if trace:
-        clk.append(("lib_synced", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+        clk.append(("flushed", time.clock_gettime_ns(time.CLOCK_MONOTONIC),
                     time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
-    be.sync()   # device-wide (torch.cuda.synchronize on the GPU): nothing may be left running
+    be.sync()   # device-wide (torch.cuda.synchronize on the GPU): waits for the library's streams too
     # this rank's own region (its K messages, enqueue to device-wide sync); the closing barrier
     # aligns the ranks, and reduce_ranks takes the MAX of these over ranks
     elapsed = time.perf_counter() - t0
+    # the library's own sync after the region: its errors / timeouts, and the check that the
+    # device-wide sync left nothing of it running (it returns at once then)
+    t_ls = time.perf_counter()
+    ekf.sync()
+    lib_sync_after_us = (time.perf_counter() - t_ls) * 1e6
     if world > 1:
         dist.barrier()
     if trace:
@@ -695,6 +700,10 @@ def run(args, rank, world, local, backend=None):
             },
         }
         result["roofline"]["end_to_end_frac"] = result["roofline"]["end_to_end"]["frac"]
+        result["region_end"] = {
+            "timed_until": "ekf_flush, then torch.cuda.synchronize (device-wide: the library's "
+                           "streams included)",
+            "library_sync_after_us": lib_sync_after_us}
         if host_rate is not None:
             result["host_inputs"] = host_rate
         if n_asc:

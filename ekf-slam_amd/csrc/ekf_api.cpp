@@ -1515,6 +1515,11 @@ int ekf_posterior(ekf_t h, int f) {
   return submit(h);
 }
 
+int ekf_flush(ekf_t h) {
+  if (!h) return EKF_E_ARG;
+  return flush(h);
+}
+
 int ekf_sync(ekf_t h) {
   if (!h) return EKF_E_ARG;
   // (a device replay's planning state stays on the device: the next host access adopts it)

@@ -33,7 +33,7 @@ EXPORTS = [
     "ekf_set_odom",
     "ekf_fake_sensor", "ekf_sensor", "ekf_batch_sensor", "ekf_replay", "ekf_replay_device",
     "ekf_predict",
-    "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_get_pose",
+    "ekf_correct", "ekf_associate_correct", "ekf_posterior", "ekf_sync", "ekf_flush", "ekf_get_pose",
     "ekf_get_map_odom", "ekf_get_state", "ekf_set_state", "ekf_get_status", "ekf_defer",
     "ekf_set_joseph",
     "ekf_reset", "slam_reset",
@@ -101,6 +101,7 @@ def lib():
             "ekf_associate_correct": (_i, [_vp, _i, _d, _d, _ip, _ip]),
             "ekf_posterior": (_i, [_vp, _i]),
             "ekf_sync": (_i, [_vp]),
+            "ekf_flush": (_i, [_vp]),
             "ekf_get_pose": (_i, [_vp, _i, _vp]),
             "ekf_get_map_odom": (_i, [_vp, _i, _vp]),
             "ekf_get_state": (_i, [_vp, _i, _vp, _vp, _vp]),
@@ -284,6 +285,10 @@ class EKF:
     # state
     def sync(self):
         _check(lib().ekf_sync(self.h), "ekf_sync")
+
+    def flush(self):
+        """Submit what is planned, without waiting (ekf_flush)."""
+        _check(lib().ekf_flush(self.h), "ekf_flush")
 
     def pose(self, f=0):
         p = np.zeros(3)

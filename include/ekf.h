@@ -190,6 +190,10 @@ int ekf_defer(ekf_t h, int on);
  * odometry set by ekf_set_odom is kept. Synchronises. */
 int ekf_reset(ekf_t h, int filter);
 
+/* Submits what the host has planned (deferred callbacks included) without waiting for it: after
+ * it, a device-wide synchronisation (hipDeviceSynchronize) covers all of the handle's work. */
+int ekf_flush(ekf_t h);
+
 /* ---- state access (synchronising) ---- */
 /* Waits for everything submitted; EKF_E_TIMEOUT if a device hand-off timed out since the last
  * report (see EKF_E_TIMEOUT). */

@@ -65,6 +65,9 @@ class OracleSwarm:
     def sync(self):
         pass
 
+    def flush(self):
+        pass
+
     def profile(self, on=True):
         pass
 
