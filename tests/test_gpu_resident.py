@@ -253,6 +253,37 @@ def test_deferred_submission_and_reset(resident, monkeypatch):
 
 
 @pytest.mark.parametrize("resident", [True, False], ids=["resident", "pipeline"])
+def test_flush_then_device_sync(resident, monkeypatch):
+    """ekf_flush submits a deferred plan without waiting (bench.py's timed region ends on it and a
+    device-wide synchronisation): the golden drive planned under ekf_defer, flushed, the device
+    synchronised, equals the same drive submitted message by message, bit for bit."""
+    import torch
+    _env(monkeypatch, resident)
+    sc, g = load_golden("synth16_known")
+    odom = pyekf.odometry(sc)
+    res = []
+    for deferred in (True, False):
+        e = pyekf.EKF(n_landmarks=sc.n_landmarks)
+        if deferred:
+            e.defer(True)
+            e.replay(sc.count[:, None], sc.rel[:, None], odom[:, None], ids=sc.ids[:, None],
+                     actions=sc.actions[:, None])
+            e.flush()
+            torch.cuda.synchronize()
+        else:
+            for t in range(sc.n_messages):
+                e.replay(sc.count[t:t + 1, None], sc.rel[t:t + 1, None], odom[t:t + 1, None],
+                         ids=sc.ids[t:t + 1, None], actions=sc.actions[t:t + 1, None])
+        assert e.status() == 0
+        res.append(e.state())
+        e.close()
+    (xa, Sa, ca), (xb, Sb, cb) = res
+    assert ca == cb
+    assert np.abs(xa - xb).max() < 1e-9 and np.abs(Sa - Sb).max() < 1e-9
+    assert np.abs(xa - g["state"]).max() < TOL
+
+
+@pytest.mark.parametrize("resident", [True, False], ids=["resident", "pipeline"])
 @pytest.mark.parametrize("name", ["basic_world_known", "basic_world_assoc", "synth16_known",
                                   "crowded_assoc"])
 def test_joseph_form_matches_oracle(name, resident, monkeypatch):
