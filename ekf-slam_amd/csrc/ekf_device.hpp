@@ -78,7 +78,7 @@ struct alignas(16) FilterCtl {
 // What the chain kernel (the sequential part of a chunk) hands to the factor kernel: with
 // r(i) = Σ_pred[i][U] and c(j) = Σ_pred[U][j], K_c[i] = r(i)·Z[:, 2c..2c+1] and
 // M_c[:, j] = Y[2c..2c+1, :]·c(j); x_i += r(i)·Zx for rows outside U, xU for rows in U.
-// A Joseph chunk (kJoseph, m ≤ kMaxJoseph) adds V_c[i] = (Σ_c·Hᵀ − K_c·S_c)[i] = r(i)·Z[:, 2m+2c..]
+// A Joseph chunk (kJoseph, m ≤ kMaxJoseph) adds V_c[i] = (Σ_c·Hᵀ − K_c·S_c)[i] = r(i)·Z[:, 32+2c..]
 // (the row factor of the V_c·K_cᵀ term; its column factor is K_c itself).
 struct alignas(16) ChunkRec {
   int m, nu, flags, pad;

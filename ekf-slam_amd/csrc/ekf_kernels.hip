@@ -147,7 +147,7 @@ struct ChainSharedT {
   double Dy[kMaxChunk][4];  // wave 2, step c: D_k = H·K_k[pA_c] (2×2) for k < c
   double KU[kMaxChunk][kMaxU][2];
   double MU[kMaxChunk][kMaxU][2];
-  double Z[kMaxU][ZC + 1];       // K_c[i] = r_0(i)[U] · Z[:, 2c..2c+1] (Joseph: Zv in 2m + 2c..)
+  double Z[kMaxU][ZC + 1];       // K_c[i] = r_0(i)[U] · Z[:, 2c..2c+1] (Joseph: Zv in 32 + 2c..)
   double Y[kZC][kMaxU + 1];      // M_c[:, j] = Y[2c..2c+1, :] · c_0(j)[U]
   double Zx[kMaxU];              // Σ_c Z_c ν_c: x_i += r_0(i)[U] · Zx
   double nu[kMaxChunk][2];
@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(PassArgs<T> A, int nchu
   // Joseph (≤ kMaxJoseph markers per chunk): Σ ← Σ − K_c·M_c − (Σ_cHᵀ − K_c·S_c)·K_cᵀ per step,
   // i.e. (I−KH)Σ(I−KH)ᵀ + K·R·Kᵀ expanded (slam.cpp:264-265's update in Joseph form). Row factor
   // V_c = G_c − K_c·S_c beside K_c, column factor K_cᵀ beside M_c: the record's Z carries V_c's
-  // row map in columns 2m + 2c.., the chain's block gets the term step by step.
+  // row map in columns 32 + 2c.. (kZC + 2c), the chain's block gets the term step by step.
   const bool joseph = J && (d.flags & kJoseph) != 0;
   if ((kDiagBuild && (A.dbg & 16)) && tid < static_cast<int>(sizeof(MsgDesc) / 8))
     dlog_add(A, 0, seq, f, 0, reinterpret_cast<const unsigned long long*>(&d)[tid]);

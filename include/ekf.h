@@ -147,8 +147,7 @@ int ekf_replay(ekf_t h, int assoc, int T, int m_max, const int* counts, const in
 
 /* ekf_replay with known ids (assoc = 0) whose inputs already live in device memory of the
  * handle's GPU (same layouts; d_actions nullable): the descriptors are planned on the GPU (one
- * chunk per message, so m_max <= EKF_MAX_CHUNK; with the Joseph form two chunks of <= 8 markers
- * per message; no resident handle: EKF_E_ARG)
+ * chunk per message, so m_max <= EKF_MAX_CHUNK, in either form; no resident handle: EKF_E_ARG)
  * and no input crosses PCIe. The measurement (range, bearing) of slam.cpp:208-210 is computed on
  * the GPU (correctly rounded sqrt; the bearing's atan2 may differ from glibc's in the last bit).
  * Inputs are not validated on the host: an id outside [0, N) is skipped by the correction and
