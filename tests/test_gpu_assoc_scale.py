@@ -247,12 +247,14 @@ def test_assoc_n1024_near_the_gate(map1024, xcd, monkeypatch):
     assert np.abs(Sg - Sr).max() < SIGMA_TOL
 
 
+@pytest.mark.parametrize("joseph", [False, True], ids=["simple", "joseph"])
 @pytest.mark.parametrize("xcd", ["1", "0"], ids=["xcd_local", "agent"])
-def test_assoc_more_filters_than_resident_workgroups(map1024, xcd, monkeypatch):
+def test_assoc_more_filters_than_resident_workgroups(map1024, xcd, joseph, monkeypatch):
     """64 filters at N = 1024 in one handle: 1 024 workgroups of k_assoc_msg per chunk, more than
     the bulk stream's CUs hold at once, so the host splits the chunk into launches of co-resident
-    filters (a filter's workgroups spin on each other). Every filter ends bit-identical to a
-    one-filter handle, whose state equals the oracle's (fp32 Σ tolerances)."""
+    filters (a filter's workgroups spin on each other; the Joseph kernel's larger LDS makes its
+    groups smaller, `am_group_j`). Every filter ends bit-identical to a one-filter handle, whose
+    state equals the oracle's (fp32 Σ tolerances; the oracle's Joseph mode for the Joseph form)."""
     sc, odom, ws, (xr, Sr, _, cr), _ = map1024
     w, T, F = sc.n_warm, 4, 64
     x, S, tmo, cnt = ws
@@ -260,6 +262,9 @@ def test_assoc_more_filters_than_resident_workgroups(map1024, xcd, monkeypatch):
     rep = lambda a: np.repeat(a[sl, None], F, axis=1)  # noqa: E731
     _env(monkeypatch, EKF_AM_XCD=xcd)
     e = pyekf.EKF(n_landmarks=1024, n_filters=F, dtype=pyekf.EKF_F32)
+    if joseph:
+        assert e.set_joseph(True) == pyekf.EKF_OK
+        assert e.assoc_route != pyekf.EKF_ASSOC_MARKER
     for f in range(F):
         e.set_state(x, S, tmo=tmo, counter=cnt, f=f)
     e.replay(rep(sc.count), rep(sc.rel), rep(odom), ids=None, actions=rep(sc.actions), assoc=True)
@@ -268,6 +273,8 @@ def test_assoc_more_filters_than_resident_workgroups(map1024, xcd, monkeypatch):
     got = [e.state(f) for f in range(0, F, 9)] + [e.state(F - 1)]
     e.close()
     one = pyekf.EKF(n_landmarks=1024, dtype=pyekf.EKF_F32)
+    if joseph:
+        assert one.set_joseph(True) == pyekf.EKF_OK
     one.set_state(x, S, tmo=tmo, counter=cnt)
     one.replay(sc.count[sl, None], sc.rel[sl, None], odom[sl, None], ids=None,
                actions=sc.actions[sl, None], assoc=True)
@@ -277,7 +284,7 @@ def test_assoc_more_filters_than_resident_workgroups(map1024, xcd, monkeypatch):
         assert cg == c1
         np.testing.assert_array_equal(xg, x1)
         np.testing.assert_array_equal(Sg, S1)
-    ref = orc.OracleEKF(n_landmarks=1024)
+    ref = orc.OracleEKF(n_landmarks=1024, joseph=joseph)
     ref.set(x, S, tmo, x[:3], cnt)
     for t in range(w, w + T):
         ref.set_odom(odom[t])
