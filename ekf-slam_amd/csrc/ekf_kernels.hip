@@ -404,11 +404,65 @@ __device__ __noinline__ void chain_wave0(LdsChain<J>* shp, LdsDesc* dp, int pb, 
       }
       if (lane < nu) steplog(lg, c, 2, dbits0(ka) + dbits0(kb) + dbits0(mm0) + dbits0(mm1));
     }
+    // The next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}) after step c−1. Pose columns /
+    // rows: pk / pm (pA ⊃ pose). The nx columns / rows were read one step back (rn / qn, after
+    // step c−2) and get step c−1's rank-2 term here from registers: K_{c−1} of this lane (kp)
+    // and of the nx rows (v_readlane), M_{c−1} of this column (mp) and of the nx columns
+    // (v_readlane) — the writers' expression, operands and order (wave 3's, or this wave's cross
+    // update), so the same bits. Step 0 has kp = mp = 0: rank2_sub(v, 0, 0, 0, 0) = v.
+    double xr[5], xq[5];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      xr[k] = pk[k];
+      xq[k] = pm[k];
+    }
     // wave 3's progress, read here (≈ 1 000 cycles into the step, when it has normally finished
-    // step c − 1) and tested below, after the step's stores: the flag's LDS round trip off the
-    // chain's path
+    // step c − 1) and tested below: the flag's LDS round trip off the chain's path
     const int pd_early = __hip_atomic_load(&sh.pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    {  // K_{c−1} and M_{c−1} of the nx rows / columns: broadcast LDS reads of what step c−1
+       // stored (the stored values are the registers' values; two reads instead of 8 readlanes)
+      const int l0 = more ? nx : 0, cp = c > 0 ? c - 1 : 0;
+      const double mqx = sh.MU[cp][l0][0], mqy = sh.MU[cp][l0][1];
+      const double mq2x = sh.MU[cp][l0 + 1][0], mq2y = sh.MU[cp][l0 + 1][1];
+      const double kqx = sh.KU[cp][l0][0], kqy = sh.KU[cp][l0][1];
+      const double kq2x = sh.KU[cp][l0 + 1][0], kq2y = sh.KU[cp][l0 + 1][1];
+      // step 0: kp = mp = 0 and the (stale, finite) reads multiply zeros: rank2_sub returns v
+      xr[3] = rank2_sub(rn[0], kp0, kp1, mqx, mqy);
+      xr[4] = rank2_sub(rn[1], kp0, kp1, mq2x, mq2y);
+      xq[3] = rank2_sub(qn[0], kqx, kqy, mp0, mp1);
+      xq[4] = rank2_sub(qn[1], kq2x, kq2y, mp0, mp1);
+      if (J) {  // − V_{c−1}·K_{c−1}ᵀ (step 0: vp = kp = 0)
+        const int cj = min(cp, JM - 1);
+        const double vqx = sh.VU[cj][l0][0], vqy = sh.VU[cj][l0][1];
+        const double vq2x = sh.VU[cj][l0 + 1][0], vq2y = sh.VU[cj][l0 + 1][1];
+        xr[3] = rank2_sub(xr[3], vp0, vp1, kqx, kqy);
+        xr[4] = rank2_sub(xr[4], vp0, vp1, kq2x, kq2y);
+        xq[3] = rank2_sub(xq[3], vqx, vqy, kp0, kp1);
+        xq[4] = rank2_sub(xq[4], vq2x, vq2y, kp0, kp1);
+      }
+    }
     EKF_STAMP(66 + 8 * c);
+    // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's
+    // cross, before this step's cross update writes its Bx rows (wave 3 writes these entries for
+    // step c only after the publish below, whose release waits for the reads)
+    if (c + 2 < m) {
+      // the LDS serves this wave's accesses in order, and wave 3 stored its entries before the
+      // flag: once a flag value ≥ c has been read, later reads see the entries (a compiler fence
+      // keeps them after the test)
+      if (__builtin_amdgcn_readfirstlane(pd_early) < c) lds_wait_ge3(&sh.pdone, c);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        rn[j] = sh.P[pb][lr][nx + 2 + j];
+        qn[j] = sh.P[pb][nx + 2 + j][lr];
+      }
+    }
+    if (kDiagBuild && lg && lane < nu) {
+      unsigned long long v = 0;
+      for (int k = 0; k < 5; ++k) v += dbits0(xr[k]) + dbits0(xq[k]);
+      steplog(lg, c, 3, v);
+      steplog(lg, c, 7, dbits0(rn[0]) + dbits0(rn[1]) + dbits0(qn[0]) + dbits0(qn[1]));
+    }
     const int jx = __builtin_amdgcn_readlane(ul, pj);  // sh.u[pj] (ul = sh.u[lane], pj < kMaxU)
     EKF_STAMP(67 + 8 * c);
     const double K0 = ka * Si[0] + kb * Si[2];  // K = Σ·Hᵀ·S⁻¹
@@ -463,23 +517,6 @@ __device__ __noinline__ void chain_wave0(LdsChain<J>* shp, LdsDesc* dp, int pb, 
       sh.nu[c][0] = nv0;
       sh.nu[c][1] = nv1;
     }
-    // the cross after next (nx + 2): read once wave 3 has applied step c−1 outside this step's
-    // cross, and before the publish below (wave 3 writes these entries for step c only after it)
-    // and this step's cross update. The values are used one step on (rn / qn), so the reads are
-    // not waited for here; the flag, loaded ≈ 1 000 cycles back, has landed.
-    double rn2[2] = {rn[0], rn[1]}, qn2[2] = {qn[0], qn[1]};
-    if (c + 2 < m) {
-      // the LDS serves this wave's accesses in order, and wave 3 stored its entries before the
-      // flag: once a flag value ≥ c has been read, later reads see the entries (a compiler fence
-      // keeps them after the test)
-      if (__builtin_amdgcn_readfirstlane(pd_early) < c) lds_wait_ge3(&sh.pdone, c);
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        rn2[j] = sh.P[pb][lr][nx + 2 + j];
-        qn2[j] = sh.P[pb][nx + 2 + j][lr];
-      }
-    }
     lds_publish3(&sh.pub, c + 1);
     EKF_STAMP(68 + 8 * c);
     if (more) {
@@ -501,50 +538,7 @@ __device__ __noinline__ void chain_wave0(LdsChain<J>* shp, LdsDesc* dp, int pb, 
           vx1[k] = sh.VU[cj][l][1];
         }
       }
-      // The next marker's cross operands (Bx = {0, 1, 2, nx, nx+1}) after step c−1. Pose columns
-      // / rows: pk / pm (pA ⊃ pose). The nx columns / rows were read one step back (rn / qn, after
-      // step c−2) and get step c−1's rank-2 term here from registers: K_{c−1} of this lane (kp)
-      // and of the nx rows, M_{c−1} of this column (mp) and of the nx columns — the writers'
-      // expression, operands and order (wave 3's, or this wave's cross update), so the same bits.
-      // Step 0 has kp = mp = 0: rank2_sub(v, 0, 0, m0, m1) = v for finite m. The nx rows' K / M
-      // of step c−1 are broadcast LDS reads issued here and used after geometry(c + 1), which
-      // hides their round trip (they sat on the step's path before round 6).
-      double xr[5], xq[5];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        xr[k] = pk[k];
-        xq[k] = pm[k];
-      }
-      const int cp = c > 0 ? c - 1 : 0;
-      const double mqx = sh.MU[cp][nx][0], mqy = sh.MU[cp][nx][1];
-      const double mq2x = sh.MU[cp][nx + 1][0], mq2y = sh.MU[cp][nx + 1][1];
-      const double kqx = sh.KU[cp][nx][0], kqy = sh.KU[cp][nx][1];
-      const double kq2x = sh.KU[cp][nx + 1][0], kq2y = sh.KU[cp][nx + 1][1];
-      double vqx = 0.0, vqy = 0.0, vq2x = 0.0, vq2y = 0.0;
-      if (J) {
-        const int cj = min(cp, JM - 1);
-        vqx = sh.VU[cj][nx][0];
-        vqy = sh.VU[cj][nx][1];
-        vq2x = sh.VU[cj][nx + 1][0];
-        vq2y = sh.VU[cj][nx + 1][1];
-      }
       geometry(c + 1);
-      xr[3] = rank2_sub(rn[0], kp0, kp1, mqx, mqy);
-      xr[4] = rank2_sub(rn[1], kp0, kp1, mq2x, mq2y);
-      xq[3] = rank2_sub(qn[0], kqx, kqy, mp0, mp1);
-      xq[4] = rank2_sub(qn[1], kq2x, kq2y, mp0, mp1);
-      if (J) {  // − V_{c−1}·K_{c−1}ᵀ (step 0: vp = kp = 0)
-        xr[3] = rank2_sub(xr[3], vp0, vp1, kqx, kqy);
-        xr[4] = rank2_sub(xr[4], vp0, vp1, kq2x, kq2y);
-        xq[3] = rank2_sub(xq[3], vqx, vqy, kp0, kp1);
-        xq[4] = rank2_sub(xq[4], vq2x, vq2y, kp0, kp1);
-      }
-      if (kDiagBuild && lg && lane < nu) {
-        unsigned long long v = 0;
-        for (int k = 0; k < 5; ++k) v += dbits0(xr[k]) + dbits0(xq[k]);
-        steplog(lg, c, 3, v);
-        steplog(lg, c, 7, dbits0(rn2[0]) + dbits0(rn2[1]) + dbits0(qn2[0]) + dbits0(qn2[1]));
-      }
       // wave 3's step c−1 writes outside this step's cross must land before this cross update
       // overwrites the nx columns / rows (waited for above already when c + 2 < m)
       if (c + 2 >= m && __builtin_amdgcn_readfirstlane(pd_early) < c) lds_wait_ge3(&sh.pdone, c);
@@ -581,10 +575,6 @@ __device__ __noinline__ void chain_wave0(LdsChain<J>* shp, LdsDesc* dp, int pb, 
       vp0 = V0;
       vp1 = V1;
     }
-    rn[0] = rn2[0];
-    rn[1] = rn2[1];
-    qn[0] = qn2[0];
-    qn[1] = qn2[1];
     EKF_STAMP(70 + 8 * c);
   }
 }
