@@ -89,6 +89,44 @@ def test_n256_fp64_populated_against_oracle():
     assert np.abs(S - o["sigma"]).max() < SIGMA_TOL
 
 
+@pytest.mark.parametrize("joseph", [False, True], ids=["simple", "joseph"])
+@pytest.mark.parametrize("dtype", [pyekf.EKF_F64, pyekf.EKF_F32], ids=["f64", "f32"])
+def test_n256_survey_against_oracle(dtype, joseph):
+    """configs[1]'s survey at N = 256 (every landmark's first sighting against the 1e7 prior,
+    slam.cpp:213-216, plus the circle messages) in both update forms, one chunk of ≤16 markers per
+    Joseph message, against the oracle in the same form. fp64 at the fp64 tolerances above. fp32
+    keeps Σ in fp32 and takes each first sighting's block from the chain's fp64 patch (the V·Kᵀ
+    terms too in the Joseph form, k_chain's pend block); its pose bound is 5e-6 here, not 1e-6:
+    measured (r6) simple 9.4e-7 / 3.2e-6 / 2.8e-5 and Joseph 1.9e-6 / 5.8e-6 / 1.4e-5 (pose /
+    state / Σ) — 256 first sightings each round Σ's new rows once, on top of the 40-pass walk the
+    1e-6 bound is sized for."""
+    sc = synth.populated(256, 25)
+    odom = pyekf.odometry(sc)
+    e = pyekf.EKF(n_landmarks=256, dtype=dtype)
+    assert e.path == pyekf.EKF_PATH_PIPELINE
+    assert e.set_joseph(joseph) == pyekf.EKF_OK
+    _replay(e, slice(0, sc.n_messages), sc, odom)
+    x, S, cnt = e.state()
+    assert e.status() == 0
+    e.close()
+    ref = orc.OracleEKF(n_landmarks=256, joseph=joseph)
+    for t in range(sc.n_messages):
+        ref.set_odom(odom[t])
+        c = int(sc.count[t])
+        ref.fake_sensor_cb(sc.ids[t, :c], sc.actions[t, :c], sc.rel[t, :c])
+    xr, Sr, _, cr = ref.get()
+    assert cnt == cr and _initialised(x) == 256
+    key = (f"n256_survey_{'joseph' if joseph else 'simple'}_"
+           + ("f64" if dtype == pyekf.EKF_F64 else "f32"))
+    ERRORS[key] = {"pose": float(np.abs(x[:3] - xr[:3]).max()),
+                   "state": float(np.abs(x - xr).max()), "sigma": float(np.abs(S - Sr).max())}
+    pt, st, sg = ((POSE_TOL, STATE_TOL, SIGMA_TOL) if dtype == pyekf.EKF_F64 else
+                  (5e-6, F32_STATE_TOL, F32_SIGMA_TOL))
+    assert np.abs(x[:3] - xr[:3]).max() < pt
+    assert np.abs(x - xr).max() < st
+    assert np.abs(S - Sr).max() < sg
+
+
 @pytest.fixture(scope="module")
 def n1024():
     """configs[2]'s map: the fp64 survey on the GPU (every landmark sighted), and its state."""
